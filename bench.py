@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""CTR-forward examples/sec on a Criteo-shaped synthetic batch (BASELINE.json metric).
+
+Workload (default, configs[1]): DeepFM fp32, 39 fields / 1M vocab / k = 16, fcDims 400,400,400,
+over a 1M-row synthetic set whose ids and table live in HBM before timing starts.  One step =
+one forward (gather + first order + FM + tower + sigmoid) over one batch of --batch rows of that
+set; successive steps walk the set.  --workload xdeepfm runs configs[2] (CIN 200,200,200).
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank owns a replica of the 1M-row
+table and its own batches (replicas only: the V = 1M forward has no exchange step), so
+scaling is weak and value = sum of all ranks' examples / max rank time.
+
+Prints ONE JSON line (rank 0).  Only the cpu_baseline leg touches oracle/ (the checker).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "recommendation-models_amd"))
+
+F, K, V = 39, 16, 1_000_000
+FC = [400, 400, 400]
+CIN = [200, 200, 200]
+ROWS = 1 << 20  # the "1M-row synthetic" set
+SEED_IDS, SEED_TAB, SEED_MATS = 0x5EED2026, 0x7AB1E, 0x3A75
+
+# Peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+PEAK_FP32_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["deepfm", "xdeepfm"], default="deepfm")
+    ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def stage_work(workload, stage, B):
+    """Algorithmic work of one launch of a stage: ('flop'|'byte', amount)."""
+    D = F * K
+    if stage == "encoder_fm":  # ids + w + emb rows + y  (2,812 B / example)
+        return "byte", B * (F * 4 + F * 4 + F * K * 4 + 4)
+    if stage == "first_order":
+        return "byte", B * (F * 4 + F * 4 + 4)
+    if stage == "tower_layer1":
+        return "flop", 2.0 * B * D * FC[0]
+    if stage == "tower_layer2":
+        return "flop", 2.0 * B * FC[0] * FC[1]
+    if stage == "tower_layer3":
+        return "flop", 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
+    if stage.startswith("cin_layer"):
+        idx = {"cin_layer1": 0, "cin_layer2": 1, "cin_layer3+": 2}[stage]
+        hp = F if idx == 0 else CIN[idx - 1]
+        return "flop", 2.0 * B * K * F * hp * CIN[idx]
+    return None, 0
+
+
+def cpu_baseline(workload, budget_s, threads):
+    """Oracle (C restatement, OpenMP) on the host cores: examples/s on bounded batches."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ctypes as oc
+    if workload == "deepfm":
+        om = oc.make_model(oc.DEEPFM, F, K, fc=tuple(FC))
+        B = 4096
+    else:
+        om = oc.make_model(oc.XDEEPFM, F, K, fc=tuple(FC), cin=tuple(CIN))
+        B = 16
+    mats = oc.init_mats(om, SEED_MATS)
+    # the table slice for the rows we touch is regenerated on the host (same generator)
+    done, t_tot, row0 = 0, 0.0, 0
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    while t_tot < budget_s:
+        ids = oc.gen_ids(SEED_IDS, row0, B, F, V).astype(np.int64)
+        w, e = oc.gather(wt, et, 1, ids)  # makeWeights / makeEmbeddings are part of the CPU path
+        index = np.repeat(np.arange(B, dtype=np.int64), F)
+        t0 = time.perf_counter()
+        w, e = oc.gather(wt, et, 1, ids)
+        oc.forward(om, B, index, np.array([0.01], np.float32), w, e, mats, 0, threads)
+        t_tot += time.perf_counter() - t0
+        done += B
+        row0 += B
+    return {"value": done / t_tot, "unit": "examples/s", "cores": threads, "kind": "port",
+            "sample": "%d rows (%d batches of %d) of the same synthetic %s workload, fp32 oracle "
+                      "(oracle/rmx_oracle.c, OpenMP, gather + forward), %.1f s"
+                      % (done, done // B, B, workload, t_tot)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # CPU (gloo) barrier / max only: the GPU work is librmx
+        dist.init_process_group("gloo")
+    import rmx
+
+    B = args.batch or (65536 if args.workload == "deepfm" else 2048)
+    rmx.set_device(local)
+    ctx = rmx.default_context()
+    stream = ctx.stream
+    if args.workload == "deepfm":
+        model = rmx.DeepFM(V, F, K, FC, ctx=ctx)
+    else:
+        model = rmx.XDeepFM(V, F, K, FC, CIN, ctx=ctx)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    model.setMats(model.initMats(SEED_MATS))
+    model.setBias(0.01)
+    nrows = max(ROWS, B)
+    ids = rmx.DeviceArray(ctx, nrows * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, rank * nrows, nrows, F, V, ids)
+    out = rmx.DeviceArray(ctx, nrows, np.float32)
+    ctx.sync()
+    nb = nrows // B
+    import ctypes
+
+    views = [(ids.view(s * B * F, B * F), out.view(s * B, B)) for s in range(nb)]
+
+    def step(i):
+        ids_v, out_v = views[i % nb]
+        model.forward_ids(table, B, ids_v, out_v, stream)
+
+    for i in range(args.warmup):
+        step(i)
+    ctx.sync()
+
+    ev0, ev1 = ctypes.c_void_p(), ctypes.c_void_p()
+    rmx._lib.lib.rmx_event_create(ctypes.byref(ev0))
+    rmx._lib.lib.rmx_event_create(ctypes.byref(ev1))
+    if dist:
+        dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    rmx._lib.lib.rmx_event_record(ev0, stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    rmx._lib.lib.rmx_event_record(ev1, stream)
+    ctx.sync()
+    wall = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    ms = ctypes.c_float()
+    rmx._lib.lib.rmx_event_elapsed_ms(ev0, ev1, ctypes.byref(ms))
+    t_rank = max(wall, ms.value / 1e3)
+    if dist:
+        import torch
+        t = torch.tensor([t_rank], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_rank = float(t.item())
+    value = world * B * args.steps / t_rank
+
+    # ---- roofline of the dominant kernel: per-stage HIP events on the launch stream ----
+    model.set_timing(True)
+    nt = max(5, min(args.steps, 20))
+    for i in range(nt):
+        step(i)
+    ctx.sync()
+    stages, calls = model.get_timing()
+    model.set_timing(False)
+    per_stage = {}
+    for name, tot in stages.items():
+        avg_ms = tot / max(calls, 1)
+        kind, work = stage_work(args.workload, name, B)
+        ent = {"avg_ms": round(avg_ms, 4)}
+        if kind == "flop":
+            ent["tflops"] = round(work / (avg_ms / 1e3) / 1e12, 2)
+            ent["frac_fp32_peak"] = round(ent["tflops"] / PEAK_FP32_TFLOPS, 3)
+        elif kind == "byte":
+            ent["gbs"] = round(work / (avg_ms / 1e3) / 1e9, 1)
+            ent["frac_hbm_peak"] = round(ent["gbs"] / PEAK_HBM_GBS, 3)
+        per_stage[name] = ent
+    dom = max(stages.items(), key=lambda kv: kv[1])[0]
+    kind, work = stage_work(args.workload, dom, B)
+    avg_s = stages[dom] / max(calls, 1) / 1e3
+    if kind == "byte":
+        roof = {"bound": "hbm", "achieved": round(work / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+    else:
+        roof = {"bound": "mfma", "achieved": round(work / avg_s / 1e12, 2), "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["traffic"] = None
+    roof["kernel"] = dom
+    roof["algorithmic_per_launch"] = work
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(args.workload, args.cpu_seconds, threads)
+
+    if rank == 0:
+        line = {
+            "metric": "CTR-forward examples/sec on Criteo-shaped batch, DeepFM & xDeepFM, 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "examples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_rank * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (splitmix64 Criteo-shaped ids, U(-0.05,0.05) table, Xavier mats)",
+            "config": {"workload": "%s_fp32_F39_V1M_k16_fc400x3%s_B%d" % (
+                args.workload, "_cin200x3" if args.workload == "xdeepfm" else "", B),
+                "global_batch": world * B, "rows_per_gpu_set": nrows, "parallelism": "replicas%d" % world},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stages": per_stage,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,170 @@
+/*
+ * rmx.h -- C ABI of the MI355X-native CTR forward path (librmx.so).
+ *
+ * Drop-in boundary for the reference's model plugin API
+ *   abstract class RecModel           yr/model/RecModel.scala:6-127
+ * and for the Angel-PS pull + gather that feeds it
+ *   ParRecModel.pull* / make*         yr/model/ParRecModel.scala:165-199, 270-306
+ * (paths relative to /root/reference/src/main/scala/, yr/ = io/yaochi/recommendation/).
+ *
+ * Two levels, one library:
+ *   L-A  rmx_forward():      the exact RecModel.forward(batchSize, batch, bias, weights,
+ *                            embeddings, embeddingDim, mats, matSizes[, fields]) contract
+ *                            on host buffers (RecModel.scala:37-63, buildParams :146-155).
+ *   L-B  rmx_forward_ids():  device-resident table + device ids (replaces pull* + make*).
+ *
+ * Conventions: every entry point returns 0 (RMX_OK) or a negative RMX_E_* code and
+ * sets a thread-local message readable with rmx_last_error().  Calls on one model
+ * are synchronous on return for L-A; L-B calls are asynchronous on the given
+ * stream (pass NULL for the model's own stream; rmx_stream_sync to wait).
+ * No torch types: plain pointers and sizes only.
+ */
+#ifndef RMX_H
+#define RMX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMX_ABI_VERSION 1
+
+/* Status codes -- mirror the reference's failure modes. */
+#define RMX_OK 0
+#define RMX_E_INVALID (-1)  /* bad argument / missing params-map key (NoSuchElementException)      */
+#define RMX_E_INDEX (-2)    /* COO row index >= batchSize: bnn/Scatter.scala:29-30 require(...)       */
+#define RMX_E_SHAPE (-3)    /* nnz*k != B*F*k: BigDL Reshape(B, F, k) size mismatch                    */
+#define RMX_E_TYPE (-4)     /* unknown model type / array missing for the RecModelType (MatchError)    */
+#define RMX_E_HIP (-5)      /* HIP runtime error                                                      */
+#define RMX_E_NOMEM (-6)    /* device allocation failed                                               */
+#define RMX_E_MATS (-7)     /* mats length / matSizes disagree with getMatsSize                       */
+
+/* Model kinds: yr/model/{lr,deepfm,xdeepfm,dcn,pnn,dnn}/ */
+#define RMX_MODEL_LR 0
+#define RMX_MODEL_DEEPFM 1
+#define RMX_MODEL_XDEEPFM 2
+#define RMX_MODEL_DCN 3
+#define RMX_MODEL_PNN 4
+#define RMX_MODEL_DNN 5
+
+/* RecModelType (yr/model/RecModelType.scala:5-8). */
+#define RMX_BIAS_WEIGHT 0
+#define RMX_BIAS_WEIGHT_EMBEDDING 1
+#define RMX_BIAS_WEIGHT_EMBEDDING_MATS 2
+#define RMX_BIAS_WEIGHT_EMBEDDING_MATS_FIELD 3
+
+/* Embedding-table host layouts for rmx_table_upload. */
+#define RMX_LAYOUT_K_MAJOR 0   /* reference Angel PS layout: k rows x V columns (ParRecModel.scala:95-101) */
+#define RMX_LAYOUT_ROW_MAJOR 1 /* V rows x k columns                                                      */
+
+typedef struct rmx_ctx rmx_ctx;
+typedef struct rmx_model rmx_model;
+typedef struct rmx_table rmx_table;
+
+/* ------------------------------------------------------------------ misc -- */
+const char* rmx_last_error(void);
+int rmx_abi_version(void);
+
+/* ------------------------------------------------------------- context ---- */
+/* One context per (process, GPU).  Owns a HIP stream. */
+int rmx_ctx_create(int device, rmx_ctx** out);
+int rmx_ctx_destroy(rmx_ctx* ctx);
+void* rmx_ctx_stream(rmx_ctx* ctx);            /* hipStream_t of the context */
+int rmx_stream_sync(void* stream);             /* hipStreamSynchronize        */
+
+/* Device memory helpers for L-B callers (ids / outputs resident in HBM). */
+int rmx_malloc(rmx_ctx* ctx, size_t bytes, void** dptr);
+int rmx_free(rmx_ctx* ctx, void* dptr);
+int rmx_memcpy_htod(rmx_ctx* ctx, void* dst, const void* src, size_t bytes);
+int rmx_memcpy_dtoh(rmx_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* HIP events on the given stream (NULL = context stream), for in-band timing. */
+int rmx_event_create(void** ev);
+int rmx_event_destroy(void* ev);
+int rmx_event_record(void* ev, void* stream);
+int rmx_event_elapsed_ms(void* start, void* stop, float* ms);
+
+/* ---------------------------------------------------------------- model ---- */
+/* new LR(inputDim)                                       yr/model/lr/LR.scala:10
+ * new DeepFM(inputDim, nFields, embeddingDim, fcDims)      yr/model/deepfm/DeepFM.scala:10
+ * new XDeepFM(inputDim, nFields, embeddingDim, fcDims, cinDims)  yr/model/xdeepfm/XDeepFM.scala:10
+ * new DCN(inputDim, nFields, embeddingDim, crossDepth, fcDims)   yr/model/dcn/DCN.scala:10
+ * new PNN(inputDim, nFields, embeddingDim, fcDims)         yr/model/pnn/PNN.scala:10
+ * new DNN(inputDim, nFields, embeddingDim, fcDims)         yr/model/dnn/DNN.scala:10
+ * Unused arguments are ignored (pass 0 / NULL).  ctx may be NULL for a host-only model that
+ * answers the metadata calls (getMatsSize ...) without a GPU. */
+int rmx_model_create(rmx_ctx* ctx, int type, int64_t input_dim, int n_fields, int embedding_dim,
+                     const int32_t* fc_dims, int n_fc, const int32_t* cin_dims, int n_cin,
+                     int cross_depth, rmx_model** out);
+int rmx_model_destroy(rmx_model* m);
+/* RecModel.getType / getMatsSize / getInputDim / getEmbeddingDim (RecModel.scala:7, :121-125).
+ * getMatsSize writes up to cap ints into sizes and stores the full count in *n. */
+int rmx_model_get_type(const rmx_model* m);
+int rmx_model_get_mats_size(const rmx_model* m, int32_t* sizes, int cap, int* n);
+int64_t rmx_model_mats_len(const rmx_model* m);
+int64_t rmx_model_get_input_dim(const rmx_model* m);
+int rmx_model_get_embedding_dim(const rmx_model* m);
+
+/* L-A: RecModel.forward(batchSize, batch: CooLongFloatMatrix, bias, weights, embeddings,
+ *        embeddingDim, mats, matSizes[, fields]): Array[Float]     RecModel.scala:9-63
+ * index[nnz] = batch.getRowIndices, feats[nnz] = batch.getColIndices (unused by the math,
+ * as in the reference), weights[nnz] / embedding[nnz*k] already gathered by the caller,
+ * bias[1].  Arrays not used by the model's RecModelType may be NULL.  fields is ignored
+ * (no reference model reads it).  out[batch_size] receives sigmoid probabilities. */
+int rmx_forward(rmx_model* m, int32_t batch_size, int64_t nnz, const int64_t* index,
+                const int64_t* feats, const float* bias, const float* weights,
+                const float* embedding, int32_t embedding_dim, const float* mats,
+                const int32_t* mat_sizes, int32_t n_sizes, const int64_t* fields, float* out);
+
+/* Deterministic synthetic mats (Xavier-uniform weights, U(-0.01, 0.01) biases), bit-identical
+ * to oracle/orc_init_mats; works on host-only models (ctx == NULL). */
+int rmx_model_init_mats(const rmx_model* m, uint64_t seed, float* mats);
+
+/* L-B parameters: load mats (getMatsSize layout) and the global bias once, on device. */
+int rmx_model_set_mats(rmx_model* m, const float* mats, int64_t n_mats);
+int rmx_model_set_bias(rmx_model* m, float bias);
+
+/* ---------------------------------------------------------------- table ---- */
+/* HBM-resident first-order weights + embedding table (replaces the Angel PS rows
+ * "weights" and "embedding", ParRecModel.scala:74-105).  Stored row-major [V][k]. */
+int rmx_table_create(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, rmx_table** out);
+int rmx_table_destroy(rmx_table* t);
+/* Host upload; weights may be NULL, embedding may be NULL (then left as is). */
+int rmx_table_upload(rmx_table* t, const float* weights, const float* embedding, int layout);
+/* Deterministic synthetic fill, bit-identical to oracle/orc_gen_table (U(-0.05, 0.05)). */
+int rmx_table_fill_synthetic(rmx_table* t, uint64_t seed);
+int64_t rmx_table_rows(const rmx_table* t);
+/* Device pointers of the table (for debugging/parity only). */
+int rmx_table_device_ptrs(const rmx_table* t, float** d_weights, float** d_embedding);
+
+/* Synthetic field-partitioned ids into device memory, bit-identical to orc_gen_ids. */
+int rmx_gen_ids(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,
+                int64_t num_rows, int32_t* d_ids, void* stream);
+
+/* Debug gather: d_w[n] = weights[ids[n]], d_emb[n*k+j] = emb[ids[n]][j] (makeWeights /
+ * makeEmbeddings, ParRecModel.scala:279-306).  Bit-exact copies. */
+int rmx_gather(const rmx_table* t, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
+               void* stream);
+
+/* L-B forward: d_ids[batch * nFields] (int32, device), d_out[batch] (device).
+ * Requires rmx_model_set_mats / rmx_model_set_bias first.  Asynchronous on stream. */
+int rmx_forward_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32_t* d_ids,
+                    float* d_out, void* stream);
+
+/* Per-stage timing of the last rmx_forward_ids calls made with timing enabled:
+ * names/ms of up to cap stages (kernels) accumulated since enable. */
+int rmx_model_set_timing(rmx_model* m, int enable);
+int rmx_model_get_timing(rmx_model* m, char* names, int name_stride, float* ms, int cap, int* n,
+                         int* calls);
+
+/* Encoder-only launch (gather + first order + FM for DeepFM, first order otherwise):
+ * d_y[batch] = y1 + y2 (DeepFM) / y1.  Used to measure the HBM-bound encoder alone. */
+int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32_t* d_ids,
+                    float* d_y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

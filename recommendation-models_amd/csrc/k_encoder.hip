@@ -1,0 +1,309 @@
+// k_encoder.hip -- HBM-bound encoder kernels: embedding / first-order gather, Scatter
+// first order, FM second order, plus the synthetic id / table generators.
+//
+//   gather        yr/model/ParRecModel.scala:279-306 (makeWeights / makeEmbeddings)
+//   first order   bnn/Scatter.scala:17-36 (ascending-n accumulation into row index[n])
+//   FM            yr/model/encoder/SecondOrderEncoder.scala:19-34
+//                 y2 = 0.5 * (sum_j[(sum_f e)^2 - sum_f e^2] / k)
+//
+// The FM / first-order sums follow the oracle's order exactly (sequential over f, then
+// sequential over j) with FMA contraction disabled, so y1 and y2 are bit-identical to
+// oracle/rmx_oracle.c.
+#include "rmx_internal.hpp"
+
+namespace rmx {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+// mode: 0 = y = y1 (first order), 1 = y = y1 + y2 (DeepFM), 2 = prob = sigmoid(y1 + beta) (LR),
+//       3 = y += y2 (L-A path with an irregular COO index: y already holds y1 from the CSR kernel).
+// k = 16 fast path: 4 lanes per sample (one float4 of the 64-B row each), 16 samples per wave,
+// all F row loads of a lane independent (ids staged in registers first).
+template <int MODE>
+__global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* __restrict__ ids,
+                                                          const float* __restrict__ table,
+                                                          const float* __restrict__ wtab, int F,
+                                                          float* __restrict__ y, float beta,
+                                                          float* __restrict__ prob) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int s = lane >> 2, c = lane & 3;
+  const int b = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + s;
+  const bool valid = b < M;
+  const int bb = valid ? b : 0;
+  float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = s4;
+  float y1 = 0.f;
+  const float4* emb4 = reinterpret_cast<const float4*>(table);
+  int f = 0;
+  for (; f + 8 <= F; f += 8) {
+    int id[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) id[u] = ids ? ids[(int64_t)bb * F + f + u] : bb * F + f + u;
+    float4 v[8];
+    float wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (MODE == 1 || MODE == 3) v[u] = emb4[(int64_t)id[u] * 4 + c];
+      if (MODE != 3) wv[u] = (c == 0) ? wtab[id[u]] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (MODE == 1 || MODE == 3) {
+        s4.x += v[u].x; s4.y += v[u].y; s4.z += v[u].z; s4.w += v[u].w;
+        q4.x += v[u].x * v[u].x; q4.y += v[u].y * v[u].y;
+        q4.z += v[u].z * v[u].z; q4.w += v[u].w * v[u].w;
+      }
+      if (MODE != 3) y1 += wv[u];
+    }
+  }
+  for (; f < F; ++f) {
+    const int id = ids ? ids[(int64_t)bb * F + f] : bb * F + f;
+    if (MODE == 1 || MODE == 3) {
+      const float4 v = emb4[(int64_t)id * 4 + c];
+      s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+      q4.x += v.x * v.x; q4.y += v.y * v.y; q4.z += v.z * v.z; q4.w += v.w * v.w;
+    }
+    if (MODE != 3 && c == 0) y1 += wtab[id];
+  }
+  float y2 = 0.f;
+  if (MODE == 1 || MODE == 3) {
+    // d_j = s_j^2 - q_j for j = 4c..4c+3; lane c==0 sums j = 0..15 sequentially.
+    float d0 = s4.x * s4.x - q4.x, d1 = s4.y * s4.y - q4.y;
+    float d2 = s4.z * s4.z - q4.z, d3 = s4.w * s4.w - q4.w;
+    float acc = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int src = (lane & ~3) | cc;
+      acc += __shfl(d0, src);
+      acc += __shfl(d1, src);
+      acc += __shfl(d2, src);
+      acc += __shfl(d3, src);
+    }
+    y2 = 0.5f * (acc / 16.0f);
+  }
+  if (!valid || c != 0) return;
+  if (MODE == 0) y[b] = y1;
+  if (MODE == 1) y[b] = y1 + y2;
+  if (MODE == 2) prob[b] = 1.0f / (1.0f + expf(-(y1 + beta)));
+  if (MODE == 3) y[b] = y[b] + y2;  // y holds y1 from the CSR kernel
+}
+
+// Generic-k fallback: one thread per sample, oracle order.
+template <int MODE>
+__global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32_t* __restrict__ ids,
+                                                              const float* __restrict__ table,
+                                                              const float* __restrict__ wtab, int F,
+                                                              int k, float* __restrict__ y,
+                                                              float beta, float* __restrict__ prob) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= M) return;
+  float y1 = 0.f, y2 = 0.f;
+  if (MODE != 3)
+    for (int f = 0; f < F; ++f) {
+      const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
+      y1 += wtab[id];
+    }
+  if (MODE == 1 || MODE == 3) {
+    float acc = 0.f;
+    for (int j = 0; j < k; ++j) {
+      float s = 0.f, q = 0.f;
+      for (int f = 0; f < F; ++f) {
+        const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
+        const float v = table[(int64_t)id * k + j];
+        s += v;
+        q += v * v;
+      }
+      acc += s * s - q;
+    }
+    y2 = 0.5f * (acc / (float)k);
+  }
+  if (MODE == 0) y[b] = y1;
+  if (MODE == 1) y[b] = y1 + y2;
+  if (MODE == 2) prob[b] = 1.0f / (1.0f + expf(-(y1 + beta)));
+  if (MODE == 3) y[b] = y[b] + y2;
+}
+
+int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const float* table,
+                   const float* wtab, int F, int k, float* y, const float* beta, float* prob) {
+  if (M <= 0) return RMX_OK;
+  const float bt = beta ? *beta : 0.f;
+  if (k == 16) {
+    dim3 grid((M + 63) / 64);
+    switch (mode) {
+      case 0: hipLaunchKernelGGL(encoder_k16_kernel<0>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      case 1: hipLaunchKernelGGL(encoder_k16_kernel<1>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      case 2: hipLaunchKernelGGL(encoder_k16_kernel<2>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      default: hipLaunchKernelGGL(encoder_k16_kernel<3>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+    }
+  } else {
+    dim3 grid((M + 255) / 256);
+    switch (mode) {
+      case 0: hipLaunchKernelGGL(encoder_generic_kernel<0>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      case 1: hipLaunchKernelGGL(encoder_generic_kernel<1>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      case 2: hipLaunchKernelGGL(encoder_generic_kernel<2>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      default: hipLaunchKernelGGL(encoder_generic_kernel<3>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+    }
+  }
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// Scatter first order over a CSR view of a (row-sorted) COO index: y[b] = sum of w[n] for
+// n in [row_ptr[b], row_ptr[b+1]) in ascending n (bnn/Scatter.scala:25-33 order).
+__global__ __launch_bounds__(256) void first_order_csr_kernel(int B, const int64_t* __restrict__ row_ptr,
+                                                              const float* __restrict__ w,
+                                                              float* __restrict__ y) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float acc = 0.f;
+  for (int64_t n = row_ptr[b]; n < row_ptr[b + 1]; ++n) acc += w[n];
+  y[b] = acc;
+}
+
+int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y) {
+  if (B <= 0) return RMX_OK;
+  hipLaunchKernelGGL(first_order_csr_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, row_ptr, w, y);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+__global__ void sigmoid_out_kernel(int B, const float* __restrict__ y, float beta, float* __restrict__ out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) out[b] = 1.0f / (1.0f + expf(-(y[b] + beta)));
+}
+
+int launch_sigmoid_out(hipStream_t s, int B, const float* y, float beta, float* out) {
+  if (B <= 0) return RMX_OK;
+  hipLaunchKernelGGL(sigmoid_out_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, y, beta, out);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// ----------------------------------------------------------- synthetic ------
+__global__ void gen_ids_kernel(uint64_t seed, int64_t row0, int B, int F, uint64_t per, int32_t* ids) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * F) return;
+  const int64_t b = i / F;
+  const int f = (int)(i - b * F);
+  const uint64_t cnt = (uint64_t)(row0 + b) * (uint64_t)F + (uint64_t)f;
+  ids[i] = (int32_t)((uint64_t)f * per + splitmix64(seed ^ cnt) % per);
+}
+
+int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids) {
+  const int64_t n = (int64_t)B * F;
+  if (n <= 0) return RMX_OK;
+  hipLaunchKernelGGL(gen_ids_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, seed, row0, B,
+                     F, (uint64_t)(V / F), ids);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+__global__ void fill_table_kernel(uint64_t seed, int64_t V, int k, float scale, float* w, float* emb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = V * (k + 1);
+  if (i >= tot) return;
+  const int64_t id = i / (k + 1);
+  const int j = (int)(i - id * (k + 1));
+  const uint64_t h = splitmix64(seed ^ (uint64_t)i);  // i == id*(k+1) + j
+  const float v = (float)((int32_t)(h >> 40) - 8388608) * scale;
+  if (j < k) emb[id * k + j] = v;
+  else w[id] = v;
+}
+
+int launch_fill_table(hipStream_t s, uint64_t seed, int64_t V, int k, float* w, float* emb) {
+  const int64_t tot = V * (k + 1);
+  const float scale = 0.05f * (1.0f / 8388608.0f);
+  hipLaunchKernelGGL(fill_table_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, V, k,
+                     scale, w, emb);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+__global__ void gather_kernel(int64_t n, const int32_t* __restrict__ ids, const float* __restrict__ wtab,
+                              const float* __restrict__ emb, int k, float* __restrict__ w_out,
+                              float* __restrict__ e_out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * (k + 1)) return;
+  const int64_t r = i / (k + 1);
+  const int j = (int)(i - r * (k + 1));
+  const int id = ids[r];
+  if (j < k) {
+    if (e_out) e_out[r * k + j] = emb[(int64_t)id * k + j];
+  } else if (w_out) {
+    w_out[r] = wtab[id];
+  }
+}
+
+int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const float* wtab, const float* emb,
+                  int k, float* w_out, float* e_out) {
+  if (n <= 0) return RMX_OK;
+  const int64_t tot = n * (k + 1);
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, ids, wtab, emb,
+                     k, w_out, e_out);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// W (out x in row-major at mats + w_off) -> [Kpad/16][Npad][16]; bias -> [Npad].
+// (PNN: columns >= K1 come from a second matrix at w_off2; bias_mode 2 broadcasts one scalar.)
+__global__ void pack_linear_kernel(const float* __restrict__ mats, int64_t w_off, int64_t w_off2, int K1,
+                                   int64_t b_off, int bias_mode, int K, int N, int Kpad, int Npad,
+                                   float* __restrict__ Wp, float* __restrict__ bp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)Kpad * Npad;
+  if (i < tot) {
+    const int kk = (int)(i & 15);
+    const int64_t rest = i >> 4;
+    const int n = (int)(rest % Npad);
+    const int c = (int)(rest / Npad);
+    const int kx = c * 16 + kk;
+    float v = 0.f;
+    if (n < N && kx < K) {
+      if (K1 < 0) v = mats[w_off + (int64_t)n * K + kx];
+      else if (kx < K1) v = mats[w_off + (int64_t)n * K1 + kx];
+      else v = mats[w_off2 + (int64_t)n * (K - K1) + (kx - K1)];
+    }
+    Wp[i] = v;
+  }
+  if (i < Npad) {
+    float v = 0.f;
+    if (i < N && bias_mode == 1) v = mats[b_off + i];
+    if (i < N && bias_mode == 2) v = mats[b_off];
+    bp[i] = v;
+  }
+}
+
+int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L) {
+  const int64_t tot = (int64_t)L.Kpad * L.Npad;
+  const int64_t n = tot > L.Npad ? tot : L.Npad;
+  hipLaunchKernelGGL(pack_linear_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mats_dev,
+                     L.w_off, L.w_off2, L.K1, L.b_off, L.b_off >= 0 ? L.bias_mode : 0, L.K, L.N, L.Kpad,
+                     L.Npad, L.W, L.b);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+__global__ void transpose_kmajor_kernel(const float* __restrict__ src, int64_t V, int k, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= V * k) return;
+  const int64_t id = i / k;
+  const int j = (int)(i - id * k);
+  dst[i] = src[(int64_t)j * V + id];
+}
+
+int launch_transpose_kmajor(hipStream_t s, const float* src_kv, int64_t V, int k, float* dst_vk) {
+  const int64_t tot = V * k;
+  if (tot <= 0) return RMX_OK;
+  hipLaunchKernelGGL(transpose_kmajor_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src_kv, V,
+                     k, dst_vk);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+}  // namespace rmx

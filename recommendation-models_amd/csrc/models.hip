@@ -1,0 +1,694 @@
+// models.hip -- per-model layer plans, parameter packing and forward sequences.
+//
+// Layer plans restate the mats offset walk of each reference model (LayerUtil.buildLinear at
+// running offsets, util/LayerUtil.scala:7-40):
+//   DeepFM / DNN  model/encoder/HigherOrderEncoder.scala:48-58
+//   xDeepFM       model/xdeepfm/CINEncoder.scala:123-176
+//   DCN           model/dcn/CrossEncoder.scala:134-185
+//   PNN           model/pnn/ProductEncoder.scala:72-108 + PNN.scala:78 (tail tower, start = end offset)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rmx_models.hpp"
+
+namespace rmx {
+
+namespace {
+
+void push(std::vector<int32_t>& v, int a, int b) {
+  v.push_back(a);
+  v.push_back(b);
+}
+
+// getMatsSize of each model (see oracle/rmx_oracle.c for the per-model file:line).
+std::vector<int32_t> mats_sizes(const rmx_model& m) {
+  std::vector<int32_t> s;
+  const int F = m.F, k = m.k, D = F * k;
+  switch (m.type) {
+    case RMX_MODEL_LR:
+      break;
+    case RMX_MODEL_DEEPFM:
+    case RMX_MODEL_DNN: {
+      int prev = D;
+      for (size_t i = 0; i <= m.fc.size(); ++i) {
+        const int cur = i < m.fc.size() ? m.fc[i] : 1;
+        push(s, prev, cur);
+        push(s, cur, 1);
+        prev = cur;
+      }
+      break;
+    }
+    case RMX_MODEL_XDEEPFM: {
+      int prev = D;
+      for (int d : m.fc) {
+        push(s, prev, d);
+        push(s, d, 1);
+        prev = d;
+      }
+      int hp = F, sum = 0;
+      for (int h : m.cin) {
+        push(s, F * hp, h);
+        push(s, h, 1);
+        hp = h;
+        sum += h;
+      }
+      push(s, sum + m.fc.back(), 1);
+      break;
+    }
+    case RMX_MODEL_DCN: {
+      for (int i = 0; i < m.cross_depth; ++i) push(s, D, 1);
+      for (int i = 0; i < m.cross_depth; ++i) push(s, 1, 1);
+      int prev = D;
+      for (int d : m.fc) {
+        push(s, prev, d);
+        push(s, d, 1);
+        prev = d;
+      }
+      push(s, D + m.fc.back(), 1);
+      break;
+    }
+    case RMX_MODEL_PNN: {
+      const int P = F * (F - 1) / 2;
+      push(s, D, m.fc[0]);
+      push(s, P, m.fc[0]);
+      push(s, 1, 1);
+      int prev = m.fc[0];
+      for (size_t i = 1; i <= m.fc.size(); ++i) {
+        const int cur = i < m.fc.size() ? m.fc[i] : 1;
+        push(s, prev, cur);
+        push(s, cur, 1);
+        prev = cur;
+      }
+      break;
+    }
+  }
+  return s;
+}
+
+uint64_t splitmix64_h(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+float unif_h(uint64_t h, float a) {
+  const float scale = a * (1.0f / 8388608.0f);
+  return (float)((int32_t)(h >> 40) - 8388608) * scale;
+}
+
+DenseLayer make_layer(int K, int N, int64_t w_off, int64_t b_off) {
+  DenseLayer L;
+  L.K = K;
+  L.N = N;
+  L.Kpad = round_up(K, kChunk);
+  L.Npad = round_up(N, 80);
+  L.w_off = w_off;
+  L.b_off = b_off;
+  return L;
+}
+
+int dev_alloc(float** p, size_t n) {
+  if (hipMalloc(p, sizeof(float) * (n ? n : 1)) != hipSuccess) {
+    set_error("out of device memory (" + std::to_string(n * 4) + " bytes)");
+    return RMX_E_NOMEM;
+  }
+  return RMX_OK;
+}
+
+template <class T>
+void dev_free(T*& p) {
+  if (p) hipFree(p);
+  p = nullptr;
+}
+
+bool needs_gather_x(const rmx_model& m) { return m.k % 4 != 0; }
+
+}  // namespace
+
+int model_build(rmx_model& m) {
+  const int t = m.type;
+  if (t != RMX_MODEL_LR) {
+    if (m.F <= 0 || m.k <= 0) {
+      set_error("nFields and embeddingDim must be positive");
+      return RMX_E_INVALID;
+    }
+    // "".split(",").map(_.toInt) throws in the reference (example/*LocalExample.scala:21)
+    if (m.fc.empty()) {
+      set_error("fcDims must not be empty");
+      return RMX_E_INVALID;
+    }
+    for (int d : m.fc)
+      if (d <= 0) {
+        set_error("fcDims must be positive");
+        return RMX_E_INVALID;
+      }
+  }
+  if (t == RMX_MODEL_XDEEPFM) {
+    if (m.cin.empty()) {
+      set_error("cinDims must not be empty");
+      return RMX_E_INVALID;
+    }
+    if (m.k != 16) {
+      set_error("xDeepFM CIN kernel supports embeddingDim 16 only");
+      return RMX_E_INVALID;
+    }
+    for (int h : m.cin)
+      if (h <= 0 || h > 256) {
+        set_error("cinDims must be in [1, 256]");
+        return RMX_E_INVALID;
+      }
+  }
+  if (t == RMX_MODEL_DCN) {
+    if (m.cross_depth <= 0) {  // (0 until 0).map(...).reduce throws (DCN.scala:17-19)
+      set_error("crossDepth must be positive");
+      return RMX_E_INVALID;
+    }
+    if (m.F * m.k > 1024) {
+      set_error("DCN cross kernel supports nFields*embeddingDim <= 1024");
+      return RMX_E_INVALID;
+    }
+  }
+  if (t == RMX_MODEL_PNN && m.F < 2) {
+    set_error("PNN needs at least two fields");
+    return RMX_E_INVALID;
+  }
+  m.sizes = mats_sizes(m);
+  m.mats_len = 0;
+  for (size_t i = 0; i < m.sizes.size(); i += 2) m.mats_len += (int64_t)m.sizes[i] * m.sizes[i + 1];
+
+  const int D = m.F * m.k;
+  int64_t off = 0;
+  switch (t) {
+    case RMX_MODEL_LR:
+      break;
+    case RMX_MODEL_DEEPFM:
+    case RMX_MODEL_DNN: {
+      int prev = D;
+      for (int d : m.fc) {
+        m.layers.push_back(make_layer(prev, d, off, off + (int64_t)prev * d));
+        off += (int64_t)prev * d + d;
+        prev = d;
+      }
+      m.wo_off = off;
+      m.bo_off = off + prev;
+      m.has_bo = true;
+      break;
+    }
+    case RMX_MODEL_XDEEPFM: {
+      int prev = D;
+      for (int d : m.fc) {
+        m.layers.push_back(make_layer(prev, d, off, off + (int64_t)prev * d));
+        off += (int64_t)prev * d + d;
+        prev = d;
+      }
+      int hp = m.F, sum = 0;
+      for (int h : m.cin) {
+        CinLayer c;
+        c.Hp = hp;
+        c.Hp_pad = round_up(hp, 16);
+        c.H = h;
+        c.Npad = round_up(h, 16);
+        c.w_off = off;
+        c.b_off = off + (int64_t)m.F * hp * h;
+        off += (int64_t)m.F * hp * h + h;
+        hp = h;
+        sum += h;
+        m.cin_layers.push_back(c);
+      }
+      m.wo_cin_off = off;
+      int base = 0;
+      for (auto& c : m.cin_layers) {
+        c.wo_off = off + base;
+        base += c.H;
+      }
+      m.wo_off = off + sum;  // the DNN slice of the output Linear (no bias)
+      m.has_bo = false;
+      break;
+    }
+    case RMX_MODEL_DCN: {
+      m.cross_w_off = 0;
+      m.cross_b_off = (int64_t)m.cross_depth * D;
+      off = m.cross_b_off + m.cross_depth;
+      int prev = D;
+      for (int d : m.fc) {
+        m.layers.push_back(make_layer(prev, d, off, off + (int64_t)prev * d));
+        off += (int64_t)prev * d + d;
+        prev = d;
+      }
+      m.wo_x_off = off;
+      m.wo_off = off + D;
+      m.has_bo = false;
+      break;
+    }
+    case RMX_MODEL_PNN: {
+      const int P = m.F * (m.F - 1) / 2, D1 = m.fc[0];
+      DenseLayer L0 = make_layer(D + P, D1, 0, (int64_t)D * D1 + (int64_t)P * D1);
+      L0.K1 = D;
+      L0.w_off2 = (int64_t)D * D1;
+      L0.bias_mode = 2;
+      m.layers.push_back(L0);
+      off = (int64_t)D * D1 + (int64_t)P * D1 + 1;
+      int prev = D1;
+      for (size_t i = 1; i < m.fc.size(); ++i) {
+        const int d = m.fc[i];
+        m.layers.push_back(make_layer(prev, d, off, off + (int64_t)prev * d));
+        off += (int64_t)prev * d + d;
+        prev = d;
+      }
+      m.wo_off = off;
+      m.bo_off = off + prev;
+      m.has_bo = true;
+      break;
+    }
+  }
+  if (t != RMX_MODEL_LR && off + (m.has_bo ? m.layers.back().N + 1 : 0) != m.mats_len &&
+      t != RMX_MODEL_XDEEPFM && t != RMX_MODEL_DCN) {
+    set_error("internal: mats layout mismatch");
+    return RMX_E_INVALID;
+  }
+  for (auto& L : m.layers)
+    if (L.Npad > 640 && &L == &m.layers.back()) {
+      set_error("last hidden layer wider than 640 is not supported");
+      return RMX_E_INVALID;
+    }
+
+  if (!m.ctx) return RMX_OK;  // host-only model: metadata only
+  // device parameter buffers
+  RMX_HIP(hipSetDevice(m.ctx->device));
+  int st = RMX_OK;
+  if (m.mats_len > 0 && (st = dev_alloc(&m.mats_dev, m.mats_len))) return st;
+  for (auto& L : m.layers) {
+    if ((st = dev_alloc(&L.W, (size_t)L.Kpad * L.Npad))) return st;
+    if ((st = dev_alloc(&L.b, L.Npad))) return st;
+  }
+  if (!m.layers.empty()) {
+    if ((st = dev_alloc(&m.wo, m.layers.back().Npad))) return st;
+  }
+  for (auto& c : m.cin_layers) {
+    if ((st = dev_alloc(&c.W, (size_t)c.Hp_pad * m.F * c.Npad))) return st;
+    if ((st = dev_alloc(&c.b, c.Npad))) return st;
+    if ((st = dev_alloc(&c.wo, c.Npad))) return st;
+  }
+  if (t == RMX_MODEL_DCN) {
+    if ((st = dev_alloc(&m.cross_w, (size_t)m.cross_depth * D))) return st;
+    if ((st = dev_alloc(&m.cross_b, m.cross_depth))) return st;
+    if ((st = dev_alloc(&m.wo_x, D))) return st;
+  }
+  if (t == RMX_MODEL_PNN) {
+    // pairs (i < j) lexicographic: ProductEncoder.calcIndices (ProductEncoder.scala:110-120)
+    std::vector<int32_t> pr;
+    for (int i = 0; i < m.F; ++i)
+      for (int j = i + 1; j < m.F; ++j) {
+        pr.push_back(i);
+        pr.push_back(j);
+      }
+    if (hipMalloc(&m.pairs, sizeof(int32_t) * pr.size()) != hipSuccess) {
+      set_error("out of device memory");
+      return RMX_E_NOMEM;
+    }
+    RMX_HIP(hipMemcpy(m.pairs, pr.data(), sizeof(int32_t) * pr.size(), hipMemcpyHostToDevice));
+  }
+  return RMX_OK;
+}
+
+// Synthetic parameters: Xavier-uniform +-sqrt(6/(in+out)) for every Linear
+// weight, U(-0.01, 0.01) for biases, value i of a segment from splitmix64(seed ^ (offset + i)).
+// Which getMatsSize pairs are biases follows the LayerUtil calls of each model.
+void model_init_mats(const rmx_model& m, uint64_t seed, float* mats) {
+  int64_t off = 0;
+  const int npairs = (int)m.sizes.size() / 2;
+  for (int pair = 0; pair < npairs; ++pair) {
+    const int a = m.sizes[2 * pair], b = m.sizes[2 * pair + 1];
+    const int64_t len = (int64_t)a * b;
+    bool is_bias = false;
+    switch (m.type) {
+      case RMX_MODEL_DEEPFM:
+      case RMX_MODEL_DNN:
+        is_bias = pair & 1;
+        break;
+      case RMX_MODEL_XDEEPFM: {
+        const int nfc = 2 * (int)m.fc.size(), ncin = 2 * (int)m.cin.size();
+        is_bias = pair < nfc + ncin ? ((pair < nfc ? pair : pair - nfc) & 1) : false;
+        break;
+      }
+      case RMX_MODEL_DCN: {
+        const int L = m.cross_depth, nfc = 2 * (int)m.fc.size();
+        if (pair < L) is_bias = false;
+        else if (pair < 2 * L) is_bias = true;
+        else if (pair < 2 * L + nfc) is_bias = (pair - 2 * L) & 1;
+        break;
+      }
+      case RMX_MODEL_PNN:
+        is_bias = pair < 2 ? false : (pair == 2 ? true : ((pair - 3) & 1));
+        break;
+      default:
+        break;
+    }
+    const float amp = is_bias ? 0.01f : sqrtf(6.0f / (float)(a + b));
+    for (int64_t i = 0; i < len; ++i) mats[off + i] = unif_h(splitmix64_h(seed ^ (uint64_t)(off + i)), amp);
+    off += len;
+  }
+}
+
+void model_release(rmx_model& m) {
+  if (!m.ctx) return;
+  hipSetDevice(m.ctx->device);
+  hipStreamSynchronize(m.ctx->stream);
+  dev_free(m.mats_dev);
+  for (auto& L : m.layers) {
+    dev_free(L.W);
+    dev_free(L.b);
+  }
+  dev_free(m.wo);
+  for (auto& c : m.cin_layers) {
+    dev_free(c.W);
+    dev_free(c.b);
+    dev_free(c.wo);
+  }
+  dev_free(m.cross_w);
+  dev_free(m.cross_b);
+  dev_free(m.wo_x);
+  dev_free(m.pairs);
+  dev_free(m.h[0]);
+  dev_free(m.h[1]);
+  dev_free(m.y12);
+  dev_free(m.pre2);
+  dev_free(m.xbuf);
+  dev_free(m.ubuf[0]);
+  dev_free(m.ubuf[1]);
+  dev_free(m.rowdot);
+  dev_free(m.la_E);
+  dev_free(m.la_w);
+  dev_free(m.la_rowptr);
+  dev_free(m.la_out);
+  for (auto& p : m.pending) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : m.ev_pool) hipEventDestroy(e);
+}
+
+__global__ void copy_slice_kernel(const float* __restrict__ src, int n, int npad, float* __restrict__ dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < npad) dst[i] = i < n ? src[i] : 0.f;
+}
+
+static int copy_slice(hipStream_t s, const float* src, int n, int npad, float* dst) {
+  if (npad <= 0) return RMX_OK;
+  hipLaunchKernelGGL(copy_slice_kernel, dim3((npad + 255) / 256), dim3(256), 0, s, src, n, npad, dst);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// Upload mats and pack every layer on the device (the reference rebuilds its BigDL modules
+// from mats on every call: LayerUtil.scala:13-19; here it is one H2D copy + pack kernels).
+int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
+  hipStream_t s = m.ctx->stream;
+  RMX_HIP(hipSetDevice(m.ctx->device));
+  if (m.mats_len > 0)
+    RMX_HIP(hipMemcpyAsync(m.mats_dev, host_mats, sizeof(float) * m.mats_len, hipMemcpyHostToDevice, s));
+  int st;
+  for (auto& L : m.layers)
+    if ((st = launch_pack_linear(s, m.mats_dev, L))) return st;
+  if (!m.layers.empty()) {
+    const auto& last = m.layers.back();
+    if ((st = copy_slice(s, m.mats_dev + m.wo_off, last.N, last.Npad, m.wo))) return st;
+    m.bo = m.has_bo ? host_mats[m.bo_off] : 0.f;
+  }
+  for (auto& c : m.cin_layers) {
+    if ((st = launch_pack_cin(s, m.mats_dev, m.F, c))) return st;
+    if ((st = copy_slice(s, m.mats_dev + c.b_off, c.H, c.Npad, c.b))) return st;
+    if ((st = copy_slice(s, m.mats_dev + c.wo_off, c.H, c.Npad, c.wo))) return st;
+  }
+  if (m.type == RMX_MODEL_DCN) {
+    const int D = m.F * m.k;
+    RMX_HIP(hipMemcpyAsync(m.cross_w, m.mats_dev + m.cross_w_off, sizeof(float) * m.cross_depth * D,
+                           hipMemcpyDeviceToDevice, s));
+    RMX_HIP(hipMemcpyAsync(m.cross_b, m.mats_dev + m.cross_b_off, sizeof(float) * m.cross_depth,
+                           hipMemcpyDeviceToDevice, s));
+    RMX_HIP(hipMemcpyAsync(m.wo_x, m.mats_dev + m.wo_x_off, sizeof(float) * D, hipMemcpyDeviceToDevice, s));
+  }
+  if (sync) RMX_HIP(hipStreamSynchronize(s));
+  m.params_ready = true;
+  return RMX_OK;
+}
+
+namespace {
+
+int ensure_ws(rmx_model& m, int B) {
+  if (B <= m.ws_B) return RMX_OK;
+  RMX_HIP(hipStreamSynchronize(m.ctx->stream));
+  dev_free(m.h[0]);
+  dev_free(m.h[1]);
+  dev_free(m.y12);
+  dev_free(m.pre2);
+  dev_free(m.xbuf);
+  dev_free(m.ubuf[0]);
+  dev_free(m.ubuf[1]);
+  dev_free(m.rowdot);
+  int st;
+  int maxN = 16;
+  for (auto& L : m.layers) maxN = std::max(maxN, L.Npad);
+  if (!m.layers.empty()) {
+    if ((st = dev_alloc(&m.h[0], (size_t)B * maxN))) return st;
+    if ((st = dev_alloc(&m.h[1], (size_t)B * maxN))) return st;
+  }
+  if ((st = dev_alloc(&m.y12, B))) return st;
+  if ((st = dev_alloc(&m.pre2, B))) return st;
+  if (m.type == RMX_MODEL_PNN || (m.type != RMX_MODEL_LR && needs_gather_x(m))) {
+    if ((st = dev_alloc(&m.xbuf, (size_t)B * m.layers[0].Kpad))) return st;
+  }
+  if (!m.cin_layers.empty()) {
+    int maxH = 16;
+    for (auto& c : m.cin_layers) maxH = std::max(maxH, c.Npad);
+    if ((st = dev_alloc(&m.ubuf[0], (size_t)B * m.k * maxH))) return st;
+    if ((st = dev_alloc(&m.ubuf[1], (size_t)B * m.k * maxH))) return st;
+    if ((st = dev_alloc(&m.rowdot, (size_t)B * m.k))) return st;
+  }
+  m.ws_B = B;
+  return RMX_OK;
+}
+
+// --- stage timing -----------------------------------------------------------
+hipEvent_t take_event(rmx_model& m) {
+  if (!m.ev_pool.empty()) {
+    hipEvent_t e = m.ev_pool.back();
+    m.ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct StageTimer {
+  rmx_model& m;
+  hipStream_t s;
+  int idx = -1;
+  hipEvent_t a = nullptr;
+  StageTimer(rmx_model& mm, hipStream_t ss, const char* name) : m(mm), s(ss) {
+    if (!m.timing) return;
+    auto it = std::find(m.stage_names.begin(), m.stage_names.end(), std::string(name));
+    if (it == m.stage_names.end()) {
+      m.stage_names.push_back(name);
+      m.stage_ms.push_back(0.f);
+      idx = (int)m.stage_names.size() - 1;
+    } else {
+      idx = (int)(it - m.stage_names.begin());
+    }
+    a = take_event(m);
+    hipEventRecord(a, s);
+  }
+  ~StageTimer() {
+    if (!m.timing) return;
+    hipEvent_t b = take_event(m);
+    hipEventRecord(b, s);
+    m.pending.push_back({idx, a, b});
+  }
+};
+
+}  // namespace
+
+int model_collect_timing(rmx_model& m) {
+  for (auto& p : m.pending) {
+    RMX_HIP(hipEventSynchronize(p.b));
+    float ms = 0.f;
+    RMX_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    m.stage_ms[p.stage] += ms;
+    m.ev_pool.push_back(p.a);
+    m.ev_pool.push_back(p.b);
+  }
+  m.pending.clear();
+  return RMX_OK;
+}
+
+// The per-model kernel sequence.  in.ids == nullptr means implicit ids (L-A gathered rows).
+int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
+  const int B = in.B;
+  if (B == 0) return RMX_OK;
+  int st = ensure_ws(m, B);
+  if (st) return st;
+  if (m.timing) ++m.timed_calls;
+  const int F = m.F, k = m.k;
+
+  if (m.type == RMX_MODEL_LR) {
+    StageTimer t(m, s, "first_order_sigmoid");
+    if (in.y1) return launch_sigmoid_out(s, B, in.y1, in.beta, in.out);
+    return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, F, 0, nullptr, &in.beta, in.out);
+  }
+
+  // 1. first order (+ FM for DeepFM)
+  const float* pre = nullptr;
+  if (m.type == RMX_MODEL_DEEPFM) {
+    StageTimer t(m, s, "encoder_fm");
+    st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, F, k, m.y12, nullptr, nullptr);
+    pre = m.y12;
+  } else if (m.type != RMX_MODEL_DNN) {
+    if (!in.y1) {
+      StageTimer t(m, s, "first_order");
+      st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, F, k, m.y12, nullptr, nullptr);
+    }
+    pre = m.y12;  // (the L-A irregular path already wrote y1 here)
+  }
+  if (st) return st;
+
+  // 2. interaction encoders
+  OutArgs oa{};
+  oa.wo = m.wo;
+  oa.bo = m.bo;
+  oa.has_bo = m.has_bo ? 1 : 0;
+  oa.pre = pre;
+  oa.beta = in.beta;
+  oa.out = in.out;
+  const float* A = nullptr;
+  int lda = 0;
+  AGatherArgs ga{in.ids, in.table, F, k};
+  bool gather_first = !needs_gather_x(m);
+
+  if (m.type == RMX_MODEL_XDEEPFM) {
+    const float* uprev = nullptr;
+    for (size_t l = 0; l < m.cin_layers.size(); ++l) {
+      StageTimer t(m, s, l == 0 ? "cin_layer1" : (l == 1 ? "cin_layer2" : "cin_layer3+"));
+      const bool last = l + 1 == m.cin_layers.size();
+      float* uout = last ? nullptr : m.ubuf[l & 1];
+      if ((st = launch_cin_layer(s, m.cin_layers[l], l == 0, last, B, F, k, in.ids, in.table, uprev, uout,
+                                 m.rowdot)))
+        return st;
+      uprev = uout;
+    }
+    oa.rowsum = m.rowdot;
+    oa.rowsum_k = k;
+  } else if (m.type == RMX_MODEL_DCN) {
+    StageTimer t(m, s, "cross");
+    if ((st = launch_cross(s, B, F, k, m.cross_depth, in.ids, in.table, m.cross_w, m.cross_b, m.wo_x,
+                           m.pre2)))
+      return st;
+    oa.pre2 = m.pre2;
+  } else if (m.type == RMX_MODEL_PNN) {
+    StageTimer t(m, s, "product");
+    if ((st = launch_product(s, B, F, k, in.ids, in.table, m.pairs, F * (F - 1) / 2, m.xbuf, m.layers[0].Kpad)))
+      return st;
+    A = m.xbuf;
+    lda = m.layers[0].Kpad;
+    gather_first = false;
+  }
+  if (m.type != RMX_MODEL_PNN && !gather_first) {
+    StageTimer t(m, s, "gather_x");
+    if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, m.xbuf, m.layers[0].Kpad))) return st;
+    A = m.xbuf;
+    lda = m.layers[0].Kpad;
+  }
+
+  // 3. tower (the last layer runs the output head: dot + bias + CAddTable + Sigmoid)
+  static const char* names[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
+  for (size_t i = 0; i < m.layers.size(); ++i) {
+    const bool last = i + 1 == m.layers.size();
+    const DenseLayer& L = m.layers[i];
+    float* C = m.h[i & 1];
+    StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
+    st = launch_tower_layer(s, L, B, A, lda, (i == 0 && gather_first) ? &ga : nullptr, C, L.Npad,
+                            last ? Epi::kOutput : Epi::kReluStore, last ? &oa : nullptr);
+    if (st) return st;
+    A = C;
+    lda = L.Npad;
+  }
+  return RMX_OK;
+}
+
+// L-A: the reference's host-array contract.
+int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
+                       float bias, const float* weights, const float* embedding, const float* mats,
+                       float* out) {
+  hipStream_t s = m.ctx->stream;
+  int st;
+  if (nnz > m.la_nnz) {
+    RMX_HIP(hipStreamSynchronize(s));
+    dev_free(m.la_E);
+    dev_free(m.la_w);
+    if (m.type != RMX_MODEL_LR && (st = dev_alloc(&m.la_E, (size_t)nnz * m.k))) return st;
+    if ((st = dev_alloc(&m.la_w, nnz))) return st;
+    m.la_nnz = nnz;
+  }
+  if (B > m.la_B) {
+    RMX_HIP(hipStreamSynchronize(s));
+    dev_free(m.la_out);
+    dev_free(m.la_rowptr);
+    if ((st = dev_alloc(&m.la_out, B))) return st;
+    if (hipMalloc(&m.la_rowptr, sizeof(int64_t) * (B + 1)) != hipSuccess) {
+      set_error("out of device memory");
+      return RMX_E_NOMEM;
+    }
+    m.la_B = B;
+  }
+  if ((st = ensure_ws(m, B))) return st;
+  if (m.mats_len > 0 && (st = model_load_mats(m, mats, false))) return st;
+  if (m.type != RMX_MODEL_LR && nnz > 0)
+    RMX_HIP(hipMemcpyAsync(m.la_E, embedding, sizeof(float) * nnz * m.k, hipMemcpyHostToDevice, s));
+
+  const bool use_w = m.type != RMX_MODEL_DNN;
+  const bool csr = use_w && (m.type == RMX_MODEL_LR || !regular);
+  if (use_w && nnz > 0) {
+    if (csr && !sorted) {
+      // stable counting sort by row keeps ascending-n order inside every row (Scatter order)
+      m.h_rowptr.assign(B + 1, 0);
+      for (int64_t n = 0; n < nnz; ++n) ++m.h_rowptr[(int32_t)index[n] + 1];
+      for (int b = 0; b < B; ++b) m.h_rowptr[b + 1] += m.h_rowptr[b];
+      std::vector<int64_t> pos(m.h_rowptr.begin(), m.h_rowptr.end() - 1);
+      m.h_wperm.resize(nnz);
+      for (int64_t n = 0; n < nnz; ++n) m.h_wperm[pos[(int32_t)index[n]]++] = weights[n];
+      RMX_HIP(hipMemcpyAsync(m.la_w, m.h_wperm.data(), sizeof(float) * nnz, hipMemcpyHostToDevice, s));
+    } else {
+      RMX_HIP(hipMemcpyAsync(m.la_w, weights, sizeof(float) * nnz, hipMemcpyHostToDevice, s));
+    }
+  }
+  if (csr) {
+    if (sorted) {
+      m.h_rowptr.assign(B + 1, 0);
+      for (int64_t n = 0; n < nnz; ++n) ++m.h_rowptr[(int32_t)index[n] + 1];
+      for (int b = 0; b < B; ++b) m.h_rowptr[b + 1] += m.h_rowptr[b];
+    }
+    RMX_HIP(hipMemcpyAsync(m.la_rowptr, m.h_rowptr.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, s));
+    if ((st = launch_first_order_csr(s, B, m.la_rowptr, m.la_w, m.y12))) return st;
+  }
+  FwdInputs in;
+  in.B = B;
+  in.ids = nullptr;
+  in.table = m.la_E;
+  in.wtab = m.la_w;
+  in.y1 = csr ? m.y12 : nullptr;
+  in.beta = bias;
+  in.out = m.la_out;
+  if ((st = model_forward(m, s, in))) return st;
+  RMX_HIP(hipMemcpyAsync(out, m.la_out, sizeof(float) * B, hipMemcpyDeviceToHost, s));
+  RMX_HIP(hipStreamSynchronize(s));
+  // host buffers (h_rowptr / h_wperm) stay alive until the sync above
+  return RMX_OK;
+}
+
+}  // namespace rmx

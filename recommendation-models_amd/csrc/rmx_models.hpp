@@ -1,0 +1,127 @@
+// rmx_models.hpp -- model / table / context objects behind the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "rmx_internal.hpp"
+
+struct rmx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+};
+
+struct rmx_table {
+  rmx_ctx* ctx = nullptr;
+  int64_t V = 0;
+  int k = 0;
+  float* w = nullptr;    // [V]     first-order weights (Angel "weights" row 0)
+  float* emb = nullptr;  // [V][k]  embeddings, row-major (Angel "embedding" rows 0..k-1, transposed)
+};
+
+namespace rmx {
+
+// One forward's inputs, already on the device.
+struct FwdInputs {
+  int B = 0;
+  const int32_t* ids = nullptr;    // [B][F] or nullptr: implicit id = b*F + f (L-A path)
+  const float* table = nullptr;    // [rows][k]
+  const float* wtab = nullptr;     // [rows]
+  const float* y1 = nullptr;       // precomputed first order (L-A irregular index) or nullptr
+  float beta = 0.f;
+  float* out = nullptr;            // [B]
+};
+
+// CIN layer (xDeepFM): C_l (H x F*Hp) packed [Hp_pad/16][F][Npad][16], bias, output slice.
+struct CinLayer {
+  int Hp = 0, Hp_pad = 0, H = 0, Npad = 0;
+  int64_t w_off = -1, b_off = -1, wo_off = -1;
+  float* W = nullptr;
+  float* b = nullptr;
+  float* wo = nullptr;  // [Npad] slice of the output Linear for this layer's pooled maps
+};
+
+}  // namespace rmx
+
+struct rmx_model {
+  rmx_ctx* ctx = nullptr;
+  int type = 0;
+  int64_t input_dim = 0;
+  int F = 0, k = 0;
+  std::vector<int> fc, cin;
+  int cross_depth = 0;
+  std::vector<int32_t> sizes;  // getMatsSize
+  int64_t mats_len = 0;
+
+  // ---- device parameters (packed from mats) ----
+  float* mats_dev = nullptr;                // raw mats copy
+  std::vector<rmx::DenseLayer> layers;      // tower; the last one runs the output head
+  int64_t wo_off = -1, bo_off = -1;         // output Linear weights / bias in mats
+  float* wo = nullptr;                      // device [Npad of last layer]
+  float bo = 0.f;
+  bool has_bo = false;
+  std::vector<rmx::CinLayer> cin_layers;    // xDeepFM
+  int64_t wo_cin_off = -1;                  // start of the pooled-CIN slice of W_out
+  int64_t cross_w_off = -1, cross_b_off = -1, wo_x_off = -1;  // DCN
+  float* cross_w = nullptr;                 // [L][D]
+  float* cross_b = nullptr;                 // [L]
+  float* wo_x = nullptr;                    // [D] slice of W_out for x_L
+  int32_t* pairs = nullptr;                 // PNN (row, col) pairs [P][2]
+  bool params_ready = false;
+  float beta = 0.f;
+  bool beta_set = false;
+
+  // ---- workspace (grown on demand) ----
+  int ws_B = 0;
+  float* h[2] = {nullptr, nullptr};   // [B][Npad] tower activations
+  float* y12 = nullptr;               // [B] first order (+ FM)
+  float* pre2 = nullptr;              // [B] model-specific additive term (CIN / cross)
+  float* xbuf = nullptr;              // [B][Kpad0] materialised A (PNN [x | ip], generic k)
+  float* ubuf[2] = {nullptr, nullptr};  // [B*k][Npad] CIN maps
+  float* rowdot = nullptr;            // [B*k] CIN per-row output partials
+  // L-A staging
+  int64_t la_nnz = 0;
+  int la_B = 0;
+  float* la_E = nullptr;
+  float* la_w = nullptr;
+  int64_t* la_rowptr = nullptr;
+  float* la_out = nullptr;
+  std::vector<int64_t> h_rowptr;
+  std::vector<float> h_wperm;
+
+  // ---- stage timing ----
+  bool timing = false;
+  int timed_calls = 0;
+  std::vector<std::string> stage_names;
+  std::vector<float> stage_ms;
+  struct Pending { int stage; hipEvent_t a, b; };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> ev_pool;
+};
+
+namespace rmx {
+int model_build(rmx_model& m);
+void model_init_mats(const rmx_model& m, uint64_t seed, float* mats);
+void model_release(rmx_model& m);
+int model_load_mats(rmx_model& m, const float* host_mats, bool sync);
+int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in);
+int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
+                       float bias, const float* weights, const float* embedding, const float* mats,
+                       float* out);
+int model_collect_timing(rmx_model& m);
+
+// kernels specific to the interaction encoders
+int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L);
+int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
+                     const int32_t* ids, const float* table, const float* u_prev, float* u_out,
+                     float* rowdot);
+int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const float* table,
+                 const float* cross_w, const float* cross_b, const float* wo_x, float* pre2);
+int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table,
+                   const int32_t* pairs, int P, float* xbuf, int ldx);
+int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table, float* xbuf,
+                    int ldx);
+int tower_wn_for(int Npad);
+}  // namespace rmx

@@ -1,0 +1,438 @@
+"""rmx -- MI355X-native CTR forward path behind the reference's RecModel plugin API.
+
+Host-side mirror of yaochitc/recommendation-models' model boundary
+(src/main/scala/io/yaochi/recommendation/model/RecModel.scala:6-155 and the model classes in
+model/{lr,deepfm,xdeepfm,dcn,pnn,dnn}/), over the C ABI of librmx.so (include/rmx.h).
+
+    from rmx import DeepFM, CooLongFloatMatrix
+    model = DeepFM(inputDim, nFields, embeddingDim, fcDims)
+    model.getMatsSize()                      # same sizes as DeepFM.getMatsSize
+    probs = model.forward(batchSize, batch, bias, weights, embeddings, embeddingDim, mats, matSizes)
+
+Arguments, their meaning and the failure modes follow the reference (see each docstring).
+The math runs in HIP kernels on the GPU; there is no CPU fallback.
+"""
+import numpy as np
+
+from . import _lib
+from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT_K_MAJOR,  # noqa: F401
+                   LAYOUT_ROW_MAJOR, check, ptr)
+
+import ctypes
+
+__all__ = ["RecModelType", "CooLongFloatMatrix", "RecModel", "LR", "DeepFM", "XDeepFM", "DCN", "PNN", "DNN",
+           "Context", "DeviceArray", "EmbeddingTable", "SampleParser", "RmxError", "IllegalArgumentError",
+           "ShapeError", "MatsError", "default_context", "set_device"]
+
+MODEL_LR, MODEL_DEEPFM, MODEL_XDEEPFM, MODEL_DCN, MODEL_PNN, MODEL_DNN = range(6)
+
+
+class RecModelType:
+    """yr/model/RecModelType.scala:5-8"""
+    BIAS_WEIGHT = "BIAS_WEIGHT"
+    BIAS_WEIGHT_EMBEDDING = "BIAS_WEIGHT_EMBEDDING"
+    BIAS_WEIGHT_EMBEDDING_MATS = "BIAS_WEIGHT_EMBEDDING_MATS"
+    BIAS_WEIGHT_EMBEDDING_MATS_FIELD = "BIAS_WEIGHT_EMBEDDING_MATS_FIELD"
+
+
+class CooLongFloatMatrix:
+    """The COO batch the reference passes around (Angel CooLongFloatMatrix):
+    getRowIndices / getColIndices / getValues (RecModel.scala:130-155 reads the first two)."""
+
+    def __init__(self, rows, cols, values=None):
+        self.rows = np.ascontiguousarray(rows, dtype=np.int64)
+        self.cols = np.ascontiguousarray(cols, dtype=np.int64)
+        self.values = (np.ones(len(self.rows), np.float32) if values is None
+                       else np.ascontiguousarray(values, dtype=np.float32))
+        if not (len(self.rows) == len(self.cols) == len(self.values)):
+            raise ValueError("rows / cols / values lengths differ")
+
+    def getRowIndices(self):
+        return self.rows
+
+    def getColIndices(self):
+        return self.cols
+
+    def getValues(self):
+        return self.values
+
+
+# ----------------------------------------------------------------- device ----
+class Context:
+    """One GPU + one HIP stream (rmx_ctx)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(_lib.lib.rmx_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = int(device)
+
+    @property
+    def stream(self):
+        return _lib.lib.rmx_ctx_stream(self.handle)
+
+    def sync(self, stream=None):
+        check(_lib.lib.rmx_stream_sync(stream if stream is not None else self.stream))
+
+    def close(self):
+        if self.handle:
+            _lib.lib.rmx_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx = None
+_default_device = 0
+
+
+def set_device(device):
+    global _default_device
+    _default_device = int(device)
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(_default_device)
+    return _default_ctx
+
+
+class DeviceArray:
+    """A device (HBM) buffer of a numpy dtype, owned by a Context."""
+
+    def __init__(self, ctx, n, dtype, _ptr=None, _owner=None):
+        self.ctx = ctx
+        self.n = int(n)
+        self.dtype = np.dtype(dtype)
+        self._owner = _owner  # views keep their parent alive and never free
+        if _ptr is not None:
+            self.ptr = _ptr
+            return
+        p = ctypes.c_void_p()
+        check(_lib.lib.rmx_malloc(ctx.handle, self.nbytes, ctypes.byref(p)))
+        self.ptr = p
+
+    def view(self, offset, n):
+        """Non-owning view of elements [offset, offset + n)."""
+        if offset < 0 or offset + n > self.n:
+            raise IndexError("view out of range")
+        return DeviceArray(self.ctx, n, self.dtype, ctypes.c_void_p(self.ptr.value + offset * self.dtype.itemsize),
+                           self)
+
+    @property
+    def nbytes(self):
+        return self.n * self.dtype.itemsize
+
+    @classmethod
+    def from_numpy(cls, ctx, a):
+        a = np.ascontiguousarray(a)
+        d = cls(ctx, a.size, a.dtype)
+        d.upload(a)
+        return d
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        if a.size != self.n:
+            raise ValueError("size mismatch")
+        check(_lib.lib.rmx_memcpy_htod(self.ctx.handle, self.ptr, a.ctypes.data, self.nbytes))
+
+    def numpy(self):
+        out = np.empty(self.n, self.dtype)
+        check(_lib.lib.rmx_memcpy_dtoh(self.ctx.handle, out.ctypes.data, self.ptr, self.nbytes))
+        return out
+
+    def free(self):
+        if self._owner is not None:
+            self.ptr = None
+            return
+        if self.ptr:
+            _lib.lib.rmx_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class EmbeddingTable:
+    """HBM-resident first-order weights [V] + embeddings [V][k]: replaces the Angel PS matrices
+    "weights" and "embedding" (ParRecModel.scala:74-105) and their pull + make* gather
+    (ParRecModel.scala:165-199, 279-306)."""
+
+    def __init__(self, ctx, num_rows, embedding_dim):
+        h = ctypes.c_void_p()
+        check(_lib.lib.rmx_table_create(ctx.handle, int(num_rows), int(embedding_dim), ctypes.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+        self.rows = int(num_rows)
+        self.k = int(embedding_dim)
+
+    def upload(self, weights=None, embedding=None, layout=LAYOUT_ROW_MAJOR):
+        """layout LAYOUT_K_MAJOR: embedding is the reference PS layout, k x V."""
+        w = None if weights is None else np.ascontiguousarray(weights, np.float32)
+        e = None if embedding is None else np.ascontiguousarray(embedding, np.float32)
+        if w is not None and w.size != self.rows:
+            raise ValueError("weights must have num_rows entries")
+        if e is not None and e.size != self.rows * self.k:
+            raise ValueError("embedding must have num_rows * k entries")
+        check(_lib.lib.rmx_table_upload(self.handle, ptr(w, ctypes.c_float), ptr(e, ctypes.c_float), layout))
+
+    def fill_synthetic(self, seed):
+        check(_lib.lib.rmx_table_fill_synthetic(self.handle, int(seed)))
+
+    def gather(self, ids_dev, n, w_out=None, emb_out=None, stream=None):
+        """Debug gather (makeWeights / makeEmbeddings): bit-exact copies into device buffers."""
+        check(_lib.lib.rmx_gather(self.handle, int(n), ids_dev.ptr, w_out.ptr if w_out else None,
+                                  emb_out.ptr if emb_out else None, stream))
+
+    def close(self):
+        if self.handle:
+            _lib.lib.rmx_table_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def gen_ids(ctx, seed, row0, batch, n_fields, num_rows, ids_dev, stream=None):
+    """Synthetic field-partitioned ids straight into HBM (SURVEY.md §8d generator)."""
+    check(_lib.lib.rmx_gen_ids(ctx.handle, int(seed), int(row0), int(batch), int(n_fields), int(num_rows),
+                               ids_dev.ptr, stream))
+
+
+# ------------------------------------------------------------------ models ---
+class RecModel:
+    """abstract class RecModel(type) -- yr/model/RecModel.scala:6-127."""
+
+    _kind = None
+    _type = None
+
+    def __init__(self, inputDim, nFields=0, embeddingDim=0, fcDims=(), cinDims=(), crossDepth=0, ctx=None):
+        self._args = (int(inputDim), int(nFields), int(embeddingDim), tuple(int(d) for d in fcDims),
+                      tuple(int(d) for d in cinDims), int(crossDepth))
+        self._meta = self._create(None)  # host-only handle: metadata without a GPU
+        self._ctx = ctx
+        self._dev = None
+        self._dev_mats_loaded = False
+
+    def _create(self, ctx):
+        inputDim, nFields, k, fc, cin, depth = self._args
+        fc_a = (ctypes.c_int32 * max(len(fc), 1))(*fc)
+        cin_a = (ctypes.c_int32 * max(len(cin), 1))(*cin)
+        h = ctypes.c_void_p()
+        check(_lib.lib.rmx_model_create(ctx.handle if ctx else None, self._kind, inputDim, nFields, k, fc_a,
+                                        len(fc), cin_a, len(cin), depth, ctypes.byref(h)))
+        return h
+
+    def _device(self):
+        if self._dev is None:
+            if self._ctx is None:
+                self._ctx = default_context()
+            self._dev = self._create(self._ctx)
+        return self._dev
+
+    @property
+    def context(self):
+        self._device()
+        return self._ctx
+
+    def __del__(self):
+        try:
+            if self._dev:
+                _lib.lib.rmx_model_destroy(self._dev)
+            if self._meta:
+                _lib.lib.rmx_model_destroy(self._meta)
+        except Exception:
+            pass
+
+    # -- metadata (RecModel.scala:7, :121-125)
+    def getType(self):
+        return self._type
+
+    def getMatsSize(self):
+        n = ctypes.c_int()
+        check(_lib.lib.rmx_model_get_mats_size(self._meta, None, 0, ctypes.byref(n)))
+        buf = (ctypes.c_int32 * max(n.value, 1))()
+        check(_lib.lib.rmx_model_get_mats_size(self._meta, buf, n.value, ctypes.byref(n)))
+        return [int(buf[i]) for i in range(n.value)]
+
+    def matsLength(self):
+        """sum over pairs of getMatsSize (ParRecModel.initMats, ParRecModel.scala:107-113)."""
+        return int(_lib.lib.rmx_model_mats_len(self._meta))
+
+    def getInputDim(self):
+        return int(_lib.lib.rmx_model_get_input_dim(self._meta))
+
+    def getEmbeddingDim(self):
+        return int(_lib.lib.rmx_model_get_embedding_dim(self._meta))
+
+    def initMats(self, seed):
+        """Deterministic synthetic mats (Xavier-uniform weights, U(-0.01, 0.01) biases)."""
+        mats = np.zeros(self.matsLength(), np.float32)
+        check(_lib.lib.rmx_model_init_mats(self._meta, int(seed), ptr(mats, ctypes.c_float)))
+        return mats
+
+    # -- forward (RecModel.scala:9-63)
+    def forward(self, batchSize, batch, bias=None, weights=None, embeddings=None, embeddingDim=None, mats=None,
+                matSizes=None, fields=None):
+        """RecModel.forward overloads.  batch is a CooLongFloatMatrix (or (rows, cols[, values])); the
+        other arrays are the already-gathered flat host arrays of the reference contract.  Returns
+        batchSize sigmoid probabilities (np.float32)."""
+        if not isinstance(batch, CooLongFloatMatrix):
+            batch = CooLongFloatMatrix(*batch)
+        index = batch.getRowIndices()
+        feats = batch.getColIndices()
+        f32 = lambda a: None if a is None else np.ascontiguousarray(a, np.float32).reshape(-1)
+        bias, weights, embeddings, mats = f32(bias), f32(weights), f32(embeddings), f32(mats)
+        sizes = None if matSizes is None else np.ascontiguousarray(matSizes, np.int32)
+        fl = None if fields is None else np.ascontiguousarray(fields, np.int64)
+        if embeddingDim is None:
+            embeddingDim = self.getEmbeddingDim()
+        out = np.zeros(int(batchSize), np.float32)
+        h = self._device()
+        check(_lib.lib.rmx_forward(
+            h, int(batchSize), len(index), ptr(index, ctypes.c_int64), ptr(feats, ctypes.c_int64),
+            ptr(bias, ctypes.c_float), ptr(weights, ctypes.c_float), ptr(embeddings, ctypes.c_float),
+            int(embeddingDim), ptr(mats, ctypes.c_float), ptr(sizes, ctypes.c_int32),
+            0 if sizes is None else len(sizes), ptr(fl, ctypes.c_int64), ptr(out, ctypes.c_float)))
+        return out
+
+    def backward(self, *args, **kwargs):
+        raise NotImplementedError("backward is out of scope for this round (SURVEY.md §8f rank 1)")
+
+    # -- device-resident path (replaces ParRecModel.pull* + make*)
+    def setMats(self, mats):
+        mats = np.ascontiguousarray(mats, np.float32)
+        check(_lib.lib.rmx_model_set_mats(self._device(), ptr(mats, ctypes.c_float), len(mats)))
+
+    def setBias(self, bias):
+        check(_lib.lib.rmx_model_set_bias(self._device(), float(np.asarray(bias).reshape(-1)[0])))
+
+    def forward_ids(self, table, batch, ids_dev, out_dev, stream=None):
+        """L-B forward: ids [batch * nFields] int32 and out [batch] float32 are DeviceArrays."""
+        check(_lib.lib.rmx_forward_ids(self._device(), table.handle, int(batch), ids_dev.ptr, out_dev.ptr, stream))
+
+    def encoder_ids(self, table, batch, ids_dev, y_dev, stream=None):
+        check(_lib.lib.rmx_encoder_ids(self._device(), table.handle, int(batch), ids_dev.ptr, y_dev.ptr, stream))
+
+    def set_timing(self, enable=True):
+        check(_lib.lib.rmx_model_set_timing(self._device(), 1 if enable else 0))
+
+    def get_timing(self):
+        """{stage name: total ms} and the number of timed forward calls."""
+        cap, stride = 32, 64
+        names = ctypes.create_string_buffer(cap * stride)
+        ms = (ctypes.c_float * cap)()
+        n, calls = ctypes.c_int(), ctypes.c_int()
+        check(_lib.lib.rmx_model_get_timing(self._device(), names, stride, ms, cap, ctypes.byref(n),
+                                            ctypes.byref(calls)))
+        res = {}
+        for i in range(min(n.value, cap)):
+            res[names.raw[i * stride:(i + 1) * stride].split(b"\0", 1)[0].decode()] = float(ms[i])
+        return res, calls.value
+
+
+class LR(RecModel):
+    """class LR(inputDim) -- yr/model/lr/LR.scala:10-40.  nFields is only needed by forward_ids."""
+    _kind = MODEL_LR
+    _type = RecModelType.BIAS_WEIGHT
+
+    def __init__(self, inputDim, nFields=0, ctx=None):
+        super().__init__(inputDim, nFields, 0, ctx=ctx)
+
+
+class DeepFM(RecModel):
+    """class DeepFM(inputDim, nFields, embeddingDim, fcDims) -- yr/model/deepfm/DeepFM.scala:10-49."""
+    _kind = MODEL_DEEPFM
+    _type = RecModelType.BIAS_WEIGHT_EMBEDDING_MATS
+
+    def __init__(self, inputDim, nFields, embeddingDim, fcDims, ctx=None):
+        super().__init__(inputDim, nFields, embeddingDim, fcDims, ctx=ctx)
+
+
+class DNN(RecModel):
+    """class DNN(inputDim, nFields, embeddingDim, fcDims) -- yr/model/dnn/DNN.scala:10-49."""
+    _kind = MODEL_DNN
+    _type = RecModelType.BIAS_WEIGHT_EMBEDDING_MATS
+
+    def __init__(self, inputDim, nFields, embeddingDim, fcDims, ctx=None):
+        super().__init__(inputDim, nFields, embeddingDim, fcDims, ctx=ctx)
+
+
+class XDeepFM(RecModel):
+    """class XDeepFM(inputDim, nFields, embeddingDim, fcDims, cinDims) -- yr/model/xdeepfm/XDeepFM.scala:10-56.
+    cinDims with more than one layer follow SURVEY.md Appendix A (the reference only runs one)."""
+    _kind = MODEL_XDEEPFM
+    _type = RecModelType.BIAS_WEIGHT_EMBEDDING_MATS
+
+    def __init__(self, inputDim, nFields, embeddingDim, fcDims, cinDims, ctx=None):
+        super().__init__(inputDim, nFields, embeddingDim, fcDims, cinDims, ctx=ctx)
+
+
+class DCN(RecModel):
+    """class DCN(inputDim, nFields, embeddingDim, crossDepth, fcDims) -- yr/model/dcn/DCN.scala:10-60."""
+    _kind = MODEL_DCN
+    _type = RecModelType.BIAS_WEIGHT_EMBEDDING_MATS
+
+    def __init__(self, inputDim, nFields, embeddingDim, crossDepth, fcDims, ctx=None):
+        super().__init__(inputDim, nFields, embeddingDim, fcDims, (), crossDepth, ctx=ctx)
+
+
+class PNN(RecModel):
+    """class PNN(inputDim, nFields, embeddingDim, fcDims) -- yr/model/pnn/PNN.scala:10-54 (inner product)."""
+    _kind = MODEL_PNN
+    _type = RecModelType.BIAS_WEIGHT_EMBEDDING_MATS
+
+    def __init__(self, inputDim, nFields, embeddingDim, fcDims, ctx=None):
+        super().__init__(inputDim, nFields, embeddingDim, fcDims, ctx=ctx)
+
+
+# ------------------------------------------------------------------ parser ---
+class SampleParser:
+    """yr/data/SampleParser.scala:14-85 (LIBSVM / LIBFFM text -> COO, 1-based ids -> id - 1)."""
+
+    @staticmethod
+    def parse(lines, type_):
+        if type_ == RecModelType.BIAS_WEIGHT_EMBEDDING_MATS_FIELD:
+            return SampleParser.parseLIBFFM(lines)
+        coo, targets = SampleParser.parseLIBSVM(lines)
+        return coo, None, targets
+
+    @staticmethod
+    def parseLIBSVM(lines):
+        rows, cols, vals = [], [], []
+        targets = np.zeros(len(lines), np.float32)
+        for i, line in enumerate(lines):
+            parts = line.split(" ")
+            targets[i] = float(parts[0])
+            for kv in parts[1:]:
+                k, v = kv.split(":")
+                rows.append(i)
+                cols.append(int(k) - 1)
+                vals.append(float(v))
+        return CooLongFloatMatrix(rows, cols, vals), targets
+
+    @staticmethod
+    def parseLIBFFM(lines):
+        rows, cols, fields, vals = [], [], [], []
+        targets = np.zeros(len(lines), np.float32)
+        for i, line in enumerate(lines):
+            parts = line.split(" ")
+            targets[i] = float(parts[0])
+            for fkv in parts[1:]:
+                f, k, v = fkv.split(":")
+                rows.append(i)
+                fields.append(int(f))
+                cols.append(int(k) - 1)
+                vals.append(float(v))
+        return CooLongFloatMatrix(rows, cols, vals), np.asarray(fields, np.int64), targets
