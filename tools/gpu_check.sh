@@ -1,0 +1,44 @@
+#!/bin/bash
+# One GPU session on the gpurun box: parity tests, a bench line, a rocprofv3 kernel-trace summary.
+# Every GPU step has its own time limit; a crash / abort / timeout ends the script.
+# Usage (from the repo root): bash tools/gpu_check.sh [tag] [steps...]
+set -u
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"tests bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+run() {  # run <name> <seconds> <cmd...>; stop on anything but success / plain test failure
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+  tail -n 5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping after $name (rc=$rc)"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python bench.py ;;
+    benchx) run bench_xdeepfm 400 python bench.py --workload xdeepfm --no-cpu-baseline ;;
+    prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o deepfm -- \
+            python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    profx) run profx 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx" -o xdeepfm -- \
+            python3 bench.py --workload xdeepfm --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o fetch -- \
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+         run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+  esac
+done
+echo "== all done"
