@@ -107,7 +107,7 @@ DenseLayer make_layer(int K, int N, int64_t w_off, int64_t b_off) {
   L.K = K;
   L.N = N;
   L.Kpad = round_up(K, kChunk);
-  L.Npad = round_up(N, 80);
+  L.Npad = tower_npad_for(N);
   L.w_off = w_off;
   L.b_off = b_off;
   return L;
@@ -272,11 +272,6 @@ int model_build(rmx_model& m) {
     set_error("internal: mats layout mismatch");
     return RMX_E_INVALID;
   }
-  for (auto& L : m.layers)
-    if (L.Npad > 640 && &L == &m.layers.back()) {
-      set_error("last hidden layer wider than 640 is not supported");
-      return RMX_E_INVALID;
-    }
 
   if (!m.ctx) return RMX_OK;  // host-only model: metadata only
   // device parameter buffers

@@ -123,5 +123,5 @@ int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const
                    const int32_t* pairs, int P, float* xbuf, int ldx);
 int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table, float* xbuf,
                     int ldx);
-int tower_wn_for(int Npad);
+int tower_npad_for(int N);
 }  // namespace rmx
