@@ -107,7 +107,7 @@ def main():
         dist.init_process_group("gloo")
     import rmx
 
-    B = args.batch or (65536 if args.workload == "deepfm" else 2048)
+    B = args.batch or (65536 if args.workload == "deepfm" else 16384)
     rmx.set_device(local)
     ctx = rmx.default_context()
     stream = ctx.stream

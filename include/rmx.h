@@ -67,6 +67,12 @@ typedef struct rmx_table rmx_table;
 const char* rmx_last_error(void);
 int rmx_abi_version(void);
 
+/* Process-wide tuning knobs (kernel variant selection for A/B timing in one process).
+ * Known keys: "tower_variant" (see k_tower.hip), "cin_variant" (k_cin.hip).  Unknown keys are
+ * stored and ignored.  rmx_get_tuning returns def when the key was never set. */
+int rmx_set_tuning(const char* key, int value);
+int rmx_get_tuning(const char* key, int def);
+
 /* ------------------------------------------------------------- context ---- */
 /* One context per (process, GPU).  Owns a HIP stream. */
 int rmx_ctx_create(int device, rmx_ctx** out);

@@ -21,6 +21,16 @@ namespace rmx {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+static std::mutex g_tune_mu;
+static std::vector<std::pair<std::string, int>> g_tune;
+
+int tuning_get(const char* key, int def) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  for (auto& kv : g_tune)
+    if (kv.first == key) return kv.second;
+  return def;
+}
+
 }  // namespace rmx
 
 using namespace rmx;
@@ -28,6 +38,23 @@ using namespace rmx;
 // --------------------------------------------------------------------- misc --
 extern "C" const char* rmx_last_error(void) { return g_err.c_str(); }
 extern "C" int rmx_abi_version(void) { return RMX_ABI_VERSION; }
+
+extern "C" int rmx_set_tuning(const char* key, int value) {
+  if (!key) {
+    set_error("rmx_set_tuning: key is NULL");
+    return RMX_E_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  for (auto& kv : g_tune)
+    if (kv.first == key) {
+      kv.second = value;
+      return RMX_OK;
+    }
+  g_tune.emplace_back(key, value);
+  return RMX_OK;
+}
+
+extern "C" int rmx_get_tuning(const char* key, int def) { return key ? tuning_get(key, def) : def; }
 
 #define CHECK_ARG(cond, msg)            \
   do {                                  \

@@ -1,0 +1,536 @@
+// k_gemm.hip -- the fp32 MFMA GEMM engine behind the tower layers and the xDeepFM CIN (gfx950).
+//
+// Tower layer: BigDL Linear + ReLU chain, model/encoder/HigherOrderEncoder.scala:34-59
+// (Linear(in->out, W: out x in, y = b + x W^T) + ReLU per fcDim, then Linear(->1)) and the
+// output heads of DeepFM.scala:130-134 / XDeepFM / DCN / PNN (CAddTable + Sigmoid).
+// CIN layer: model/xdeepfm/CINEncoder.scala:36-58, 105-176 (+ SURVEY.md Appendix A for L > 1):
+//   x0[b,j,f] = e[b,f,j]; z[f*Hp + h] = x0[b,j,f] * u_{l-1}[b,j,h]  (MM(transB = true), :152)
+//   u_l[b,j,:] = ReLU(c_l + C_l z)                                   (Linear + ReLU, :154-155)
+// a GEMM with M = B*k rows (b, j), K = F * Hp, N = H whose A operand is generated in registers
+// (the reference materialises z: B*k x F*Hp floats, 2 GB per layer at B = 4096), and whose
+// epilogue folds the output Linear in: rowdot[b*k + j] (+)= sum_h u_l[b,j,h] * W_out[slice_l + h]
+// (sum_j sum_h == sum_h sum_j: the pooled pi_l . W_out, :159-176).
+//
+// All on v_mfma_f32_16x16x4_f32 (exact f32 FMA chain, 64 FLOP/clk/SIMD = the chip's fp32 peak).
+// Block = WM waves stacked on M; a wave owns MT*16 rows x all NT*16 columns of the block
+// (MT*NT accumulator tiles).  WM is a multiple of 4, so every SIMD carries the same number of
+// waves and the one barrier per K stage never waits on an overloaded SIMD.  K is consumed in
+// 16-wide chunks; inside a chunk lane group g = lane>>4 owns k = 4g..4g+3, so one ds_read_b128
+// per fragment feeds the 4 k-steps of the chunk.  LDS tiles are [rows][16] fp32 with a slot
+// XOR-swizzle that keeps the 16-row fragment reads conflict-free for all four ds_read_b128 lane
+// groups.  A stage holds BKC chunks; the next stage's global loads are issued before the MFMAs
+// of the current one and written to the idle LDS buffer after them (one barrier per stage).
+// A operand producers:
+//   kDenseA     activations of the previous layer, staged through LDS;
+//   kGatherK16  / kGatherAny: first layer, rows gathered straight from the embedding table
+//               (ids staged in LDS; x = Reshape(B, F*k) is never materialised);
+//   kCinOuter   CIN: a = x0[row][f] * u[row][h-chunk], computed in registers (x0 tile in LDS,
+//               u chunk in registers), only the weights go through LDS.
+#include <algorithm>
+
+#include "rmx_models.hpp"
+
+namespace rmx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// physical 16-B slot of logical slot g in row `row` of a [rows][16] fp32 LDS tile
+__device__ __forceinline__ int swz_slot(int row, int g) { return g ^ ((4 - ((row >> 2) & 3)) & 3); }
+
+enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
+enum EpiMode : int { kEpiRelu = 0, kEpiOutput = 1, kEpiCin = 2 };
+
+struct GemmArgs {
+  int M, K, Kpad, Npad;
+  const float* A;  // kDenseA: [M][lda]
+  int lda;
+  AGatherArgs ga;  // gather modes (ids, table, F, k); kCinOuter: ids, table, F, k of x0
+  // kCinOuter
+  const float* u_prev;  // [M][ldu] previous CIN maps, nullptr for the first layer (u = x0)
+  int ldu, XS, cin_first;
+  const float* Wp;     // [Kpad/16][Npad][16]
+  const float* bias;   // [Npad]
+  float* C;            // kEpiRelu / kEpiCin (u_out, may be null): [M][ldc]
+  int ldc;
+  OutArgs oa;          // kEpiOutput
+  const float* wo;     // kEpiCin: [Npad] slice of the output Linear
+  float* rowdot;       // kEpiCin: [M]
+};
+
+template <int MT, int NT, int WM, int BKC, int AMODE, int EPI>
+__global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
+  constexpr int BM = WM * MT * 16, BN = NT * 16, NTHR = WM * 64;
+  constexpr bool A_LDS = AMODE != kCinOuter;
+  constexpr int AROWS = A_LDS ? BM * BKC : 0, ROWS = AROWS + BN * BKC;  // 64-B rows per stage
+  constexpr int ITEMS = ROWS * 4;                                       // float4 items per stage
+  constexpr int PER = (ITEMS + NTHR - 1) / NTHR;
+  constexpr int STAGE = ROWS * 16;                                      // floats per stage
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* lds0 = smem;
+  float* lds1 = smem + STAGE;
+  float* extra = smem + 2 * STAGE;                 // gather: int ids [BM][F]; CIN: x0 [BM][XS]
+  int* sids = reinterpret_cast<int*>(extra);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = p.M;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = p.Kpad / 16;
+  const int nstages = (nchunks + BKC - 1) / BKC;
+  const int F = p.ga.F;
+
+  if constexpr (AMODE == kGatherK16 || AMODE == kGatherAny) {
+    for (int i = tid; i < BM * F; i += NTHR) {
+      const int r = i / F, f = i - r * F;
+      const int m = m0 + r;
+      int id = 0;
+      if (m < M) id = p.ga.ids ? p.ga.ids[(int64_t)m * F + f] : m * F + f;
+      sids[i] = id;
+    }
+    __syncthreads();
+  }
+  if constexpr (AMODE == kCinOuter) {
+    // x0 tile: x0s[r][f] = e[b, f, j] for row m0 + r = b*k + j, zero padded to XS columns
+    const int k = p.ga.k, XS = p.XS;
+    for (int i = tid; i < BM * XS; i += NTHR) {
+      const int j = i % k;
+      const int rest = i / k;
+      const int f = rest % XS;
+      const int rb = rest / XS;
+      const int r = rb * k + j;
+      if (r >= BM) continue;
+      const int m = m0 + r;
+      float v = 0.f;
+      if (f < F && m < M) {
+        const int b = m / k;
+        const int id = p.ga.ids ? p.ga.ids[(int64_t)b * F + f] : b * F + f;
+        v = p.ga.table[(int64_t)id * k + j];
+      }
+      extra[r * XS + f] = v;
+    }
+    __syncthreads();
+  }
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 stage[PER];
+  // item i of a stage: row = i >> 2 (A rows first: [BKC][BM], then B rows [BKC][BN]), slot g = i & 3
+  auto gload = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = tid + q * NTHR;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int row = i >> 2, g = i & 3;
+      if (row < AROWS) {
+        const int cc = row / BM, r = row - cc * BM;
+        const int c = st * BKC + cc;
+        const int m = m0 + r;
+        const int kk = c * 16 + g * 4;
+        if (m < M && kk < p.K) {
+          if constexpr (AMODE == kGatherK16) {
+            const int id = sids[r * F + c];
+            v = *reinterpret_cast<const float4*>(p.ga.table + (int64_t)id * 16 + g * 4);
+          } else if constexpr (AMODE == kGatherAny) {
+            const int f = kk / p.ga.k, j = kk - f * p.ga.k;
+            const int id = sids[r * F + f];
+            v = *reinterpret_cast<const float4*>(p.ga.table + (int64_t)id * p.ga.k + j);
+          } else {
+            v = *reinterpret_cast<const float4*>(p.A + (int64_t)m * p.lda + kk);
+          }
+        }
+      } else if (row < ROWS) {
+        const int rb = row - AROWS;
+        const int cc = rb / BN, n = rb - cc * BN;
+        const int c = st * BKC + cc;
+        if (c < nchunks) v = *reinterpret_cast<const float4*>(p.Wp + ((int64_t)c * p.Npad + n0 + n) * 16 + g * 4);
+      }
+      stage[q] = v;
+    }
+  };
+  auto sstore = [&](float* buf) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = tid + q * NTHR;
+      const int row = i >> 2, g = i & 3;
+      if (row < ROWS) {
+        const int lrow = row < AROWS ? (row % BM) : ((row - AROWS) % BN);
+        *reinterpret_cast<float4*>(buf + row * 16 + swz_slot(lrow, g) * 4) = stage[q];
+      }
+    }
+  };
+
+  gload(0);
+  sstore(lds0);
+  __syncthreads();
+
+  const int g = lane >> 4, r16 = lane & 15;
+  int arow[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) arow[i] = wid * MT * 16 + i * 16 + r16;
+
+  // kCinOuter: the row's u[h-chunk] for the current hc, reloaded when hc changes
+  float4 uf[MT];
+  int cur_hc = -1;
+  auto load_u = [&](int hc) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (p.cin_first) {
+        uf[i] = *reinterpret_cast<const float4*>(extra + arow[i] * p.XS + hc * 16 + g * 4);
+      } else {
+        const int m = m0 + arow[i];
+        uf[i] = m < M ? *reinterpret_cast<const float4*>(p.u_prev + (int64_t)m * p.ldu + hc * 16 + g * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    cur_hc = hc;
+  };
+
+  for (int st = 0; st < nstages; ++st) {
+    const float* cur = (st & 1) ? lds1 : lds0;
+    float* nxt = (st & 1) ? lds0 : lds1;
+    const bool more = st + 1 < nstages;
+    if (more) gload(st + 1);
+#pragma unroll
+    for (int cc = 0; cc < BKC; ++cc) {
+      const int c = st * BKC + cc;
+      if (BKC > 1 && c >= nchunks) break;
+      const float* Bt = cur + AROWS * 16 + cc * BN * 16;
+      float4 a[MT];
+      if constexpr (A_LDS) {
+        const float* At = cur + cc * BM * 16;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          a[i] = *reinterpret_cast<const float4*>(At + arow[i] * 16 + swz_slot(arow[i], g) * 4);
+      } else {
+        const int hc = c / F, f = c - hc * F;
+        if (hc != cur_hc) load_u(hc);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const float xv = extra[arow[i] * p.XS + f];
+          a[i] = make_float4(xv * uf[i].x, xv * uf[i].y, xv * uf[i].z, xv * uf[i].w);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NT; j += 2) {
+        const int row0 = j * 16 + r16;
+        const float4 b0 = *reinterpret_cast<const float4*>(Bt + row0 * 16 + swz_slot(row0, g) * 4);
+        if (j + 1 < NT) {
+          const int row1 = row0 + 16;
+          const float4 b1 = *reinterpret_cast<const float4*>(Bt + row1 * 16 + swz_slot(row1, g) * 4);
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b0.x, acc[i][j], 0, 0, 0);
+            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b1.x, acc[i][j + 1], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b0.y, acc[i][j], 0, 0, 0);
+            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b1.y, acc[i][j + 1], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b0.z, acc[i][j], 0, 0, 0);
+            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b1.z, acc[i][j + 1], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b0.w, acc[i][j], 0, 0, 0);
+            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b1.w, acc[i][j + 1], 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b0.x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b0.y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b0.z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b0.w, acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (more) sstore(nxt);
+    __syncthreads();
+  }
+
+  // C/D layout of 16x16 MFMA: lane holds rows 4*(lane>>4) + r (r = 0..3), column lane & 15.
+  if constexpr (EPI == kEpiRelu) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int mw = m0 + wid * MT * 16 + i * 16 + g * 4;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + j * 16 + r16;
+        const float bn = p.bias[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bn;
+          v = v > 0.f ? v : 0.f;
+          if (mw + r < M) p.C[(int64_t)(mw + r) * p.ldc + n] = v;
+        }
+      }
+    }
+  } else {
+    // row reduction sum_n ReLU(acc + b)[n] * w[n] over the block's (= the layer's) columns
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int mw = m0 + wid * MT * 16 + i * 16 + g * 4;
+      float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = j * 16 + r16;
+        const float bn = p.bias[n];
+        const float wn = EPI == kEpiOutput ? p.oa.wo[n] : p.wo[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bn;
+          v = v > 0.f ? v : 0.f;
+          part[r] += v * wn;
+          if (EPI == kEpiCin && p.C && mw + r < M) p.C[(int64_t)(mw + r) * p.ldc + n] = v;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = part[r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        part[r] = v;
+      }
+      if (r16 < 4) {
+        // lane r16 = r finalises row mw + r (rows of the lane group g)
+        const int m = mw + r16;
+        float y = r16 == 0 ? part[0] : (r16 == 1 ? part[1] : (r16 == 2 ? part[2] : part[3]));
+        if (m < M) {
+          if constexpr (EPI == kEpiCin) {
+            p.rowdot[m] = p.cin_first ? y : p.rowdot[m] + y;
+          } else {
+            const OutArgs& oa = p.oa;
+            if (oa.has_bo) y = y + oa.bo;
+            if (oa.rowsum) {
+              float rs = 0.f;
+              for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
+              y = rs + y;
+            }
+            if (oa.pre2) y = oa.pre2[m] + y;
+            float t = oa.pre ? oa.pre[m] + y : y;
+            t = t + oa.beta;
+            oa.out[m] = 1.0f / (1.0f + expf(-t));
+          }
+        }
+      }
+    }
+  }
+}
+
+// Output head for a last hidden layer too wide for one block: logit from the stored ReLU
+// activations h[m][0..N) (one wave per row).
+__global__ __launch_bounds__(256) void tower_head_kernel(int M, int N, const float* __restrict__ h, int ldh,
+                                                         OutArgs oa) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float p = 0.f;
+  for (int n = lane; n < N; n += 64) p += h[(int64_t)m * ldh + n] * oa.wo[n];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+  if (lane != 0) return;
+  float y = p;
+  if (oa.has_bo) y = y + oa.bo;
+  if (oa.rowsum) {
+    float rs = 0.f;
+    for (int j = 0; j < oa.rowsum_k; ++j) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + j];
+    y = rs + y;
+  }
+  if (oa.pre2) y = oa.pre2[m] + y;
+  float t = oa.pre ? oa.pre[m] + y : y;
+  t = t + oa.beta;
+  oa.out[m] = 1.0f / (1.0f + expf(-t));
+}
+
+// C_l (H x F*Hp row-major, column f*Hp + h) -> [Hp_pad/16][F][Npad][16]
+__global__ void pack_cin_kernel(const float* __restrict__ C, int F, int Hp, int H, int Npad, int64_t tot,
+                                float* __restrict__ Wp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int kk = (int)(i & 15);
+  const int64_t rest = i >> 4;
+  const int n = (int)(rest % Npad);
+  const int64_t c = rest / Npad;
+  const int f = (int)(c % F);
+  const int hc = (int)(c / F);
+  const int h = hc * 16 + kk;
+  Wp[i] = (n < H && h < Hp) ? C[(int64_t)n * F * Hp + (int64_t)f * Hp + h] : 0.f;
+}
+
+int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L) {
+  const int64_t tot = (int64_t)L.Hp_pad * F * L.Npad;
+  hipLaunchKernelGGL(pack_cin_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats + L.w_off, F,
+                     L.Hp, L.H, L.Npad, tot, L.W);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// -------------------------------------------------------------- dispatch ----
+namespace {
+
+// column tiles per block that have kernels (a layer's Npad is a multiple of one of them)
+constexpr int kNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16, 20, 25, 26};
+constexpr int kCinNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16};
+
+template <int MT, int NT, int WM, int BKC, int AMODE, int EPI>
+int launch_cfg(hipStream_t s, GemmArgs& p) {
+  constexpr int BM = WM * MT * 16, BN = NT * 16;
+  constexpr int AROWS = AMODE != kCinOuter ? BM * BKC : 0;
+  size_t lds = sizeof(float) * 2 * (AROWS + BN * BKC) * 16;
+  if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * BM * p.ga.F;
+  if (AMODE == kCinOuter) lds += sizeof(float) * BM * p.XS;
+  if (lds > 160 * 1024) {
+    set_error("gemm: LDS budget exceeded (" + std::to_string(lds) + " bytes)");
+    return RMX_E_INVALID;
+  }
+  dim3 grid((p.M + BM - 1) / BM, p.Npad / BN);
+  auto kern = gemm_kernel<MT, NT, WM, BKC, AMODE, EPI>;
+  if (lds > 64 * 1024)
+    RMX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, grid, dim3(WM * 64), lds, s, p);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+template <int NT>
+int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
+  // 8 waves (2 per SIMD) for large batches, 4 for small ones; two K chunks per stage when the
+  // A rows come from a dense activation buffer, one when they are gathered (ids share the LDS).
+  const bool big = p.M >= 8192;
+#define RMX_TOWER_CASE(WM, BKC, AM)                                                        \
+  if (epi == Epi::kReluStore) return launch_cfg<1, NT, WM, BKC, AM, kEpiRelu>(s, p); \
+  return launch_cfg<1, NT, WM, BKC, AM, kEpiOutput>(s, p);
+  if (big) {
+    if (amode == kDenseA) { RMX_TOWER_CASE(8, 2, kDenseA) }
+    if (amode == kGatherK16) { RMX_TOWER_CASE(8, 1, kGatherK16) }
+    RMX_TOWER_CASE(8, 1, kGatherAny)
+  }
+  if (amode == kDenseA) { RMX_TOWER_CASE(4, 1, kDenseA) }
+  if (amode == kGatherK16) { RMX_TOWER_CASE(4, 1, kGatherK16) }
+  RMX_TOWER_CASE(4, 1, kGatherAny)
+#undef RMX_TOWER_CASE
+}
+
+template <int NT>
+int launch_cin_nt(hipStream_t s, GemmArgs& p) {
+  // knob "cin_variant": 0 = 8 waves x 16 rows, 2 chunks per stage (measured fastest at
+  // B = 4096: 1.637 ms / layer vs 1.663 for 8 x 32 rows and 1.682 for 4 x 32 rows);
+  // 1 = 8 waves x 32 rows.  Small M always uses 4 waves x 16 rows.
+  const int var = tuning_get("cin_variant", 0);
+  if (p.M < 8192) return launch_cfg<1, NT, 4, 2, kCinOuter, kEpiCin>(s, p);
+  if (var == 1) return launch_cfg<2, NT, 8, 2, kCinOuter, kEpiCin>(s, p);
+  return launch_cfg<1, NT, 8, 2, kCinOuter, kEpiCin>(s, p);
+}
+
+}  // namespace
+
+// Npad of a tower layer of width N: a multiple of one block width NT*16 (NT from kNTs), chosen
+// to minimise padding (ties: the wider block).
+int tower_npad_for(int N) {
+  const int nt = (N + 15) / 16;
+  int best = -1, best_pad = 1 << 30;
+  for (int c : kNTs) {
+    const int pad = (nt + c - 1) / c * c;
+    if (pad < best_pad || (pad == best_pad && c > best)) {
+      best_pad = pad;
+      best = c;
+    }
+  }
+  return best_pad * 16;
+}
+
+// Npad of a CIN layer of H maps: one block spans the layer (the rowdot epilogue), so the
+// smallest instantiated NT >= ceil(H/16); -1 if H is too wide.
+int cin_npad_for(int H) {
+  const int nt = (H + 15) / 16;
+  for (int c : kCinNTs)
+    if (c >= nt) return c * 16;
+  return -1;
+}
+
+static int tower_nt_for(int Npad) {
+  const int nt = Npad / 16;
+  int best = 1;
+  for (int c : kNTs)
+    if (nt % c == 0 && c > best) best = c;
+  return best;
+}
+
+int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
+                       const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa) {
+  if (M <= 0) return RMX_OK;
+  const int nt = tower_nt_for(L.Npad);
+  if (epi == Epi::kOutput && nt * 16 != L.Npad) {
+    // too wide for one block: store the ReLU activations, then a separate head pass
+    int st = launch_tower_layer(s, L, M, A, lda, ga, C, ldc, Epi::kReluStore, nullptr);
+    if (st != RMX_OK) return st;
+    hipLaunchKernelGGL(tower_head_kernel, dim3((M + 3) / 4), dim3(256), 0, s, M, L.N, C, ldc, *oa);
+    RMX_HIP(hipGetLastError());
+    return RMX_OK;
+  }
+  GemmArgs p{};
+  p.M = M;
+  p.K = L.K;
+  p.Kpad = L.Kpad;
+  p.Npad = L.Npad;
+  p.A = A;
+  p.lda = lda;
+  if (ga) p.ga = *ga;
+  p.Wp = L.W;
+  p.bias = L.b;
+  p.C = C;
+  p.ldc = ldc;
+  if (oa) p.oa = *oa;
+  const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
+  switch (nt) {
+#define RMX_NT(n) \
+  case n: return launch_tower_nt<n>(s, p, amode, epi);
+    RMX_NT(1) RMX_NT(2) RMX_NT(3) RMX_NT(4) RMX_NT(5) RMX_NT(6) RMX_NT(7)
+    RMX_NT(8) RMX_NT(10) RMX_NT(13) RMX_NT(16) RMX_NT(20) RMX_NT(25) RMX_NT(26)
+#undef RMX_NT
+    default: set_error("bad tower width"); return RMX_E_INVALID;
+  }
+}
+
+int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
+                     const int32_t* ids, const float* table, const float* u_prev, float* u_out, float* rowdot) {
+  if (B <= 0) return RMX_OK;
+  if (!first && !u_prev) {
+    set_error("cin: missing previous layer maps");
+    return RMX_E_INVALID;
+  }
+  GemmArgs p{};
+  p.M = B * k;
+  p.K = L.Hp_pad * F;
+  p.Kpad = p.K;
+  p.Npad = L.Npad;
+  p.ga = AGatherArgs{ids, table, F, k};
+  p.u_prev = u_prev;
+  p.ldu = L.Hp_pad;
+  p.XS = round_up(std::max(F, first ? L.Hp_pad : 0), 16) + 4;  // 16-B rows; x0 and (layer 1) u
+  p.cin_first = first ? 1 : 0;
+  p.Wp = L.W;
+  p.bias = L.b;
+  p.C = last ? nullptr : u_out;
+  p.ldc = L.Npad;
+  p.wo = L.wo;
+  p.rowdot = rowdot;
+  if (first && L.Hp_pad > p.XS - 4) {
+    set_error("cin: first layer Hp_pad mismatch");
+    return RMX_E_INVALID;
+  }
+  switch (L.Npad / 16) {
+#define RMX_NT(n) \
+  case n: return launch_cin_nt<n>(s, p);
+    RMX_NT(1) RMX_NT(2) RMX_NT(3) RMX_NT(4) RMX_NT(5) RMX_NT(6) RMX_NT(7)
+    RMX_NT(8) RMX_NT(10) RMX_NT(13) RMX_NT(16)
+#undef RMX_NT
+    default:
+      set_error("cin: layer width must be <= 256");
+      return RMX_E_INVALID;
+  }
+}
+
+}  // namespace rmx

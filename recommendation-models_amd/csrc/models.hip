@@ -207,13 +207,14 @@ int model_build(rmx_model& m) {
         off += (int64_t)prev * d + d;
         prev = d;
       }
-      int hp = m.F, sum = 0;
+      int hp = m.F, sum = 0, hp_pad = round_up(m.F, 16);
       for (int h : m.cin) {
         CinLayer c;
         c.Hp = hp;
-        c.Hp_pad = round_up(hp, 16);
+        c.Hp_pad = hp_pad;  // = the previous layer's Npad (its maps' row stride)
         c.H = h;
-        c.Npad = round_up(h, 16);
+        c.Npad = cin_npad_for(h);
+        hp_pad = c.Npad;
         c.w_off = off;
         c.b_off = off + (int64_t)m.F * hp * h;
         off += (int64_t)m.F * hp * h + h;

@@ -12,6 +12,7 @@
 namespace rmx {
 
 void set_error(const std::string& msg);
+int tuning_get(const char* key, int def);  // rmx_set_tuning knobs (capi.hip)
 
 #define RMX_HIP(expr)                                                              \
   do {                                                                             \

@@ -124,4 +124,5 @@ int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const
 int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table, float* xbuf,
                     int ldx);
 int tower_npad_for(int N);
+int cin_npad_for(int H);
 }  // namespace rmx

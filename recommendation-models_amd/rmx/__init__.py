@@ -57,6 +57,15 @@ class CooLongFloatMatrix:
         return self.values
 
 
+def set_tuning(key, value):
+    """Process-wide kernel variant knob (rmx_set_tuning), for A/B timing in one process."""
+    check(_lib.lib.rmx_set_tuning(key.encode(), int(value)))
+
+
+def get_tuning(key, default=0):
+    return int(_lib.lib.rmx_get_tuning(key.encode(), int(default)))
+
+
 # ----------------------------------------------------------------- device ----
 class Context:
     """One GPU + one HIP stream (rmx_ctx)."""

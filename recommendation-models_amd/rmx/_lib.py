@@ -36,6 +36,8 @@ P = ctypes.POINTER
 SIGNATURES = [
     ("rmx_last_error", ctypes.c_char_p, []),
     ("rmx_abi_version", c_int, []),
+    ("rmx_set_tuning", c_int, [ctypes.c_char_p, c_int]),
+    ("rmx_get_tuning", c_int, [ctypes.c_char_p, c_int]),
     ("rmx_ctx_create", c_int, [c_int, P(c_vp)]),
     ("rmx_ctx_destroy", c_int, [c_vp]),
     ("rmx_ctx_stream", c_vp, [c_vp]),

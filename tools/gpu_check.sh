@@ -35,6 +35,10 @@ for s in $STEPS; do
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     profx) run profx 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx" -o xdeepfm -- \
             python3 bench.py --workload xdeepfm --steps 5 --warmup 2 --no-cpu-baseline ;;
+    sq) run pmc_sq 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_sq" -o sq -- \
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+        run pmc_grbm 400 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmc_grbm" -o grbm -- \
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o fetch -- \
             python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
          run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
