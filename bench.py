@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["deepfm", "xdeepfm"], default="deepfm")
+    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded"], default="deepfm")
+    ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -49,6 +50,8 @@ def parse():
 def stage_work(workload, stage, B):
     """Algorithmic work of one launch of a stage: ('flop'|'byte', amount)."""
     D = F * K
+    if stage == "shard_exchange":  # ids out + (k+1)-float rows back, all ranks' shares incl. self
+        return "byte", B * F * (4 + 4 + (K + 1) * 4 * 2)
     if stage == "encoder_fm":  # ids + w + emb rows + y  (SURVEY.md §8d: 2,812 B / example)
         return "byte", B * (F * 4 + F * 4 + F * K * 4 + 4)
     if stage == "first_order":
@@ -70,7 +73,7 @@ def cpu_baseline(workload, budget_s, threads):
     """Oracle (C restatement, OpenMP) on the host cores: examples/s on bounded batches."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ctypes as oc
-    if workload == "deepfm":
+    if workload != "xdeepfm":  # deepfm_sharded: same per-example CPU work (V = 1M table on the host)
         om = oc.make_model(oc.DEEPFM, F, K, fc=tuple(FC))
         B = 4096
     else:
@@ -107,21 +110,32 @@ def main():
         dist.init_process_group("gloo")
     import rmx
 
-    B = args.batch or (65536 if args.workload == "deepfm" else 16384)
+    B = args.batch or (16384 if args.workload == "xdeepfm" else 65536)
+    sharded = args.workload == "deepfm_sharded"
+    Vw = args.vocab or (100_000_000 if sharded else V)
     rmx.set_device(local)
     ctx = rmx.default_context()
     stream = ctx.stream
-    if args.workload == "deepfm":
-        model = rmx.DeepFM(V, F, K, FC, ctx=ctx)
+    if args.workload == "xdeepfm":
+        model = rmx.XDeepFM(Vw, F, K, FC, CIN, ctx=ctx)
     else:
-        model = rmx.XDeepFM(V, F, K, FC, CIN, ctx=ctx)
-    table = rmx.EmbeddingTable(ctx, V, K)
+        model = rmx.DeepFM(Vw, F, K, FC, ctx=ctx)
+    if sharded:
+        # configs[3]: table hash-sharded over the ranks, RCCL exchange per batch
+        uid = rmx.comm_unique_id() if rank == 0 else None
+        if dist:
+            box = [uid]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
+    else:
+        table = rmx.EmbeddingTable(ctx, Vw, K)
     table.fill_synthetic(SEED_TAB)
     model.setMats(model.initMats(SEED_MATS))
     model.setBias(0.01)
     nrows = max(ROWS, B)
     ids = rmx.DeviceArray(ctx, nrows * F, np.int32)
-    rmx.gen_ids(ctx, SEED_IDS, rank * nrows, nrows, F, V, ids)
+    rmx.gen_ids(ctx, SEED_IDS, rank * nrows, nrows, F, Vw, ids)
     out = rmx.DeviceArray(ctx, nrows, np.float32)
     ctx.sync()
     nb = nrows // B
@@ -131,7 +145,10 @@ def main():
 
     def step(i):
         ids_v, out_v = views[i % nb]
-        model.forward_ids(table, B, ids_v, out_v, stream)
+        if sharded:
+            model.forward_ids_sharded(table, B, ids_v, out_v, stream)
+        else:
+            model.forward_ids(table, B, ids_v, out_v, stream)
 
     for i in range(args.warmup):
         step(i)
@@ -214,9 +231,11 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (splitmix64 Criteo-shaped ids, U(-0.05,0.05) table, Xavier mats)",
-            "config": {"workload": "%s_fp32_F39_V1M_k16_fc400x3%s_B%d" % (
-                args.workload, "_cin200x3" if args.workload == "xdeepfm" else "", B),
-                "global_batch": world * B, "rows_per_gpu_set": nrows, "parallelism": "replicas%d" % world},
+            "config": {"workload": "%s_fp32_F39_V%s_k16_fc400x3%s_B%d" % (
+                args.workload, ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
+                "_cin200x3" if args.workload == "xdeepfm" else "", B),
+                "global_batch": world * B, "rows_per_gpu_set": nrows,
+                "parallelism": ("hashshard%d_rccl" % world) if sharded else "replicas%d" % world},
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages": per_stage,

@@ -40,6 +40,7 @@ extern "C" {
 #define RMX_E_HIP (-5)      /* HIP runtime error                                                      */
 #define RMX_E_NOMEM (-6)    /* device allocation failed                                               */
 #define RMX_E_MATS (-7)     /* mats length / matSizes disagree with getMatsSize                       */
+#define RMX_E_COMM (-8)     /* RCCL error in the sharded-table exchange                               */
 
 /* Model kinds: yr/model/{lr,deepfm,xdeepfm,dcn,pnn,dnn}/ */
 #define RMX_MODEL_LR 0
@@ -62,6 +63,7 @@ extern "C" {
 typedef struct rmx_ctx rmx_ctx;
 typedef struct rmx_model rmx_model;
 typedef struct rmx_table rmx_table;
+typedef struct rmx_shard rmx_shard;
 
 /* ------------------------------------------------------------------ misc -- */
 const char* rmx_last_error(void);
@@ -169,6 +171,31 @@ int rmx_model_get_timing(rmx_model* m, char* names, int name_stride, float* ms, 
  * d_y[batch] = y1 + y2 (DeepFM) / y1.  Used to measure the HBM-bound encoder alone. */
 int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32_t* d_ids,
                     float* d_y, void* stream);
+
+/* -------------------------------------------------------- sharded table ---- */
+/* Hash-sharded table over nranks processes, one GPU each (BASELINE.json configs[3]): replaces
+ * the column-range-partitioned Angel PS matrices and their sparse pulls (ParRecModel.scala:74-105,
+ * :165-199).  owner(id) = id mod nranks, local row = id div nranks.  One exchange per batch over
+ * RCCL (grouped send/recv = all-to-all over xGMI): ids to owners, rows back.
+ * rmx_comm_unique_id: rank 0 creates the RCCL id (RMX_UNIQUE_ID_BYTES bytes) and the caller
+ * broadcasts it (e.g. torch.distributed / MPI / Spark broadcast).  unique_id == NULL creates a
+ * LOOPBACK shard: all nranks partitions live in this process on ctx's GPU and the exchange is
+ * in-device (single-GPU testing of the routing at nranks > 1). */
+#define RMX_UNIQUE_ID_BYTES 128
+int rmx_comm_unique_id(void* out, size_t cap);
+int rmx_shard_create(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, int nranks, int rank,
+                     const void* unique_id, rmx_shard** out);
+int rmx_shard_destroy(rmx_shard* sh);
+/* Owned rows from the same generator as rmx_table_fill_synthetic (bit-identical rows). */
+int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);
+int64_t rmx_shard_local_rows(const rmx_shard* sh);
+/* Collective (every rank calls it): d_w[i] = w[ids[i]], d_emb[i*k+j] = emb[ids[i]][j] gathered
+ * from the owners (makeWeights / makeEmbeddings through the exchange).  Bit-exact copies. */
+int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
+                     void* stream);
+/* Collective: L-B forward of this rank's batch (d_ids [batch * nFields]) over the sharded table. */
+int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t batch, const int32_t* d_ids,
+                            float* d_out, void* stream);
 
 #ifdef __cplusplus
 }

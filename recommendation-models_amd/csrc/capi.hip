@@ -87,9 +87,9 @@ extern "C" int rmx_ctx_create(int device, rmx_ctx** out) {
 
 extern "C" int rmx_ctx_destroy(rmx_ctx* c) {
   if (!c) return RMX_OK;
-  hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
-  hipStreamDestroy(c->stream);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamDestroy(c->stream);
   delete c;
   return RMX_OK;
 }
@@ -261,7 +261,7 @@ extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
   t->k = k;
   if (hipMalloc(&t->w, sizeof(float) * V) != hipSuccess ||
       (k > 0 && hipMalloc(&t->emb, sizeof(float) * V * k) != hipSuccess)) {
-    if (t->w) hipFree(t->w);
+    if (t->w) (void)hipFree(t->w);
     delete t;
     set_error("rmx_table_create: out of device memory");
     return RMX_E_NOMEM;
@@ -272,10 +272,10 @@ extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
 
 extern "C" int rmx_table_destroy(rmx_table* t) {
   if (!t) return RMX_OK;
-  hipSetDevice(t->ctx->device);
-  hipStreamSynchronize(t->ctx->stream);
-  if (t->w) hipFree(t->w);
-  if (t->emb) hipFree(t->emb);
+  (void)hipSetDevice(t->ctx->device);
+  (void)hipStreamSynchronize(t->ctx->stream);
+  if (t->w) (void)hipFree(t->w);
+  if (t->emb) (void)hipFree(t->emb);
   delete t;
   return RMX_OK;
 }
@@ -308,7 +308,7 @@ extern "C" int rmx_table_upload(rmx_table* t, const float* weights, const float*
       RMX_HIP(hipMemcpyAsync(tmp, emb, bytes, hipMemcpyHostToDevice, s));
       int st = launch_transpose_kmajor(s, tmp, t->V, t->k, t->emb);
       RMX_HIP(hipStreamSynchronize(s));
-      hipFree(tmp);
+      (void)hipFree(tmp);
       if (st != RMX_OK) return st;
     }
   }

@@ -123,7 +123,7 @@ int dev_alloc(float** p, size_t n) {
 
 template <class T>
 void dev_free(T*& p) {
-  if (p) hipFree(p);
+  if (p) (void)hipFree(p);
   p = nullptr;
 }
 
@@ -354,8 +354,8 @@ void model_init_mats(const rmx_model& m, uint64_t seed, float* mats) {
 
 void model_release(rmx_model& m) {
   if (!m.ctx) return;
-  hipSetDevice(m.ctx->device);
-  hipStreamSynchronize(m.ctx->stream);
+  (void)hipSetDevice(m.ctx->device);
+  (void)hipStreamSynchronize(m.ctx->stream);
   dev_free(m.mats_dev);
   for (auto& L : m.layers) {
     dev_free(L.W);
@@ -384,10 +384,10 @@ void model_release(rmx_model& m) {
   dev_free(m.la_rowptr);
   dev_free(m.la_out);
   for (auto& p : m.pending) {
-    hipEventDestroy(p.a);
-    hipEventDestroy(p.b);
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
   }
-  for (auto e : m.ev_pool) hipEventDestroy(e);
+  for (auto e : m.ev_pool) (void)hipEventDestroy(e);
 }
 
 __global__ void copy_slice_kernel(const float* __restrict__ src, int n, int npad, float* __restrict__ dst) {
@@ -472,44 +472,40 @@ int ensure_ws(rmx_model& m, int B) {
 }
 
 // --- stage timing -----------------------------------------------------------
-hipEvent_t take_event(rmx_model& m) {
+
+}  // namespace
+
+static hipEvent_t take_event(rmx_model& m) {
   if (!m.ev_pool.empty()) {
     hipEvent_t e = m.ev_pool.back();
     m.ev_pool.pop_back();
     return e;
   }
   hipEvent_t e;
-  hipEventCreate(&e);
+  (void)hipEventCreate(&e);
   return e;
 }
 
-struct StageTimer {
-  rmx_model& m;
-  hipStream_t s;
-  int idx = -1;
-  hipEvent_t a = nullptr;
-  StageTimer(rmx_model& mm, hipStream_t ss, const char* name) : m(mm), s(ss) {
-    if (!m.timing) return;
-    auto it = std::find(m.stage_names.begin(), m.stage_names.end(), std::string(name));
-    if (it == m.stage_names.end()) {
-      m.stage_names.push_back(name);
-      m.stage_ms.push_back(0.f);
-      idx = (int)m.stage_names.size() - 1;
-    } else {
-      idx = (int)(it - m.stage_names.begin());
-    }
-    a = take_event(m);
-    hipEventRecord(a, s);
+StageTimer::StageTimer(rmx_model& mm, hipStream_t ss, const char* name) : m(mm), s(ss) {
+  if (!m.timing) return;
+  auto it = std::find(m.stage_names.begin(), m.stage_names.end(), std::string(name));
+  if (it == m.stage_names.end()) {
+    m.stage_names.push_back(name);
+    m.stage_ms.push_back(0.f);
+    idx = (int)m.stage_names.size() - 1;
+  } else {
+    idx = (int)(it - m.stage_names.begin());
   }
-  ~StageTimer() {
-    if (!m.timing) return;
-    hipEvent_t b = take_event(m);
-    hipEventRecord(b, s);
-    m.pending.push_back({idx, a, b});
-  }
-};
+  a = take_event(m);
+  (void)hipEventRecord(a, s);
+}
 
-}  // namespace
+StageTimer::~StageTimer() {
+  if (!m.timing) return;
+  hipEvent_t b = take_event(m);
+  (void)hipEventRecord(b, s);
+  m.pending.push_back({idx, a, b});
+}
 
 int model_collect_timing(rmx_model& m) {
   for (auto& p : m.pending) {

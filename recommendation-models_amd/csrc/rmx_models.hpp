@@ -112,6 +112,18 @@ int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, b
                        float* out);
 int model_collect_timing(rmx_model& m);
 
+// Records HIP events around a stage on stream s when the model's timing is enabled.
+struct StageTimer {
+  rmx_model& m;
+  hipStream_t s;
+  int idx = -1;
+  hipEvent_t a = nullptr;
+  StageTimer(rmx_model& mm, hipStream_t ss, const char* name);
+  ~StageTimer();
+};
+int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* unique_id, rmx_shard** out);
+int shard_destroy(rmx_shard* sh);
+
 // kernels specific to the interaction encoders
 int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L);
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,

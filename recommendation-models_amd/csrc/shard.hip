@@ -1,0 +1,460 @@
+// shard.hip -- hash-sharded embedding table across ranks (one process per GPU), RCCL exchange.
+//
+// Replaces the reference's column-range-partitioned Angel PS matrices and their sparse pulls
+// (ParRecModel.scala:74-105 ColumnRangePartitioner, pull :165-199, make* :279-306) for tables
+// that are sharded over GPUs (BASELINE.json configs[3]: V = 100M over 8 x MI355X).
+//
+// Partitioning: owner(id) = id mod N, local row = id div N (Criteo ids are feature hashes, so
+// modulo partitioning balances; it is a bijection [0, V) -> [N] x [ceil(V/N)]).
+// One exchange step per batch on the caller's stream:
+//   1. route   : per id, owner o and a slot in o's send bucket (block-local LDS histogram + one
+//                global atomic per (block, owner) to reserve a range); send_ids[slot] = local row,
+//                perm[n] = slot.  Copies only, so the bucket order inside a range is irrelevant.
+//   2. counts  : grouped ncclSend/ncclRecv of one int per peer, then one D2H of the 2N counts
+//                (the only host sync: NCCL needs host-side message sizes).
+//   3. ids     : grouped send/recv of each bucket to its owner.
+//   4. gather  : the owner copies emb[local][0..k) and w[local] for every received id.
+//   5. rows    : grouped send/recv of the rows back, into the requester's bucket order.
+//   6. forward : the model runs on (ids = perm, table = received rows): every kernel already
+//                gathers through an id list, so nothing else changes and the outputs are bitwise
+//                those of the replicated table (tests/test_shard.py).
+// A "loopback" shard (unique_id == NULL) keeps all N partitions in this process on one GPU and
+// replaces steps 2-5's transport by in-place reads: it exercises the routing and owner-gather
+// kernels at N > 1 on a single device.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "rmx_models.hpp"
+
+#define RMX_NCCL(expr)                                                                          \
+  do {                                                                                          \
+    ncclResult_t _r = (expr);                                                                   \
+    if (_r != ncclSuccess) {                                                                    \
+      ::rmx::set_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " __FILE__ ":" + \
+                       std::to_string(__LINE__) + ": " #expr);                                   \
+      return RMX_E_COMM;                                                                        \
+    }                                                                                           \
+  } while (0)
+
+struct rmx_shard {
+  rmx_ctx* ctx = nullptr;
+  int64_t V = 0;
+  int k = 0, N = 1, rank = 0;
+  bool loopback = false;
+  ncclComm_t comm = nullptr;
+  int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
+  std::vector<float*> emb, w;           // partitions held here: [rows_per][k], [rows_per] (loopback: N)
+  // per-batch buffers (grow only)
+  int64_t cap_send = 0, cap_recv = 0;
+  int32_t* counts = nullptr;            // [4N]: send counts, recv counts, cursors, scratch
+  int32_t* h_counts = nullptr;          // pinned host [2N]
+  int32_t* send_ids = nullptr;          // [nnz] local rows, bucketed by owner
+  int32_t* perm = nullptr;              // [nnz] slot of id n
+  int32_t* recv_ids = nullptr;          // [recv] local rows requested from this rank
+  float* send_emb = nullptr;            // [recv][k] rows gathered for requesters
+  float* send_w = nullptr;              // [recv]
+  float* recv_emb = nullptr;            // [nnz][k] rows for this rank's batch (bucket order)
+  float* recv_w = nullptr;              // [nnz]
+};
+
+namespace rmx {
+
+namespace {
+
+constexpr int kRouteThreads = 256, kRoutePer = 8, kMaxRanks = 64;
+
+// counts[o] += number of ids owned by o (block histogram in LDS, one global atomic per owner)
+__global__ __launch_bounds__(kRouteThreads) void route_count_kernel(int64_t nnz, int N, const int32_t* __restrict__ ids,
+                                                                   int32_t* __restrict__ counts) {
+  __shared__ int h[kMaxRanks];
+  for (int i = threadIdx.x; i < N; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRouteThreads * kRoutePer;
+#pragma unroll
+  for (int u = 0; u < kRoutePer; ++u) {
+    const int64_t n = base + u * kRouteThreads + threadIdx.x;
+    if (n < nnz) atomicAdd(&h[ids[n] % N], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += blockDim.x)
+    if (h[i]) atomicAdd(&counts[i], h[i]);
+}
+
+// slot of id n = exclusive_scan(counts)[o] + (range reserved by this block for o) + rank in block
+__global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nnz, int N, const int32_t* __restrict__ ids,
+                                                                     const int32_t* __restrict__ counts,
+                                                                     int32_t* __restrict__ cursor,
+                                                                     int32_t* __restrict__ send_ids,
+                                                                     int32_t* __restrict__ perm) {
+  __shared__ int h[kMaxRanks], start[kMaxRanks], off[kMaxRanks];
+  for (int i = threadIdx.x; i < N; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRouteThreads * kRoutePer;
+  int own[kRoutePer], loc[kRoutePer], rk[kRoutePer];
+#pragma unroll
+  for (int u = 0; u < kRoutePer; ++u) {
+    const int64_t n = base + u * kRouteThreads + threadIdx.x;
+    own[u] = -1;
+    if (n < nnz) {
+      const int id = ids[n];
+      own[u] = id % N;
+      loc[u] = id / N;
+      rk[u] = atomicAdd(&h[own[u]], 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int o = 0; o < N; ++o) {
+      off[o] = s;
+      s += counts[o];
+    }
+  }
+  for (int o = threadIdx.x; o < N; o += blockDim.x) start[o] = h[o] ? atomicAdd(&cursor[o], h[o]) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kRoutePer; ++u) {
+    const int64_t n = base + u * kRouteThreads + threadIdx.x;
+    if (own[u] >= 0) {
+      const int slot = off[own[u]] + start[own[u]] + rk[u];
+      send_ids[slot] = loc[u];
+      perm[n] = slot;
+    }
+  }
+}
+
+// rows for requested local ids: 4 lanes per row at k = 16 (one float4 each), generic otherwise
+__global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, int k, const int32_t* __restrict__ rows,
+                                                          const float* __restrict__ emb, const float* __restrict__ w,
+                                                          float* __restrict__ out_emb, float* __restrict__ out_w) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 16) {
+    const int64_t i = t >> 2;
+    const int c = (int)(t & 3);
+    if (i >= n) return;
+    const int r = rows[i];
+    reinterpret_cast<float4*>(out_emb)[i * 4 + c] = reinterpret_cast<const float4*>(emb)[(int64_t)r * 4 + c];
+    if (c == 0) out_w[i] = w[r];
+    return;
+  }
+  if (t >= n) return;
+  const int r = rows[t];
+  for (int j = 0; j < k; ++j) out_emb[t * k + j] = emb[(int64_t)r * k + j];
+  out_w[t] = w[r];
+}
+
+__device__ __forceinline__ uint64_t splitmix64_d(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+// owned rows of partition `part`: global id = l*N + part, values of the global generator
+// (oracle orc_gen_table / fill_table_kernel): bit-identical to the replicated table's rows
+__global__ void shard_fill_kernel(uint64_t seed, int64_t V, int64_t rows_per, int N, int part, int k,
+                                  float scale, float* __restrict__ emb, float* __restrict__ w) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows_per * (k + 1)) return;
+  const int64_t l = i / (k + 1);
+  const int j = (int)(i - l * (k + 1));
+  const int64_t id = l * N + part;
+  float v = 0.f;
+  if (id < V) {
+    const uint64_t h = splitmix64_d(seed ^ (uint64_t)(id * (k + 1) + j));
+    v = (float)((int32_t)(h >> 40) - 8388608) * scale;
+  }
+  if (j < k) emb[l * k + j] = v;
+  else w[l] = v;
+}
+
+}  // namespace
+
+namespace {
+
+template <class T>
+int realloc_dev(T** p, int64_t n) {
+  if (*p) RMX_HIP(hipFree(*p));
+  *p = nullptr;
+  if (hipMalloc((void**)p, sizeof(T) * std::max<int64_t>(n, 1)) != hipSuccess) {
+    set_error("shard: out of device memory (" + std::to_string(n * (int64_t)sizeof(T)) + " bytes)");
+    return RMX_E_NOMEM;
+  }
+  return RMX_OK;
+}
+
+// [nnz]-sized buffers of this rank's batch
+int ensure_batch(rmx_shard& sh, int64_t nnz) {
+  if (nnz <= sh.cap_send) return RMX_OK;
+  RMX_HIP(hipStreamSynchronize(sh.ctx->stream));
+  int st;
+  if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.perm, nnz)) ||
+      (st = realloc_dev(&sh.recv_emb, nnz * sh.k)) || (st = realloc_dev(&sh.recv_w, nnz)))
+    return st;
+  sh.cap_send = nnz;
+  return RMX_OK;
+}
+
+// [received]-sized buffers of the owner side
+int ensure_recv(rmx_shard& sh, int64_t n) {
+  if (n <= sh.cap_recv) return RMX_OK;
+  int st;
+  if ((st = realloc_dev(&sh.recv_ids, n)) || (st = realloc_dev(&sh.send_emb, n * sh.k)) ||
+      (st = realloc_dev(&sh.send_w, n)))
+    return st;
+  sh.cap_recv = n;
+  return RMX_OK;
+}
+
+int launch_owner_gather(hipStream_t s, int64_t n, int k, const int32_t* rows, const float* emb, const float* w,
+                        float* out_emb, float* out_w) {
+  if (n <= 0) return RMX_OK;
+  const int64_t threads = k == 16 ? n * 4 : n;
+  hipLaunchKernelGGL(owner_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, k, rows, emb,
+                     w, out_emb, out_w);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+}  // namespace
+
+int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* unique_id, rmx_shard** out) {
+  if (N < 1 || N > kMaxRanks || rank < 0 || rank >= N || V < N || k <= 0) {
+    set_error("rmx_shard_create: bad arguments (need 1 <= nranks <= 64, 0 <= rank < nranks, rows >= nranks)");
+    return RMX_E_INVALID;
+  }
+  if (V >= (int64_t(1) << 31)) {
+    set_error("rmx_shard_create: rows must fit int32 (ParRecModel.scala:282 .toInt)");
+    return RMX_E_INVALID;
+  }
+  RMX_HIP(hipSetDevice(ctx->device));
+  std::unique_ptr<rmx_shard> sh(new rmx_shard());
+  sh->ctx = ctx;
+  sh->V = V;
+  sh->k = k;
+  sh->N = N;
+  sh->rank = rank;
+  sh->loopback = unique_id == nullptr;
+  sh->rows_per = (V + N - 1) / N;
+  const int parts = sh->loopback ? N : 1;
+  for (int p = 0; p < parts; ++p) {
+    float *e = nullptr, *w = nullptr;
+    if (hipMalloc(&e, sizeof(float) * sh->rows_per * k) != hipSuccess ||
+        hipMalloc(&w, sizeof(float) * sh->rows_per) != hipSuccess) {
+      if (e) (void)hipFree(e);
+      for (size_t i = 0; i < sh->emb.size(); ++i) {
+        (void)hipFree(sh->emb[i]);
+        (void)hipFree(sh->w[i]);
+      }
+      set_error("rmx_shard_create: out of device memory for the partition");
+      return RMX_E_NOMEM;
+    }
+    sh->emb.push_back(e);
+    sh->w.push_back(w);
+  }
+  RMX_HIP(hipMalloc(&sh->counts, sizeof(int32_t) * 4 * N));
+  RMX_HIP(hipHostMalloc(&sh->h_counts, sizeof(int32_t) * 2 * N));
+  if (!sh->loopback) {
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof(id));
+    RMX_NCCL(ncclCommInitRank(&sh->comm, N, id, rank));
+  }
+  *out = sh.release();
+  return RMX_OK;
+}
+
+int shard_destroy(rmx_shard* sh) {
+  if (!sh) return RMX_OK;
+  (void)hipSetDevice(sh->ctx->device);
+  (void)hipStreamSynchronize(sh->ctx->stream);
+  if (sh->comm) ncclCommDestroy(sh->comm);
+  for (size_t i = 0; i < sh->emb.size(); ++i) {
+    (void)hipFree(sh->emb[i]);
+    (void)hipFree(sh->w[i]);
+  }
+  for (void* p : {(void*)sh->counts, (void*)sh->send_ids, (void*)sh->perm, (void*)sh->recv_ids,
+                  (void*)sh->send_emb, (void*)sh->send_w, (void*)sh->recv_emb, (void*)sh->recv_w})
+    if (p) (void)hipFree(p);
+  if (sh->h_counts) (void)hipHostFree(sh->h_counts);
+  delete sh;
+  return RMX_OK;
+}
+
+int shard_fill_synthetic(rmx_shard& sh, uint64_t seed) {
+  RMX_HIP(hipSetDevice(sh.ctx->device));
+  hipStream_t s = sh.ctx->stream;
+  const float scale = 0.05f * (1.0f / 8388608.0f);
+  const int64_t tot = sh.rows_per * (sh.k + 1);
+  for (size_t p = 0; p < sh.emb.size(); ++p) {
+    const int part = sh.loopback ? (int)p : sh.rank;
+    hipLaunchKernelGGL(shard_fill_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, sh.V,
+                       sh.rows_per, sh.N, part, sh.k, scale, sh.emb[p], sh.w[p]);
+    RMX_HIP(hipGetLastError());
+  }
+  RMX_HIP(hipStreamSynchronize(s));
+  return RMX_OK;
+}
+
+// Steps 1-5 of the exchange: fills sh.perm / sh.recv_emb / sh.recv_w for this rank's batch.
+int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids) {
+  const int N = sh.N, k = sh.k;
+  int st;
+  if ((st = ensure_batch(sh, nnz))) return st;
+  int32_t* cnt = sh.counts;           // [N] send counts
+  int32_t* rcnt = sh.counts + N;      // [N] recv counts
+  int32_t* cursor = sh.counts + 2 * N;
+  RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
+  if (nnz > 0) {
+    const unsigned nb = (unsigned)((nnz + kRouteThreads * kRoutePer - 1) / (kRouteThreads * kRoutePer));
+    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, nnz, N, d_ids, cnt);
+    RMX_HIP(hipGetLastError());
+    hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, nnz, N, d_ids, cnt, cursor,
+                       sh.send_ids, sh.perm);
+    RMX_HIP(hipGetLastError());
+  }
+  if (!sh.comm) {
+    // loopback: partition o serves bucket o in place
+    RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * N, hipMemcpyDeviceToHost, s));
+    RMX_HIP(hipStreamSynchronize(s));
+    int64_t off = 0;
+    for (int o = 0; o < N; ++o) {
+      const int64_t c = sh.h_counts[o];
+      if ((st = launch_owner_gather(s, c, k, sh.send_ids + off, sh.emb[o], sh.w[o], sh.recv_emb + off * k,
+                                    sh.recv_w + off)))
+        return st;
+      off += c;
+    }
+    return RMX_OK;
+  }
+  // 2. counts
+  RMX_NCCL(ncclGroupStart());
+  for (int o = 0; o < N; ++o) {
+    RMX_NCCL(ncclSend(cnt + o, 1, ncclInt32, o, sh.comm, s));
+    RMX_NCCL(ncclRecv(rcnt + o, 1, ncclInt32, o, sh.comm, s));
+  }
+  RMX_NCCL(ncclGroupEnd());
+  RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * 2 * N, hipMemcpyDeviceToHost, s));
+  RMX_HIP(hipStreamSynchronize(s));
+  const int32_t* hc = sh.h_counts;
+  const int32_t* hr = sh.h_counts + N;
+  int64_t nrecv = 0;
+  for (int o = 0; o < N; ++o) nrecv += hr[o];
+  if ((st = ensure_recv(sh, nrecv))) return st;
+  // 3. ids to owners
+  RMX_NCCL(ncclGroupStart());
+  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += hr[o], ++o) {
+    if (hc[o]) RMX_NCCL(ncclSend(sh.send_ids + so, hc[o], ncclInt32, (int)o, sh.comm, s));
+    if (hr[o]) RMX_NCCL(ncclRecv(sh.recv_ids + ro, hr[o], ncclInt32, (int)o, sh.comm, s));
+  }
+  RMX_NCCL(ncclGroupEnd());
+  // 4. owner gather
+  if ((st = launch_owner_gather(s, nrecv, k, sh.recv_ids, sh.emb[0], sh.w[0], sh.send_emb, sh.send_w))) return st;
+  // 5. rows back, into the requester's bucket order
+  RMX_NCCL(ncclGroupStart());
+  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += hr[o], ++o) {
+    if (hr[o]) {
+      RMX_NCCL(ncclSend(sh.send_emb + ro * k, (size_t)hr[o] * k, ncclFloat32, (int)o, sh.comm, s));
+      RMX_NCCL(ncclSend(sh.send_w + ro, hr[o], ncclFloat32, (int)o, sh.comm, s));
+    }
+    if (hc[o]) {
+      RMX_NCCL(ncclRecv(sh.recv_emb + so * k, (size_t)hc[o] * k, ncclFloat32, (int)o, sh.comm, s));
+      RMX_NCCL(ncclRecv(sh.recv_w + so, hc[o], ncclFloat32, (int)o, sh.comm, s));
+    }
+  }
+  RMX_NCCL(ncclGroupEnd());
+  return RMX_OK;
+}
+
+}  // namespace rmx
+
+// ------------------------------------------------------------------ C ABI --
+using namespace rmx;
+
+extern "C" int rmx_comm_unique_id(void* out, size_t cap) {
+  if (!out || cap < sizeof(ncclUniqueId)) {
+    set_error("rmx_comm_unique_id: buffer must hold RMX_UNIQUE_ID_BYTES bytes");
+    return RMX_E_INVALID;
+  }
+  ncclUniqueId id;
+  RMX_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof(id));
+  return RMX_OK;
+}
+
+extern "C" int rmx_shard_create(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, int nranks, int rank,
+                                const void* unique_id, rmx_shard** out) {
+  if (!ctx || !out) {
+    set_error("rmx_shard_create: bad args");
+    return RMX_E_INVALID;
+  }
+  return shard_create(ctx, num_rows, embedding_dim, nranks, rank, unique_id, out);
+}
+
+extern "C" int rmx_shard_destroy(rmx_shard* sh) { return shard_destroy(sh); }
+
+extern "C" int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed) {
+  if (!sh) {
+    set_error("rmx_shard_fill_synthetic: NULL shard");
+    return RMX_E_INVALID;
+  }
+  return shard_fill_synthetic(*sh, seed);
+}
+
+extern "C" int64_t rmx_shard_local_rows(const rmx_shard* sh) { return sh ? sh->rows_per : -1; }
+
+extern "C" int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
+                                void* stream) {
+  if (!sh || (!d_ids && n > 0) || n < 0 || (n > 0 && (!d_w || !d_emb))) {
+    set_error("rmx_shard_gather: bad args");
+    return RMX_E_INVALID;
+  }
+  RMX_HIP(hipSetDevice(sh->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : sh->ctx->stream;
+  int st = shard_exchange(*sh, s, n, d_ids);
+  if (st) return st;
+  // un-permute into id order: d_emb[i] = recv_emb[perm[i]]
+  return launch_owner_gather(s, n, sh->k, sh->perm, sh->recv_emb, sh->recv_w, d_emb, d_w);
+}
+
+extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, const int32_t* d_ids, float* d_out,
+                                       void* stream) {
+  if (!m || !sh || !d_out || B < 0 || (!d_ids && B > 0) || !m->ctx) {
+    set_error("rmx_forward_ids_sharded: bad args");
+    return RMX_E_INVALID;
+  }
+  if (!m->params_ready && m->mats_len > 0) {
+    set_error("rmx_forward_ids_sharded: call rmx_model_set_mats first");
+    return RMX_E_INVALID;
+  }
+  if (!m->beta_set) {
+    set_error("rmx_forward_ids_sharded: call rmx_model_set_bias first");
+    return RMX_E_INVALID;
+  }
+  if (m->type != RMX_MODEL_LR && sh->k != m->k) {
+    set_error("rmx_forward_ids_sharded: table embedding_dim differs from the model's");
+    return RMX_E_SHAPE;
+  }
+  RMX_HIP(hipSetDevice(m->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  int st;
+  {
+    StageTimer t(*m, s, "shard_exchange");
+    st = shard_exchange(*sh, s, (int64_t)B * m->F, d_ids);
+  }
+  if (st) return st;
+  if (m->timing) ++m->timed_calls;  // model_forward counts it again; undone below
+  FwdInputs in;
+  in.B = B;
+  in.ids = sh->perm;
+  in.table = sh->recv_emb;
+  in.wtab = sh->recv_w;
+  in.beta = m->beta;
+  in.out = d_out;
+  st = model_forward(*m, s, in);
+  if (m->timing) --m->timed_calls;
+  return st;
+}

@@ -21,7 +21,7 @@ from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT
 import ctypes
 
 __all__ = ["RecModelType", "CooLongFloatMatrix", "RecModel", "LR", "DeepFM", "XDeepFM", "DCN", "PNN", "DNN",
-           "Context", "DeviceArray", "EmbeddingTable", "SampleParser", "RmxError", "IllegalArgumentError",
+           "Context", "DeviceArray", "EmbeddingTable", "ShardedTable", "comm_unique_id", "SampleParser", "RmxError", "IllegalArgumentError",
            "ShapeError", "MatsError", "default_context", "set_device"]
 
 MODEL_LR, MODEL_DEEPFM, MODEL_XDEEPFM, MODEL_DCN, MODEL_PNN, MODEL_DNN = range(6)
@@ -213,6 +213,56 @@ class EmbeddingTable:
             pass
 
 
+def comm_unique_id():
+    """RCCL unique id (bytes) for rmx.ShardedTable; rank 0 creates it, the caller broadcasts it."""
+    buf = ctypes.create_string_buffer(_lib.UNIQUE_ID_BYTES)
+    check(_lib.lib.rmx_comm_unique_id(buf, _lib.UNIQUE_ID_BYTES))
+    return buf.raw
+
+
+class ShardedTable:
+    """Hash-sharded table (owner = id mod nranks) over nranks processes, one GPU each, exchanging ids
+    and rows over RCCL (replaces the PS partitions + sparse pulls, ParRecModel.scala:74-105, :165-199).
+    unique_id=None makes a loopback shard: all partitions in this process (single-GPU testing)."""
+
+    def __init__(self, ctx, num_rows, embedding_dim, nranks, rank=0, unique_id=None):
+        h = ctypes.c_void_p()
+        uid = None
+        if unique_id is not None:
+            if len(unique_id) != _lib.UNIQUE_ID_BYTES:
+                raise ValueError("unique_id must have %d bytes" % _lib.UNIQUE_ID_BYTES)
+            uid = ctypes.create_string_buffer(bytes(unique_id), _lib.UNIQUE_ID_BYTES)
+        check(_lib.lib.rmx_shard_create(ctx.handle, int(num_rows), int(embedding_dim), int(nranks), int(rank),
+                                        uid, ctypes.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+        self.rows = int(num_rows)
+        self.k = int(embedding_dim)
+        self.nranks = int(nranks)
+        self.rank = int(rank)
+
+    def fill_synthetic(self, seed):
+        check(_lib.lib.rmx_shard_fill_synthetic(self.handle, int(seed)))
+
+    def local_rows(self):
+        return int(_lib.lib.rmx_shard_local_rows(self.handle))
+
+    def gather(self, ids_dev, n, w_out, emb_out, stream=None):
+        """Collective: rows of ids_dev from their owners (bit-exact copies)."""
+        check(_lib.lib.rmx_shard_gather(self.handle, int(n), ids_dev.ptr, w_out.ptr, emb_out.ptr, stream))
+
+    def close(self):
+        if self.handle:
+            _lib.lib.rmx_shard_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def gen_ids(ctx, seed, row0, batch, n_fields, num_rows, ids_dev, stream=None):
     """Synthetic field-partitioned ids straight into HBM (SURVEY.md §8d generator)."""
     check(_lib.lib.rmx_gen_ids(ctx.handle, int(seed), int(row0), int(batch), int(n_fields), int(num_rows),
@@ -330,6 +380,11 @@ class RecModel:
     def forward_ids(self, table, batch, ids_dev, out_dev, stream=None):
         """L-B forward: ids [batch * nFields] int32 and out [batch] float32 are DeviceArrays."""
         check(_lib.lib.rmx_forward_ids(self._device(), table.handle, int(batch), ids_dev.ptr, out_dev.ptr, stream))
+
+    def forward_ids_sharded(self, shard, batch, ids_dev, out_dev, stream=None):
+        """Collective L-B forward over a ShardedTable (every rank calls it with its own batch)."""
+        check(_lib.lib.rmx_forward_ids_sharded(self._device(), shard.handle, int(batch), ids_dev.ptr, out_dev.ptr,
+                                               stream))
 
     def encoder_ids(self, table, batch, ids_dev, y_dev, stream=None):
         check(_lib.lib.rmx_encoder_ids(self._device(), table.handle, int(batch), ids_dev.ptr, y_dev.ptr, stream))

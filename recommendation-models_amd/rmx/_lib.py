@@ -17,6 +17,8 @@ RMX_E_TYPE = -4
 RMX_E_HIP = -5
 RMX_E_NOMEM = -6
 RMX_E_MATS = -7
+RMX_E_COMM = -8
+UNIQUE_ID_BYTES = 128
 
 LAYOUT_K_MAJOR = 0
 LAYOUT_ROW_MAJOR = 1
@@ -75,6 +77,13 @@ SIGNATURES = [
     ("rmx_model_set_timing", c_int, [c_vp, c_int]),
     ("rmx_model_get_timing", c_int, [c_vp, ctypes.c_char_p, c_int, P(c_f32), c_int, P(c_int), P(c_int)]),
     ("rmx_encoder_ids", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
+    ("rmx_comm_unique_id", c_int, [c_vp, c_sz]),
+    ("rmx_shard_create", c_int, [c_vp, c_i64, c_int, c_int, c_int, c_vp, P(c_vp)]),
+    ("rmx_shard_destroy", c_int, [c_vp]),
+    ("rmx_shard_fill_synthetic", c_int, [c_vp, c_u64]),
+    ("rmx_shard_local_rows", c_i64, [c_vp]),
+    ("rmx_shard_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    ("rmx_forward_ids_sharded", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
 ]
 
 for _name, _res, _args in SIGNATURES:

@@ -1,0 +1,148 @@
+"""Hash-sharded table (include/rmx.h rmx_shard_*, csrc/shard.hip; BASELINE.json configs[3]).
+
+CPU (gloo, world_size 2): the exchange protocol restated in tests/shard_ref.py over a real
+torch.distributed all-to-all reproduces the global table's rows bit-exactly and the same forward.
+GPU: librmx's sharded path gives BITWISE the outputs of the replicated table -- the exchange only
+copies rows -- for loopback shards (N partitions on one GPU: routing / owner gather at N > 1) and for
+an RCCL communicator of one rank (the grouped send/recv code path).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+
+F, K = 39, 16
+SEED_IDS, SEED_TAB, SEED_MATS = 0x5EED2026, 0x7AB1E, 0x3A75
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_exchange_protocol_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+    import shard_ref
+    V, k, B, F_ = 5003, 8, 37, 5
+    mp.spawn(shard_ref.worker, args=(2, _free_port(), V, k, B, F_, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        ok = np.load(os.path.join(tmp_path, "rank%d.npy" % r))
+        assert ok.tolist() == [1, 1, 1], (r, ok)
+
+
+def test_route_is_a_bijection():
+    import shard_ref
+    ids = np.random.default_rng(0).integers(0, 1000, 5000)
+    for N in (1, 2, 3, 8):
+        counts, send_ids, perm = shard_ref.route(ids, N)
+        assert counts.sum() == len(ids) and sorted(perm.tolist()) == list(range(len(ids)))
+        owner_of_slot = np.repeat(np.arange(N), counts)
+        assert np.array_equal(owner_of_slot[perm], ids % N)
+        assert np.array_equal(send_ids[perm] * N + ids % N, ids)
+
+
+# ------------------------------------------------------------------ GPU ----
+def _setup(ctx, V, B, seed_row=0):
+    import rmx
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, seed_row, B, F, V, ids)
+    return table, ids
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 2, 3, 8])
+def test_loopback_shard_gather_bit_exact(N):
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 100_003, 300
+    _, ids = _setup(ctx, V, B)
+    sh = rmx.ShardedTable(ctx, V, K, N)
+    sh.fill_synthetic(SEED_TAB)
+    n = B * F
+    w = rmx.DeviceArray(ctx, n, np.float32)
+    e = rmx.DeviceArray(ctx, n * K, np.float32)
+    sh.gather(ids, n, w, e)
+    ctx.sync()
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    w_ref, e_ref = oc.gather(wt, et, 1, ids.numpy().astype(np.int64))
+    assert np.array_equal(w.numpy(), w_ref) and np.array_equal(e.numpy(), e_ref)
+
+
+def _models():
+    import rmx
+    V = 100_003
+    return {
+        "deepfm": lambda: rmx.DeepFM(V, F, K, [400, 400, 400]),
+        "xdeepfm": lambda: rmx.XDeepFM(V, F, K, [64, 32], [48, 32]),
+        "dcn": lambda: rmx.DCN(V, F, K, 3, [64, 32]),
+        "pnn": lambda: rmx.PNN(V, F, K, [48, 32]),
+        "lr": lambda: rmx.LR(V, F),
+    }
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn", "pnn", "lr"])
+@pytest.mark.parametrize("N", [1, 4, 8])
+def test_sharded_forward_bitwise_equals_replicated(kind, N):
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 100_003, 1000
+    table, ids = _setup(ctx, V, B, seed_row=11)
+    m = _models()[kind]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, N)
+    sh.fill_synthetic(SEED_TAB)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    got = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids, ref)
+    m.forward_ids_sharded(sh, B, ids, got)
+    ctx.sync()
+    assert np.array_equal(got.numpy(), ref.numpy())
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_shard_matches_replicated():
+    """The RCCL code path (grouped send/recv to self) on a one-rank communicator."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 200_000, 2048
+    table, ids = _setup(ctx, V, B, seed_row=3)
+    m = rmx.DeepFM(V, F, K, [400, 400, 400])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, 1, 0, rmx.comm_unique_id())
+    sh.fill_synthetic(SEED_TAB)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    got = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids, ref)
+    for _ in range(2):  # buffers are reused across batches
+        m.forward_ids_sharded(sh, B, ids, got)
+    ctx.sync()
+    assert np.array_equal(got.numpy(), ref.numpy())
+    n = 777
+    w = rmx.DeviceArray(ctx, n, np.float32)
+    e = rmx.DeviceArray(ctx, n * K, np.float32)
+    sh.gather(ids, n, w, e)
+    ctx.sync()
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    w_ref, e_ref = oc.gather(wt, et, 1, ids.numpy()[:n].astype(np.int64))
+    assert np.array_equal(w.numpy(), w_ref) and np.array_equal(e.numpy(), e_ref)
+
+
+@pytest.mark.gpu
+def test_shard_bad_args():
+    import rmx
+    ctx = rmx.default_context()
+    with pytest.raises(rmx.RmxError):
+        rmx.ShardedTable(ctx, 10, K, 0)
+    with pytest.raises(rmx.RmxError):
+        rmx.ShardedTable(ctx, 10, K, 2, 2)

@@ -31,6 +31,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     benchx) run bench_xdeepfm 400 python bench.py --workload xdeepfm --no-cpu-baseline ;;
+    benchs) run bench_sharded 400 python bench.py --workload deepfm_sharded --no-cpu-baseline ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o deepfm -- \
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     profx) run profx 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx" -o xdeepfm -- \
