@@ -57,22 +57,53 @@ struct GemmArgs {
   float* rowdot;       // kEpiCin: [M]
 };
 
-template <int MT, int NT, int WM, int BKC, int AMODE, int EPI>
-__global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
-  constexpr int BM = WM * MT * 16, BN = NT * 16, NTHR = WM * 64;
+// Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
+// tiles); the block spans BM = WM*MT*16 rows and BN = WN*NTW*16 columns.  BKC 16-wide K chunks per
+// LDS stage.  OCC = minimum waves per SIMD the register allocation must allow (launch bounds).
+template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_>
+struct Tile {
+  static constexpr int MT = MT_, NTW = NTW_, WM = WM_, WN = WN_, BKC = BKC_, OCC = OCC_;
+  static constexpr int NW = WM * WN, NTHR = NW * 64, NT = NTW * WN;
+  static constexpr int BM = WM * MT * 16, BN = NT * 16;
+};
+
+template <class T, int AMODE>
+struct StageGeom {
+  static constexpr int AROWS = AMODE != kCinOuter ? T::BM * T::BKC : 0;
+  static constexpr int ROWS = AROWS + T::BN * T::BKC;  // 64-B rows per stage
+  static constexpr int FLOATS = ROWS * 16;
+};
+
+// Epilogue slab geometry: each wave transposes NTH of its column tiles at a time through a
+// private [RW][LD] fp32 slab carved from the (then idle) stage buffers, or more LDS if needed.
+template <class T, int STAGE_FLOATS>
+struct EpiGeom {
+  static constexpr int RW = T::MT * 16;
+  static constexpr int WF = (2 * STAGE_FLOATS) / T::NW;
+  static constexpr int NTH0 = (WF / RW - 4) / 16;
+  static constexpr int NTH = NTH0 < T::NTW ? (NTH0 < 1 ? 1 : NTH0) : T::NTW;
+  static constexpr int LD = NTH * 16 + 4;  // == 4 mod 8: the two 16-lane halves of a write hit disjoint banks
+  static constexpr int FLOATS = RW * LD * T::NW;
+};
+
+template <class T, int AMODE, int EPI>
+__global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
+  constexpr int MT = T::MT, NTW = T::NTW, WN = T::WN, BKC = T::BKC;
+  constexpr int BM = T::BM, BN = T::BN, NTHR = T::NTHR;
   constexpr bool A_LDS = AMODE != kCinOuter;
-  constexpr int AROWS = A_LDS ? BM * BKC : 0, ROWS = AROWS + BN * BKC;  // 64-B rows per stage
-  constexpr int ITEMS = ROWS * 4;                                       // float4 items per stage
+  using SG = StageGeom<T, AMODE>;
+  constexpr int AROWS = SG::AROWS, ROWS = SG::ROWS, STAGE = SG::FLOATS;
+  constexpr int ITEMS = ROWS * 4;  // float4 items per stage
   constexpr int PER = (ITEMS + NTHR - 1) / NTHR;
-  constexpr int STAGE = ROWS * 16;                                      // floats per stage
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lds0 = smem;
   float* lds1 = smem + STAGE;
-  float* extra = smem + 2 * STAGE;                 // gather: int ids [BM][F]; CIN: x0 [BM][XS]
+  float* extra = smem + 2 * STAGE;  // gather: int ids [BM][F]; CIN: x0 [BM][XS]
   int* sids = reinterpret_cast<int*>(extra);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int M = p.M;
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
@@ -112,11 +143,11 @@ __global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
     __syncthreads();
   }
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[MT][NTW];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   float4 stage[PER];
   // item i of a stage: row = i >> 2 (A rows first: [BKC][BM], then B rows [BKC][BN]), slot g = i & 3
@@ -171,7 +202,8 @@ __global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
   const int g = lane >> 4, r16 = lane & 15;
   int arow[MT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) arow[i] = wid * MT * 16 + i * 16 + r16;
+  for (int i = 0; i < MT; ++i) arow[i] = wm * MT * 16 + i * 16 + r16;
+  const int bt0 = wn * NTW;  // first column tile of this wave
 
   // kCinOuter: the row's u[h-chunk] for the current hc, reloaded when hc changes
   float4 uf[MT];
@@ -200,48 +232,42 @@ __global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
       const int c = st * BKC + cc;
       if (BKC > 1 && c >= nchunks) break;
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
-      float4 a[MT];
+      f32x4 a[MT];
       if constexpr (A_LDS) {
         const float* At = cur + cc * BM * 16;
 #pragma unroll
         for (int i = 0; i < MT; ++i)
-          a[i] = *reinterpret_cast<const float4*>(At + arow[i] * 16 + swz_slot(arow[i], g) * 4);
+          a[i] = *reinterpret_cast<const f32x4*>(At + arow[i] * 16 + swz_slot(arow[i], g) * 4);
       } else {
         const int hc = c / F, f = c - hc * F;
         if (hc != cur_hc) load_u(hc);
 #pragma unroll
         for (int i = 0; i < MT; ++i) {
           const float xv = extra[arow[i] * p.XS + f];
-          a[i] = make_float4(xv * uf[i].x, xv * uf[i].y, xv * uf[i].z, xv * uf[i].w);
+          a[i] = f32x4{xv * uf[i].x, xv * uf[i].y, xv * uf[i].z, xv * uf[i].w};
         }
       }
+      // groups of >= 4 independent accumulator tiles: consecutive MFMAs of one tile are a group
+      // apart (>= 128 cycles), past the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32
+      constexpr int NG = NTW >= 4 ? NTW / 4 : 1;
 #pragma unroll
-      for (int j = 0; j < NT; j += 2) {
-        const int row0 = j * 16 + r16;
-        const float4 b0 = *reinterpret_cast<const float4*>(Bt + row0 * 16 + swz_slot(row0, g) * 4);
-        if (j + 1 < NT) {
-          const int row1 = row0 + 16;
-          const float4 b1 = *reinterpret_cast<const float4*>(Bt + row1 * 16 + swz_slot(row1, g) * 4);
+      for (int gi = 0; gi < NG; ++gi) {
+        const int j0 = gi * NTW / NG, j1 = (gi + 1) * NTW / NG;
+        f32x4 b[8];
 #pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b0.x, acc[i][j], 0, 0, 0);
-            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b1.x, acc[i][j + 1], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b0.y, acc[i][j], 0, 0, 0);
-            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b1.y, acc[i][j + 1], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b0.z, acc[i][j], 0, 0, 0);
-            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b1.z, acc[i][j + 1], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b0.w, acc[i][j], 0, 0, 0);
-            acc[i][j + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b1.w, acc[i][j + 1], 0, 0, 0);
+        for (int t = 0; t < 8; ++t)
+          if (j0 + t < j1) {
+            const int row = (bt0 + j0 + t) * 16 + r16;
+            b[t] = *reinterpret_cast<const f32x4*>(Bt + row * 16 + swz_slot(row, g) * 4);
           }
-        } else {
 #pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, b0.x, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, b0.y, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, b0.z, acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, b0.w, acc[i][j], 0, 0, 0);
-          }
-        }
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (j0 + t < j1)
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s4], b[t][s4], acc[i][j0 + t], 0, 0, 0);
       }
     }
     if (more) sstore(nxt);
@@ -249,39 +275,58 @@ __global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
   }
 
   // C/D layout of 16x16 MFMA: lane holds rows 4*(lane>>4) + r (r = 0..3), column lane & 15.
-  if constexpr (EPI == kEpiRelu) {
+  // Stored activations go through LDS (each wave transposes its rows into a private slab of the
+  // now idle stage buffers) so the global stores are whole-row float4s instead of 4-B scatters.
+  auto store_rows = [&](float* dst, int ldd) {
+    using EG = EpiGeom<T, STAGE>;
+    constexpr int RW = EG::RW, NTH = EG::NTH, LD = EG::LD;
+    float* wbuf = smem + wid * RW * LD;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int mw = m0 + wid * MT * 16 + i * 16 + g * 4;
+    for (int j0 = 0; j0 < NTW; j0 += NTH) {
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = n0 + j * 16 + r16;
-        const float bn = p.bias[n];
+      for (int t = 0; t < NTH; ++t) {
+        if (j0 + t >= NTW) break;
+        const float bn = p.bias[n0 + (bt0 + j0 + t) * 16 + r16];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[i][j][r] + bn;
-          v = v > 0.f ? v : 0.f;
-          if (mw + r < M) p.C[(int64_t)(mw + r) * p.ldc + n] = v;
-        }
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j0 + t][r] + bn;
+            wbuf[(i * 16 + g * 4 + r) * LD + t * 16 + r16] = v > 0.f ? v : 0.f;
+          }
       }
+      __syncthreads();
+      const int nf4 = ((NTW - j0 < NTH) ? (NTW - j0) : NTH) * 4;
+      for (int q = lane; q < RW * nf4; q += 64) {
+        const int rr = q / nf4, c4 = q - rr * nf4;
+        const int m = m0 + wm * RW + rr;
+        if (m < M)
+          *reinterpret_cast<float4*>(dst + (int64_t)m * ldd + n0 + (bt0 + j0) * 16 + c4 * 4) =
+              *reinterpret_cast<const float4*>(wbuf + rr * LD + c4 * 4);
+      }
+      __syncthreads();
     }
+  };
+  if constexpr (EPI == kEpiRelu) {
+    store_rows(p.C, p.ldc);
   } else {
-    // row reduction sum_n ReLU(acc + b)[n] * w[n] over the block's (= the layer's) columns
+    // row reduction sum_n ReLU(acc + b)[n] * w[n] over the block's (= the layer's) columns;
+    // with WN > 1 the waves of a row group add their partial sums through LDS
+    float* red = smem;  // [WN][BM], the stage buffers are idle after the last barrier
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      const int mw = m0 + wid * MT * 16 + i * 16 + g * 4;
+      const int rl = wm * MT * 16 + i * 16 + g * 4;  // block-local first row of the lane group
       float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = j * 16 + r16;
+      for (int j = 0; j < NTW; ++j) {
+        const int n = (bt0 + j) * 16 + r16;
         const float bn = p.bias[n];
-        const float wn = EPI == kEpiOutput ? p.oa.wo[n] : p.wo[n];
+        const float wv = EPI == kEpiOutput ? p.oa.wo[n] : p.wo[n];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] + bn;
           v = v > 0.f ? v : 0.f;
-          part[r] += v * wn;
-          if (EPI == kEpiCin && p.C && mw + r < M) p.C[(int64_t)(mw + r) * p.ldc + n] = v;
+          part[r] += v * wv;
         }
       }
 #pragma unroll
@@ -294,26 +339,37 @@ __global__ __launch_bounds__(WM * 64) void gemm_kernel(GemmArgs p) {
         part[r] = v;
       }
       if (r16 < 4) {
-        // lane r16 = r finalises row mw + r (rows of the lane group g)
-        const int m = mw + r16;
-        float y = r16 == 0 ? part[0] : (r16 == 1 ? part[1] : (r16 == 2 ? part[2] : part[3]));
-        if (m < M) {
-          if constexpr (EPI == kEpiCin) {
-            p.rowdot[m] = p.cin_first ? y : p.rowdot[m] + y;
-          } else {
-            const OutArgs& oa = p.oa;
-            if (oa.has_bo) y = y + oa.bo;
-            if (oa.rowsum) {
-              float rs = 0.f;
-              for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
-              y = rs + y;
-            }
-            if (oa.pre2) y = oa.pre2[m] + y;
-            float t = oa.pre ? oa.pre[m] + y : y;
-            t = t + oa.beta;
-            oa.out[m] = 1.0f / (1.0f + expf(-t));
-          }
+        const float y = r16 == 0 ? part[0] : (r16 == 1 ? part[1] : (r16 == 2 ? part[2] : part[3]));
+        red[wn * BM + rl + r16] = y;
+      }
+    }
+    __syncthreads();
+    for (int rl = tid; rl < BM; rl += NTHR) {
+      const int m = m0 + rl;
+      if (m >= M) continue;
+      float y = red[rl];
+#pragma unroll
+      for (int w = 1; w < WN; ++w) y += red[w * BM + rl];
+      if constexpr (EPI == kEpiCin) {
+        p.rowdot[m] = p.cin_first ? y : p.rowdot[m] + y;
+      } else {
+        const OutArgs& oa = p.oa;
+        if (oa.has_bo) y = y + oa.bo;
+        if (oa.rowsum) {
+          float rs = 0.f;
+          for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
+          y = rs + y;
         }
+        if (oa.pre2) y = oa.pre2[m] + y;
+        float t = oa.pre ? oa.pre[m] + y : y;
+        t = t + oa.beta;
+        oa.out[m] = 1.0f / (1.0f + expf(-t));
+      }
+    }
+    if constexpr (EPI == kEpiCin) {
+      if (p.C) {
+        __syncthreads();  // red[] lives in the slab area
+        store_rows(p.C, p.ldc);  // u_l for the next CIN layer
       }
     }
   }
@@ -374,54 +430,74 @@ namespace {
 constexpr int kNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16, 20, 25, 26};
 constexpr int kCinNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16};
 
-template <int MT, int NT, int WM, int BKC, int AMODE, int EPI>
+template <class T, int AMODE, int EPI>
 int launch_cfg(hipStream_t s, GemmArgs& p) {
-  constexpr int BM = WM * MT * 16, BN = NT * 16;
-  constexpr int AROWS = AMODE != kCinOuter ? BM * BKC : 0;
-  size_t lds = sizeof(float) * 2 * (AROWS + BN * BKC) * 16;
-  if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * BM * p.ga.F;
-  if (AMODE == kCinOuter) lds += sizeof(float) * BM * p.XS;
+  using SG = StageGeom<T, AMODE>;
+  size_t lds = sizeof(float) * 2 * SG::FLOATS;
+  if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * T::BM * p.ga.F;
+  if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
+  if (EPI != kEpiOutput) lds = std::max(lds, sizeof(float) * EpiGeom<T, SG::FLOATS>::FLOATS);
+  lds = std::max(lds, sizeof(float) * T::WN * T::BM);  // row-reduction partials
   if (lds > 160 * 1024) {
     set_error("gemm: LDS budget exceeded (" + std::to_string(lds) + " bytes)");
     return RMX_E_INVALID;
   }
-  dim3 grid((p.M + BM - 1) / BM, p.Npad / BN);
-  auto kern = gemm_kernel<MT, NT, WM, BKC, AMODE, EPI>;
+  if (p.Npad % T::BN) {
+    set_error("gemm: Npad " + std::to_string(p.Npad) + " is not a multiple of the block width");
+    return RMX_E_INVALID;
+  }
+  dim3 grid((p.M + T::BM - 1) / T::BM, p.Npad / T::BN);
+  auto kern = gemm_kernel<T, AMODE, EPI>;
   if (lds > 64 * 1024)
     RMX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(kern, grid, dim3(WM * 64), lds, s, p);
+  hipLaunchKernelGGL(kern, grid, dim3(T::NTHR), lds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
 
+template <class T>
+int launch_epi(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
+#define RMX_EPI(AM)                                                      \
+  if (epi == Epi::kReluStore) return launch_cfg<T, AM, kEpiRelu>(s, p); \
+  return launch_cfg<T, AM, kEpiOutput>(s, p);
+  if (amode == kDenseA) { RMX_EPI(kDenseA) }
+  if (amode == kGatherK16) { RMX_EPI(kGatherK16) }
+  RMX_EPI(kGatherAny)
+#undef RMX_EPI
+}
+
 template <int NT>
 int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
-  // 8 waves (2 per SIMD) for large batches, 4 for small ones; two K chunks per stage when the
-  // A rows come from a dense activation buffer, one when they are gathered (ids share the LDS).
-  const bool big = p.M >= 8192;
-#define RMX_TOWER_CASE(WM, BKC, AM)                                                        \
-  if (epi == Epi::kReluStore) return launch_cfg<1, NT, WM, BKC, AM, kEpiRelu>(s, p); \
-  return launch_cfg<1, NT, WM, BKC, AM, kEpiOutput>(s, p);
-  if (big) {
-    if (amode == kDenseA) { RMX_TOWER_CASE(8, 2, kDenseA) }
-    if (amode == kGatherK16) { RMX_TOWER_CASE(8, 1, kGatherK16) }
-    RMX_TOWER_CASE(8, 1, kGatherAny)
+  // Large batches: 8-wave blocks.  Knob "tower_variant":
+  //   0: 8 waves on M (BM 128) x all NT tiles per wave, 2 waves / SIMD (1 block per CU);
+  //   1: 4 x 2 waves (BM 64, NT/2 tiles per wave), one K chunk per stage, 4 waves / SIMD
+  //      (2 blocks per CU, their barriers interleave);
+  //   2: 8 x 2 waves (16 waves, BM 128), 4 waves / SIMD in one block.
+  // Variants 1 / 2 need an even NT (the model packs N = 400 as 26 tiles when tower_split = 1).
+  // Small batches: 4-wave blocks.
+  const int var = NT % 2 == 0 ? tuning_get("tower_variant", 0) : 0;
+  const bool dense = amode == kDenseA;
+  if (p.M >= 8192) {
+    if (var == 1) return launch_epi<Tile<1, (NT + 1) / 2, 4, 2, 1, 4>>(s, p, amode, epi);
+    if (var == 2) {
+      if (dense) return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 2, 4>>(s, p, amode, epi);
+      return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 1, 4>>(s, p, amode, epi);
+    }
+    if (dense) return launch_epi<Tile<1, NT, 8, 1, 2, 1>>(s, p, amode, epi);
+    return launch_epi<Tile<1, NT, 8, 1, 1, 1>>(s, p, amode, epi);
   }
-  if (amode == kDenseA) { RMX_TOWER_CASE(4, 1, kDenseA) }
-  if (amode == kGatherK16) { RMX_TOWER_CASE(4, 1, kGatherK16) }
-  RMX_TOWER_CASE(4, 1, kGatherAny)
-#undef RMX_TOWER_CASE
+  return launch_epi<Tile<1, NT, 4, 1, 1, 1>>(s, p, amode, epi);
 }
 
 template <int NT>
 int launch_cin_nt(hipStream_t s, GemmArgs& p) {
-  // knob "cin_variant": 0 = 8 waves x 16 rows, 2 chunks per stage (measured fastest at
-  // B = 4096: 1.637 ms / layer vs 1.663 for 8 x 32 rows and 1.682 for 4 x 32 rows);
-  // 1 = 8 waves x 32 rows.  Small M always uses 4 waves x 16 rows.
+  // knob "cin_variant": 0 = 8 waves x 16 rows, 2 chunks per stage, 4 waves / SIMD (two blocks
+  // per CU: 1.637 ms / layer at B = 4,096 vs 1.84 at 3 waves / SIMD); 1 = 8 waves x 32 rows.
+  // Small M always uses 4 waves x 16 rows.
   const int var = tuning_get("cin_variant", 0);
-  if (p.M < 8192) return launch_cfg<1, NT, 4, 2, kCinOuter, kEpiCin>(s, p);
-  if (var == 1) return launch_cfg<2, NT, 8, 2, kCinOuter, kEpiCin>(s, p);
-  return launch_cfg<1, NT, 8, 2, kCinOuter, kEpiCin>(s, p);
+  if (p.M < 8192) return launch_cfg<Tile<1, NT, 4, 1, 2, 1>, kCinOuter, kEpiCin>(s, p);
+  if (var == 1) return launch_cfg<Tile<2, NT, 8, 1, 2, 1>, kCinOuter, kEpiCin>(s, p);
+  return launch_cfg<Tile<1, NT, 8, 1, 2, 4>, kCinOuter, kEpiCin>(s, p);
 }
 
 }  // namespace
@@ -430,8 +506,10 @@ int launch_cin_nt(hipStream_t s, GemmArgs& p) {
 // to minimise padding (ties: the wider block).
 int tower_npad_for(int N) {
   const int nt = (N + 15) / 16;
+  const bool even = tuning_get("tower_split", 0) != 0 && nt >= 8;  // variants 1/2 split NT in halves
   int best = -1, best_pad = 1 << 30;
   for (int c : kNTs) {
+    if (even && c % 2) continue;
     const int pad = (nt + c - 1) / c * c;
     if (pad < best_pad || (pad == best_pad && c > best)) {
       best_pad = pad;

@@ -29,25 +29,32 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--set", default="", help="extra knobs applied before building the models, k=v,k=v")
     a = ap.parse_args()
     vals = [int(v) for v in a.values.split(",")]
     ctx = rmx.default_context()
-    if a.workload == "deepfm":
-        m = rmx.DeepFM(V, F, K, [400, 400, 400], ctx=ctx)
-        B = a.batch or 65536
-    elif a.workload == "xdeepfm":
-        m = rmx.XDeepFM(V, F, K, [400, 400, 400], [200, 200, 200], ctx=ctx)
-        B = a.batch or 4096
-    elif a.workload == "dcn":
-        m = rmx.DCN(V, F, K, 3, [400, 400, 400], ctx=ctx)
-        B = a.batch or 65536
-    else:
-        m = rmx.PNN(V, F, K, [400, 400, 400], ctx=ctx)
-        B = a.batch or 65536
+    for kv in filter(None, a.set.split(",")):
+        k_, v_ = kv.split("=")
+        rmx.set_tuning(k_, int(v_))
+
+    def build():
+        if a.workload == "deepfm":
+            return rmx.DeepFM(V, F, K, [400, 400, 400], ctx=ctx), a.batch or 65536
+        if a.workload == "xdeepfm":
+            return rmx.XDeepFM(V, F, K, [400, 400, 400], [200, 200, 200], ctx=ctx), a.batch or 4096
+        if a.workload == "dcn":
+            return rmx.DCN(V, F, K, 3, [400, 400, 400], ctx=ctx), a.batch or 65536
+        return rmx.PNN(V, F, K, [400, 400, 400], ctx=ctx), a.batch or 65536
+
+    models = {}
+    for v in vals:  # a model per variant: knobs read at model build (packing) apply too
+        rmx.set_tuning(a.knob, v)
+        m, B = build()
+        m.setMats(m.initMats(0x3A75))
+        m.setBias(0.01)
+        models[v] = m
     t = rmx.EmbeddingTable(ctx, V, K)
     t.fill_synthetic(0x7AB1E)
-    m.setMats(m.initMats(0x3A75))
-    m.setBias(0.01)
     ids = rmx.DeviceArray(ctx, B * F, np.int32)
     rmx.gen_ids(ctx, 0x5EED2026, 0, B, F, V, ids)
     out = rmx.DeviceArray(ctx, B, np.float32)
@@ -56,6 +63,7 @@ def main():
     for r in range(a.rounds):
         for v in vals:
             rmx.set_tuning(a.knob, v)
+            m = models[v]
             m.forward_ids(t, B, ids, out)
             ctx.sync()
             p = out.numpy()
