@@ -32,6 +32,7 @@ SEED_IDS, SEED_TAB, SEED_MATS = 0x5EED2026, 0x7AB1E, 0x3A75
 # Peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
 PEAK_FP32_TFLOPS = 157.3
+PEAK_BF16_TFLOPS = 2500.0  # dense
 
 
 def parse():
@@ -39,7 +40,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded"], default="deepfm")
+    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded", "dcn_bf16", "pnn_bf16"],
+                    default="deepfm")
     ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
@@ -48,16 +50,23 @@ def parse():
 
 
 def stage_work(workload, stage, B):
-    """Algorithmic work of one launch of a stage: ('flop'|'byte', amount)."""
+    """Algorithmic work of one launch of a stage: ('flop'|'byte', amount) (DESIGN.md §4)."""
     D = F * K
+    P = F * (F - 1) // 2
+    es = 2 if workload.endswith("bf16") else 4  # table element bytes
     if stage == "shard_exchange":  # ids out + (k+1)-float rows back, all ranks' shares incl. self
         return "byte", B * F * (4 + 4 + (K + 1) * 4 * 2)
     if stage == "encoder_fm":  # ids + w + emb rows + y  (SURVEY.md §8d: 2,812 B / example)
-        return "byte", B * (F * 4 + F * 4 + F * K * 4 + 4)
+        return "byte", B * (F * 4 + F * es + F * K * es + 4)
     if stage == "first_order":
-        return "byte", B * (F * 4 + F * 4 + 4)
+        return "byte", B * (F * 4 + F * es + 4)
+    if stage == "cross":  # ids + rows + pre2
+        return "byte", B * (F * 4 + F * K * es + 4)
+    if stage == "product":  # ids + rows + the [x | ip] row written
+        return "byte", B * (F * 4 + F * K * es + (D + P) * es)
+    k1 = D + P if workload.startswith("pnn") else D
     if stage == "tower_layer1":
-        return "flop", 2.0 * B * D * FC[0]
+        return "flop", 2.0 * B * k1 * FC[0]
     if stage == "tower_layer2":
         return "flop", 2.0 * B * FC[0] * FC[1]
     if stage == "tower_layer3":
@@ -73,7 +82,13 @@ def cpu_baseline(workload, budget_s, threads):
     """Oracle (C restatement, OpenMP) on the host cores: examples/s on bounded batches."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ctypes as oc
-    if workload != "xdeepfm":  # deepfm_sharded: same per-example CPU work (V = 1M table on the host)
+    if workload == "dcn_bf16":
+        om = oc.make_model(oc.DCN, F, K, fc=tuple(FC), cross_depth=3)
+        B = 4096
+    elif workload == "pnn_bf16":
+        om = oc.make_model(oc.PNN, F, K, fc=tuple(FC))
+        B = 4096
+    elif workload != "xdeepfm":  # deepfm_sharded: same per-example CPU work (V = 1M table on the host)
         om = oc.make_model(oc.DEEPFM, F, K, fc=tuple(FC))
         B = 4096
     else:
@@ -116,10 +131,17 @@ def main():
     rmx.set_device(local)
     ctx = rmx.default_context()
     stream = ctx.stream
+    bf16 = args.workload.endswith("bf16")
     if args.workload == "xdeepfm":
         model = rmx.XDeepFM(Vw, F, K, FC, CIN, ctx=ctx)
+    elif args.workload == "dcn_bf16":  # configs[4]: DCN depth 3 + fcDims 400^3, bf16 table / weights
+        model = rmx.DCN(Vw, F, K, 3, FC, ctx=ctx)
+    elif args.workload == "pnn_bf16":  # configs[4]: PNN (IPNN) D1 = 400, fcDims 400^3, bf16
+        model = rmx.PNN(Vw, F, K, FC, ctx=ctx)
     else:
         model = rmx.DeepFM(Vw, F, K, FC, ctx=ctx)
+    if bf16:
+        model.setPrecision(rmx.DTYPE_BF16)
     if sharded:
         # configs[3]: table hash-sharded over the ranks, RCCL exchange per batch
         uid = rmx.comm_unique_id() if rank == 0 else None
@@ -129,7 +151,7 @@ def main():
             uid = box[0]
         table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
     else:
-        table = rmx.EmbeddingTable(ctx, Vw, K)
+        table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
     table.fill_synthetic(SEED_TAB)
     model.setMats(model.initMats(SEED_MATS))
     model.setBias(0.01)
@@ -187,6 +209,7 @@ def main():
     ctx.sync()
     stages, calls = model.get_timing()
     model.set_timing(False)
+    peak_tf = PEAK_BF16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
     per_stage = {}
     for name, tot in stages.items():
         avg_ms = tot / max(calls, 1)
@@ -194,7 +217,7 @@ def main():
         ent = {"avg_ms": round(avg_ms, 4)}
         if kind == "flop":
             ent["tflops"] = round(work / (avg_ms / 1e3) / 1e12, 2)
-            ent["frac_fp32_peak"] = round(ent["tflops"] / PEAK_FP32_TFLOPS, 3)
+            ent["frac_mfma_peak"] = round(ent["tflops"] / peak_tf, 3)
         elif kind == "byte":
             ent["gbs"] = round(work / (avg_ms / 1e3) / 1e9, 1)
             ent["frac_hbm_peak"] = round(ent["gbs"] / PEAK_HBM_GBS, 3)
@@ -205,7 +228,7 @@ def main():
     if kind == "byte":
         roof = {"bound": "hbm", "achieved": round(work / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
     else:
-        roof = {"bound": "mfma", "achieved": round(work / avg_s / 1e12, 2), "peak": PEAK_FP32_TFLOPS,
+        roof = {"bound": "mfma", "achieved": round(work / avg_s / 1e12, 2), "peak": peak_tf,
                 "unit": "TFLOP/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
     roof["traffic"] = None
@@ -229,11 +252,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16 (fp32 accumulate)" if bf16 else "f32",
             "data": "synthetic (splitmix64 Criteo-shaped ids, U(-0.05,0.05) table, Xavier mats)",
-            "config": {"workload": "%s_fp32_F39_V%s_k16_fc400x3%s_B%d" % (
-                args.workload, ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
-                "_cin200x3" if args.workload == "xdeepfm" else "", B),
+            "config": {"workload": "%s%s_F39_V%s_k16_fc400x3%s_B%d" % (
+                args.workload, "" if bf16 else "_fp32",
+                ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
+                {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(args.workload, ""), B),
                 "global_batch": world * B, "rows_per_gpu_set": nrows,
                 "parallelism": ("hashshard%d_rccl" % world) if sharded else "replicas%d" % world},
             "roofline": roof,

@@ -56,6 +56,10 @@ extern "C" {
 #define RMX_BIAS_WEIGHT_EMBEDDING_MATS 2
 #define RMX_BIAS_WEIGHT_EMBEDDING_MATS_FIELD 3
 
+/* Element types of tables and model parameters. */
+#define RMX_DTYPE_F32 0
+#define RMX_DTYPE_BF16 1
+
 /* Embedding-table host layouts for rmx_table_upload. */
 #define RMX_LAYOUT_K_MAJOR 0   /* reference Angel PS layout: k rows x V columns (ParRecModel.scala:95-101) */
 #define RMX_LAYOUT_ROW_MAJOR 1 /* V rows x k columns                                                      */
@@ -133,26 +137,35 @@ int rmx_model_init_mats(const rmx_model* m, uint64_t seed, float* mats);
 /* L-B parameters: load mats (getMatsSize layout) and the global bias once, on device. */
 int rmx_model_set_mats(rmx_model* m, const float* mats, int64_t n_mats);
 int rmx_model_set_bias(rmx_model* m, float bias);
+/* RMX_DTYPE_BF16: Linear weights stored bf16 (rounded to nearest even when mats are loaded), the
+ * towers on bf16 MFMA with fp32 accumulation, stored activations bf16 (BASELINE.json configs[4]).
+ * Biases, the output Linear and DCN cross vectors stay fp32.  Call before rmx_model_set_mats.
+ * L-B needs a table of the same dtype; L-A rounds the caller's fp32 arrays.  Not for xDeepFM. */
+int rmx_model_set_precision(rmx_model* m, int dtype);
 
 /* ---------------------------------------------------------------- table ---- */
 /* HBM-resident first-order weights + embedding table (replaces the Angel PS rows
  * "weights" and "embedding", ParRecModel.scala:74-105).  Stored row-major [V][k]. */
 int rmx_table_create(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, rmx_table** out);
+/* dtype RMX_DTYPE_BF16: the table stores bf16 (BASELINE.json configs[4]); uploads and the
+ * synthetic fill round fp32 values to nearest even. */
+int rmx_table_create_ex(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, int dtype, rmx_table** out);
+int rmx_table_dtype(const rmx_table* t);
 int rmx_table_destroy(rmx_table* t);
 /* Host upload; weights may be NULL, embedding may be NULL (then left as is). */
 int rmx_table_upload(rmx_table* t, const float* weights, const float* embedding, int layout);
 /* Deterministic synthetic fill, bit-identical to oracle/orc_gen_table (U(-0.05, 0.05)). */
 int rmx_table_fill_synthetic(rmx_table* t, uint64_t seed);
 int64_t rmx_table_rows(const rmx_table* t);
-/* Device pointers of the table (for debugging/parity only). */
-int rmx_table_device_ptrs(const rmx_table* t, float** d_weights, float** d_embedding);
+/* Device pointers of the table (for debugging/parity only; elements of the table's dtype). */
+int rmx_table_device_ptrs(const rmx_table* t, void** d_weights, void** d_embedding);
 
 /* Synthetic field-partitioned ids into device memory, bit-identical to orc_gen_ids. */
 int rmx_gen_ids(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,
                 int64_t num_rows, int32_t* d_ids, void* stream);
 
 /* Debug gather: d_w[n] = weights[ids[n]], d_emb[n*k+j] = emb[ids[n]][j] (makeWeights /
- * makeEmbeddings, ParRecModel.scala:279-306).  Bit-exact copies. */
+ * makeEmbeddings, ParRecModel.scala:279-306).  Bit-exact copies (as fp32 for a bf16 table). */
 int rmx_gather(const rmx_table* t, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
                void* stream);
 

@@ -12,6 +12,20 @@
 
 #define RB 8
 
+/* bf16 round-to-nearest-even of a finite fp32 value (v_cvt_pk_bf16_f32 for non-NaN inputs) */
+static float bf16_round(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  u &= 0xFFFF0000u;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+/* precision-2 flag (set per orc_forward call; the oracle is test infrastructure, not thread-safe
+ * across concurrent precision-2 and other calls) */
+static int g_bf16 = 0;
+
 /* ---------------------------------------------------------------- sizes ---- */
 
 static void push_pair(int32_t* out, int32_t cap, int32_t* n, int32_t a, int32_t b) {
@@ -243,6 +257,10 @@ int32_t orc_first_order(int32_t B, int64_t nnz, const int64_t* index, const floa
 #undef REAL
 #undef FN
 
+void orc_round_bf16(int64_t n, const float* x, float* y) {
+  for (int64_t i = 0; i < n; ++i) y[i] = bf16_round(x[i]);
+}
+
 int32_t orc_fm(int32_t B, int32_t F, int32_t k, const float* embedding, float* y2) {
   for (int32_t b = 0; b < B; ++b) y2[b] = fm_one_f32(F, k, embedding + (int64_t)b * F * k);
   return ORC_OK;
@@ -267,7 +285,8 @@ int32_t orc_forward(const orc_model* m, int32_t B, int64_t nnz, const int64_t* i
     if (st != ORC_OK) { free(y1); return st; }
   }
   int32_t st;
-  if (precision == 1)
+  g_bf16 = precision == 2;
+  if (precision >= 1)
     st = forward_f64(m, B, y1, bias, embedding, mats, nthreads, out);
   else
     st = forward_f32(m, B, y1, bias, embedding, mats, nthreads, out);

@@ -81,7 +81,9 @@ int32_t orc_gather(int64_t V, int32_t k, const float* w_table, const float* emb_
 /* ---- forward (RecModel.forward, yr/model/RecModel.scala:37-48 -> buildParams :146-155) ----
  * Inputs are the reference's flat arrays: index[nnz] (COO row ids), the gathered
  * weights[nnz] and embedding[nnz*k], bias[1], mats.  precision 0 = fp32 in BigDL
- * op order, 1 = fp64 accumulation (for error bounds).  nthreads <= 0 -> OpenMP default.
+ * op order, 1 = fp64 accumulation (for error bounds), 2 = fp64 accumulation with the bf16
+ * storage points of a bf16 model emulated (activations stored between GEMM layers and the PNN
+ * inner products rounded to bf16; the caller passes bf16-rounded table rows and mats).  nthreads <= 0 -> OpenMP default.
  * out[B] receives sigmoid probabilities. */
 int32_t orc_forward(const orc_model* m, int32_t B, int64_t nnz, const int64_t* index,
                     const float* bias, const float* weights, const float* embedding,
@@ -91,6 +93,8 @@ int32_t orc_forward(const orc_model* m, int32_t B, int64_t nnz, const int64_t* i
  * y1[B] first order (Scatter), y2[B] FM second order (DeepFM only, else 0). */
 int32_t orc_first_order(int32_t B, int64_t nnz, const int64_t* index, const float* weights, float* y1);
 int32_t orc_fm(int32_t B, int32_t F, int32_t k, const float* embedding, float* y2);
+/* bf16 round-to-nearest-even of n fp32 values (the device's v_cvt_pk_bf16_f32 for finite values) */
+void orc_round_bf16(int64_t n, const float* x, float* y);
 
 #ifdef __cplusplus
 }

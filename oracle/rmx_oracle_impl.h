@@ -32,6 +32,14 @@ static void FN(linear_rb)(int in, int out, const REAL* XT, const float* W, const
   }
 }
 
+/* precision 2 (bf16 emulation, f64 instantiation only): activations the device stores between
+ * GEMM layers are rounded to bf16 (round to nearest even of the fp32 value); the last hidden layer
+ * (consumed by the fused output dot in registers) stays unrounded.  See DESIGN.md §4, bf16 row. */
+static REAL FN(act)(REAL v, int store) {
+  if (!store || !g_bf16) return v;
+  return (REAL)bf16_round((float)v);
+}
+
 static REAL FN(sigmoid)(REAL x) {
   /* BigDL Sigmoid: 1 / (1 + exp(-x)), exp through java.lang.Math.exp (double). */
   const REAL e = (REAL)exp(-(double)x);
@@ -57,6 +65,8 @@ static REAL* FN(tower)(int in, const int32_t* fc, int n_fc, int with_output, con
     const float* W = mats + *off;
     const float* bb = W + (int64_t)dim * fc[l];
     FN(linear_rb)(dim, fc[l], cur, W, bb, nxt, 1);
+    if (l + 1 < n_fc) /* stored between layers (bf16 mode) */
+      for (int64_t i = 0; i < (int64_t)fc[l] * RB; ++i) nxt[i] = FN(act)(nxt[i], 1);
     *off += (int64_t)dim * fc[l] + fc[l];
     dim = fc[l];
     cur = nxt;
@@ -246,7 +256,7 @@ static int FN(forward)(const orc_model* m, int B, const float* y1f, const float*
                 const float* e = E + (int64_t)(b0 + r) * D;
                 for (int t = 0; t < k; ++t) s += (REAL)e[(int64_t)i * k + t] * (REAL)e[(int64_t)j2 * k + t];
               }
-              IP[(int64_t)p * RB + r] = s;
+              IP[(int64_t)p * RB + r] = FN(act)(s, 1);  /* [x | ip] row stored for the GEMM */
             }
         }
         const float* Wz = mats;                        /* D1 x D, :78-82 */
@@ -256,7 +266,7 @@ static int FN(forward)(const orc_model* m, int B, const float* y1f, const float*
         FN(linear_rb)(P, D1, IP, Wp, NULL, Bf, 0);
         for (int64_t i = 0; i < (int64_t)D1 * RB; ++i) {
           const REAL v = (A[i] + Bf[i]) + (REAL)bp[0];   /* CAddTable, CAdd, ReLU: :97-102 */
-          XT[i] = v > 0 ? v : (REAL)0;
+          XT[i] = FN(act)(v > 0 ? v : (REAL)0, m->n_fc > 1);
         }
         off = (int64_t)D * D1 + (int64_t)P * D1 + 1;
         REAL* y = FN(tower)(D1, m->fc + 1, m->n_fc - 1, 1, mats, &off, XT, A, Bf, &w);

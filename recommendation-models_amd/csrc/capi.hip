@@ -217,6 +217,18 @@ extern "C" int rmx_model_set_mats(rmx_model* m, const float* mats, int64_t n) {
   return model_load_mats(*m, mats, /*sync=*/true);
 }
 
+extern "C" int rmx_model_set_precision(rmx_model* m, int dtype) {
+  CHECK_ARG(m, "rmx_model_set_precision: model is NULL");
+  CHECK_ARG(m->ctx, "rmx_model_set_precision: host-only model (created without a context)");
+  CHECK_ARG(dtype == RMX_DTYPE_F32 || dtype == RMX_DTYPE_BF16, "rmx_model_set_precision: dtype must be F32 or BF16");
+  if (dtype == m->precision) return RMX_OK;
+  if (dtype == RMX_DTYPE_BF16 && m->type == RMX_MODEL_XDEEPFM) {
+    set_error("rmx_model_set_precision: the xDeepFM CIN runs in fp32 only");
+    return RMX_E_INVALID;
+  }
+  return model_set_precision(*m, dtype);
+}
+
 extern "C" int rmx_model_set_bias(rmx_model* m, float bias) {
   CHECK_ARG(m, "rmx_model_set_bias: model is NULL");
   m->beta = bias;
@@ -251,16 +263,20 @@ extern "C" int rmx_model_get_timing(rmx_model* m, char* names, int name_stride, 
 }
 
 // -------------------------------------------------------------------- table --
-extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
+static size_t dtype_size(int dt) { return dt == RMX_DTYPE_BF16 ? 2 : 4; }
+
+extern "C" int rmx_table_create_ex(rmx_ctx* c, int64_t V, int k, int dtype, rmx_table** out) {
   CHECK_ARG(c && out && V > 0 && k >= 0, "rmx_table_create: bad args");
   CHECK_ARG(V < (int64_t(1) << 31), "rmx_table_create: rows must fit int32 (ParRecModel.scala:282 .toInt)");
+  CHECK_ARG(dtype == RMX_DTYPE_F32 || dtype == RMX_DTYPE_BF16, "rmx_table_create: dtype must be F32 or BF16");
   RMX_HIP(hipSetDevice(c->device));
   auto* t = new rmx_table();
   t->ctx = c;
   t->V = V;
   t->k = k;
-  if (hipMalloc(&t->w, sizeof(float) * V) != hipSuccess ||
-      (k > 0 && hipMalloc(&t->emb, sizeof(float) * V * k) != hipSuccess)) {
+  t->dtype = dtype;
+  const size_t es = dtype_size(dtype);
+  if (hipMalloc(&t->w, es * V) != hipSuccess || (k > 0 && hipMalloc(&t->emb, es * V * k) != hipSuccess)) {
     if (t->w) (void)hipFree(t->w);
     delete t;
     set_error("rmx_table_create: out of device memory");
@@ -268,6 +284,10 @@ extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
   }
   *out = t;
   return RMX_OK;
+}
+
+extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
+  return rmx_table_create_ex(c, V, k, RMX_DTYPE_F32, out);
 }
 
 extern "C" int rmx_table_destroy(rmx_table* t) {
@@ -281,8 +301,9 @@ extern "C" int rmx_table_destroy(rmx_table* t) {
 }
 
 extern "C" int64_t rmx_table_rows(const rmx_table* t) { return t ? t->V : -1; }
+extern "C" int rmx_table_dtype(const rmx_table* t) { return t ? t->dtype : -1; }
 
-extern "C" int rmx_table_device_ptrs(const rmx_table* t, float** w, float** e) {
+extern "C" int rmx_table_device_ptrs(const rmx_table* t, void** w, void** e) {
   CHECK_ARG(t, "rmx_table_device_ptrs: NULL");
   if (w) *w = t->w;
   if (e) *e = t->emb;
@@ -294,32 +315,45 @@ extern "C" int rmx_table_upload(rmx_table* t, const float* weights, const float*
   CHECK_ARG(layout == RMX_LAYOUT_K_MAJOR || layout == RMX_LAYOUT_ROW_MAJOR, "rmx_table_upload: bad layout");
   hipStream_t s = t->ctx->stream;
   RMX_HIP(hipSetDevice(t->ctx->device));
-  if (weights) RMX_HIP(hipMemcpyAsync(t->w, weights, sizeof(float) * t->V, hipMemcpyHostToDevice, s));
-  if (emb && t->k > 0) {
+  const bool bf = t->dtype == RMX_DTYPE_BF16;
+  // fp32 host arrays; a bf16 table stores them rounded to nearest even on the device
+  const size_t need = (size_t)t->V * std::max(1, bf || layout == RMX_LAYOUT_K_MAJOR ? t->k : 0);
+  float* tmp = nullptr;
+  if (bf || (emb && layout == RMX_LAYOUT_K_MAJOR)) {
+    if (hipMalloc(&tmp, sizeof(float) * std::max<size_t>(need, t->V)) != hipSuccess) {
+      set_error("rmx_table_upload: out of device memory for the staging copy");
+      return RMX_E_NOMEM;
+    }
+  }
+  int st = RMX_OK;
+  if (weights) {
+    if (bf) {
+      RMX_HIP(hipMemcpyAsync(tmp, weights, sizeof(float) * t->V, hipMemcpyHostToDevice, s));
+      st = launch_convert_bf16(s, tmp, t->V, (bf16_t*)t->w);
+      RMX_HIP(hipStreamSynchronize(s));
+    } else {
+      RMX_HIP(hipMemcpyAsync(t->w, weights, sizeof(float) * t->V, hipMemcpyHostToDevice, s));
+    }
+  }
+  if (st == RMX_OK && emb && t->k > 0) {
     const size_t bytes = sizeof(float) * t->V * t->k;
-    if (layout == RMX_LAYOUT_ROW_MAJOR) {
+    if (layout == RMX_LAYOUT_ROW_MAJOR && !bf) {
       RMX_HIP(hipMemcpyAsync(t->emb, emb, bytes, hipMemcpyHostToDevice, s));
     } else {
-      float* tmp = nullptr;
-      if (hipMalloc(&tmp, bytes) != hipSuccess) {
-        set_error("rmx_table_upload: out of device memory for the k-major staging copy");
-        return RMX_E_NOMEM;
-      }
       RMX_HIP(hipMemcpyAsync(tmp, emb, bytes, hipMemcpyHostToDevice, s));
-      int st = launch_transpose_kmajor(s, tmp, t->V, t->k, t->emb);
-      RMX_HIP(hipStreamSynchronize(s));
-      (void)hipFree(tmp);
-      if (st != RMX_OK) return st;
+      st = layout == RMX_LAYOUT_ROW_MAJOR ? launch_convert_bf16(s, tmp, t->V * t->k, (bf16_t*)t->emb)
+                                          : launch_transpose_kmajor(s, tmp, t->V, t->k, t->emb, t->dtype);
     }
   }
   RMX_HIP(hipStreamSynchronize(s));
-  return RMX_OK;
+  if (tmp) (void)hipFree(tmp);
+  return st;
 }
 
 extern "C" int rmx_table_fill_synthetic(rmx_table* t, uint64_t seed) {
   CHECK_ARG(t, "rmx_table_fill_synthetic: NULL table");
   RMX_HIP(hipSetDevice(t->ctx->device));
-  const int st = launch_fill_table(t->ctx->stream, seed, t->V, t->k, t->w, t->emb);
+  const int st = launch_fill_table(t->ctx->stream, seed, t->V, t->k, t->w, t->emb, t->dtype);
   if (st != RMX_OK) return st;
   RMX_HIP(hipStreamSynchronize(t->ctx->stream));
   return RMX_OK;
@@ -336,7 +370,7 @@ extern "C" int rmx_gather(const rmx_table* t, int64_t n, const int32_t* d_ids, f
                           void* stream) {
   CHECK_ARG(t && d_ids && n >= 0, "rmx_gather: bad args");
   RMX_HIP(hipSetDevice(t->ctx->device));
-  return launch_gather(stream ? (hipStream_t)stream : t->ctx->stream, n, d_ids, t->w, t->emb, t->k, d_w,
+  return launch_gather(stream ? (hipStream_t)stream : t->ctx->stream, n, d_ids, t->w, t->emb, t->dtype, t->k, d_w,
                        d_emb);
 }
 
@@ -359,6 +393,10 @@ extern "C" int rmx_forward_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
               std::to_string(m->k));
     return RMX_E_SHAPE;
   }
+  if (m->type != RMX_MODEL_LR && t->dtype != m->precision) {
+    set_error("rmx_forward_ids: table dtype differs from the model precision (rmx_model_set_precision)");
+    return RMX_E_INVALID;
+  }
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
   FwdInputs in;
@@ -366,6 +404,7 @@ extern "C" int rmx_forward_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
   in.ids = d_ids;
   in.table = t->emb;
   in.wtab = t->w;
+  in.dtype = t->dtype;
   in.beta = m->beta;
   in.out = d_out;
   return model_forward(*m, s, in);
@@ -377,7 +416,7 @@ extern "C" int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
   const int mode = m->type == RMX_MODEL_DEEPFM ? 1 : 0;
-  return launch_encoder(s, mode, B, d_ids, t->emb, t->w, m->F, t->k, d_y, nullptr, nullptr);
+  return launch_encoder(s, mode, B, d_ids, t->emb, t->w, t->dtype, m->F, t->k, d_y, nullptr, nullptr);
 }
 
 extern "C" int rmx_forward(rmx_model* m, int32_t B, int64_t nnz, const int64_t* index, const int64_t* feats,

@@ -24,10 +24,10 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 //       3 = y += y2 (L-A path with an irregular COO index: y already holds y1 from the CSR kernel).
 // k = 16 fast path: 4 lanes per sample (one float4 of the 64-B row each), 16 samples per wave,
 // all F row loads of a lane independent (ids staged in registers first).
-template <int MODE>
+template <int MODE, class T>
 __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* __restrict__ ids,
-                                                          const float* __restrict__ table,
-                                                          const float* __restrict__ wtab, int F,
+                                                          const T* __restrict__ table,
+                                                          const T* __restrict__ wtab, int F,
                                                           float* __restrict__ y, float beta,
                                                           float* __restrict__ prob) {
 #pragma clang fp contract(off)
@@ -38,7 +38,6 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
   const int bb = valid ? b : 0;
   float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = s4;
   float y1 = 0.f;
-  const float4* emb4 = reinterpret_cast<const float4*>(table);
   int f = 0;
   for (; f + 8 <= F; f += 8) {
     int id[8];
@@ -48,8 +47,8 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
     float wv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if (MODE == 1 || MODE == 3) v[u] = emb4[(int64_t)id[u] * 4 + c];
-      if (MODE != 3) wv[u] = (c == 0) ? wtab[id[u]] : 0.f;
+      if (MODE == 1 || MODE == 3) v[u] = load4(table + (int64_t)id[u] * 16 + c * 4);
+      if (MODE != 3) wv[u] = (c == 0) ? ld1(wtab + id[u]) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -64,11 +63,11 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
   for (; f < F; ++f) {
     const int id = ids ? ids[(int64_t)bb * F + f] : bb * F + f;
     if (MODE == 1 || MODE == 3) {
-      const float4 v = emb4[(int64_t)id * 4 + c];
+      const float4 v = load4(table + (int64_t)id * 16 + c * 4);
       s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
       q4.x += v.x * v.x; q4.y += v.y * v.y; q4.z += v.z * v.z; q4.w += v.w * v.w;
     }
-    if (MODE != 3 && c == 0) y1 += wtab[id];
+    if (MODE != 3 && c == 0) y1 += ld1(wtab + id);
   }
   float y2 = 0.f;
   if (MODE == 1 || MODE == 3) {
@@ -94,10 +93,10 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
 }
 
 // Generic-k fallback: one thread per sample, oracle order.
-template <int MODE>
+template <int MODE, class T>
 __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32_t* __restrict__ ids,
-                                                              const float* __restrict__ table,
-                                                              const float* __restrict__ wtab, int F,
+                                                              const T* __restrict__ table,
+                                                              const T* __restrict__ wtab, int F,
                                                               int k, float* __restrict__ y,
                                                               float beta, float* __restrict__ prob) {
 #pragma clang fp contract(off)
@@ -107,7 +106,7 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
   if (MODE != 3)
     for (int f = 0; f < F; ++f) {
       const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
-      y1 += wtab[id];
+      y1 += ld1(wtab + id);
     }
   if (MODE == 1 || MODE == 3) {
     float acc = 0.f;
@@ -115,7 +114,7 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
       float s = 0.f, q = 0.f;
       for (int f = 0; f < F; ++f) {
         const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
-        const float v = table[(int64_t)id * k + j];
+        const float v = ld1(table + (int64_t)id * k + j);
         s += v;
         q += v * v;
       }
@@ -129,27 +128,35 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
   if (MODE == 3) y[b] = y[b] + y2;
 }
 
-int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const float* table,
-                   const float* wtab, int F, int k, float* y, const float* beta, float* prob) {
-  if (M <= 0) return RMX_OK;
-  const float bt = beta ? *beta : 0.f;
-  if (k == 16) {
+template <class T>
+static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids, const T* table, const T* wtab, int F,
+                             int k, float* y, float bt, float* prob) {
+  if (k == 16 || mode == 2) {  // LR (mode 2) never reads the table: any k takes the 4-lane path
     dim3 grid((M + 63) / 64);
     switch (mode) {
-      case 0: hipLaunchKernelGGL(encoder_k16_kernel<0>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
-      case 1: hipLaunchKernelGGL(encoder_k16_kernel<1>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
-      case 2: hipLaunchKernelGGL(encoder_k16_kernel<2>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
-      default: hipLaunchKernelGGL(encoder_k16_kernel<3>, grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
     }
   } else {
     dim3 grid((M + 255) / 256);
     switch (mode) {
-      case 0: hipLaunchKernelGGL(encoder_generic_kernel<0>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
-      case 1: hipLaunchKernelGGL(encoder_generic_kernel<1>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
-      case 2: hipLaunchKernelGGL(encoder_generic_kernel<2>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
-      default: hipLaunchKernelGGL(encoder_generic_kernel<3>, grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      case 0: hipLaunchKernelGGL((encoder_generic_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      case 1: hipLaunchKernelGGL((encoder_generic_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      default: hipLaunchKernelGGL((encoder_generic_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
     }
   }
+}
+
+int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table, const void* wtab, int dt,
+                   int F, int k, float* y, const float* beta, float* prob) {
+  if (M <= 0) return RMX_OK;
+  const float bt = beta ? *beta : 0.f;
+  if (dt == kBF16)
+    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob);
+  else
+    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
@@ -204,7 +211,8 @@ int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int
   return RMX_OK;
 }
 
-__global__ void fill_table_kernel(uint64_t seed, int64_t V, int k, float scale, float* w, float* emb) {
+template <class T>
+__global__ void fill_table_kernel(uint64_t seed, int64_t V, int k, float scale, T* w, T* emb) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot = V * (k + 1);
   if (i >= tot) return;
@@ -212,40 +220,72 @@ __global__ void fill_table_kernel(uint64_t seed, int64_t V, int k, float scale, 
   const int j = (int)(i - id * (k + 1));
   const uint64_t h = splitmix64(seed ^ (uint64_t)i);  // i == id*(k+1) + j
   const float v = (float)((int32_t)(h >> 40) - 8388608) * scale;
-  if (j < k) emb[id * k + j] = v;
-  else w[id] = v;
+  if (j < k) st1(emb + id * k + j, v);
+  else st1(w + id, v);
 }
 
-int launch_fill_table(hipStream_t s, uint64_t seed, int64_t V, int k, float* w, float* emb) {
+int launch_fill_table(hipStream_t s, uint64_t seed, int64_t V, int k, void* w, void* emb, int dt) {
   const int64_t tot = V * (k + 1);
   const float scale = 0.05f * (1.0f / 8388608.0f);
-  hipLaunchKernelGGL(fill_table_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, V, k,
-                     scale, w, emb);
+  if (dt == kBF16)
+    hipLaunchKernelGGL(fill_table_kernel<bf16_t>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, V, k,
+                       scale, (bf16_t*)w, (bf16_t*)emb);
+  else
+    hipLaunchKernelGGL(fill_table_kernel<float>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, V, k,
+                       scale, (float*)w, (float*)emb);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
 
-__global__ void gather_kernel(int64_t n, const int32_t* __restrict__ ids, const float* __restrict__ wtab,
-                              const float* __restrict__ emb, int k, float* __restrict__ w_out,
-                              float* __restrict__ e_out) {
+template <class T>
+__global__ void gather_kernel(int64_t n, const int32_t* __restrict__ ids, const T* __restrict__ wtab,
+                              const T* __restrict__ emb, int k, float* __restrict__ w_out, float* __restrict__ e_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * (k + 1)) return;
   const int64_t r = i / (k + 1);
   const int j = (int)(i - r * (k + 1));
   const int id = ids[r];
   if (j < k) {
-    if (e_out) e_out[r * k + j] = emb[(int64_t)id * k + j];
+    if (e_out) e_out[r * k + j] = ld1(emb + (int64_t)id * k + j);
   } else if (w_out) {
-    w_out[r] = wtab[id];
+    w_out[r] = ld1(wtab + id);
   }
 }
 
-int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const float* wtab, const float* emb,
-                  int k, float* w_out, float* e_out) {
+int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const void* wtab, const void* emb, int dt, int k,
+                  float* w_out, float* e_out) {
   if (n <= 0) return RMX_OK;
   const int64_t tot = n * (k + 1);
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, ids, wtab, emb,
-                     k, w_out, e_out);
+  if (dt == kBF16)
+    hipLaunchKernelGGL(gather_kernel<bf16_t>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, ids,
+                       (const bf16_t*)wtab, (const bf16_t*)emb, k, w_out, e_out);
+  else
+    hipLaunchKernelGGL(gather_kernel<float>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, n, ids,
+                       (const float*)wtab, (const float*)emb, k, w_out, e_out);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+__global__ void convert_bf16_kernel(const float* __restrict__ src, int64_t n, bf16_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (bf16_t)src[i];
+}
+
+__global__ void widen_bf16_kernel(const bf16_t* __restrict__ src, int64_t n, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (float)src[i];
+}
+
+int launch_widen_bf16(hipStream_t s, const bf16_t* src, int64_t n, float* dst) {
+  if (n <= 0) return RMX_OK;
+  hipLaunchKernelGGL(widen_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n, dst);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+int launch_convert_bf16(hipStream_t s, const float* src, int64_t n, bf16_t* dst) {
+  if (n <= 0) return RMX_OK;
+  hipLaunchKernelGGL(convert_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n, dst);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
@@ -279,29 +319,60 @@ __global__ void pack_linear_kernel(const float* __restrict__ mats, int64_t w_off
   }
 }
 
+// bf16 packing: [Kpad/32][Npad][32] (one 64-B row = 32 bf16 of one output column), RNE rounding
+__global__ void pack_linear_bf16_kernel(const float* __restrict__ mats, int64_t w_off, int64_t w_off2, int K1, int K,
+                                        int N, int Kpad, int Npad, bf16_t* __restrict__ Wp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)Kpad * Npad;
+  if (i >= tot) return;
+  const int kk = (int)(i & 31);
+  const int64_t rest = i >> 5;
+  const int n = (int)(rest % Npad);
+  const int c = (int)(rest / Npad);
+  const int kx = c * 32 + kk;
+  float v = 0.f;
+  if (n < N && kx < K) {
+    if (K1 < 0) v = mats[w_off + (int64_t)n * K + kx];
+    else if (kx < K1) v = mats[w_off + (int64_t)n * K1 + kx];
+    else v = mats[w_off2 + (int64_t)n * (K - K1) + (kx - K1)];
+  }
+  Wp[i] = (bf16_t)v;
+}
+
 int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L) {
   const int64_t tot = (int64_t)L.Kpad * L.Npad;
   const int64_t n = tot > L.Npad ? tot : L.Npad;
+  // bias (and, for fp32 layers, W)
   hipLaunchKernelGGL(pack_linear_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mats_dev,
-                     L.w_off, L.w_off2, L.K1, L.b_off, L.b_off >= 0 ? L.bias_mode : 0, L.K, L.N, L.Kpad,
+                     L.w_off, L.w_off2, L.K1, L.b_off, L.b_off >= 0 ? L.bias_mode : 0, L.K, L.N, L.W16 ? 0 : L.Kpad,
                      L.Npad, L.W, L.b);
   RMX_HIP(hipGetLastError());
+  if (L.W16) {
+    hipLaunchKernelGGL(pack_linear_bf16_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats_dev,
+                       L.w_off, L.w_off2, L.K1, L.K, L.N, L.Kpad, L.Npad, L.W16);
+    RMX_HIP(hipGetLastError());
+  }
   return RMX_OK;
 }
 
-__global__ void transpose_kmajor_kernel(const float* __restrict__ src, int64_t V, int k, float* __restrict__ dst) {
+template <class T>
+__global__ void transpose_kmajor_kernel(const float* __restrict__ src, int64_t V, int k, T* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= V * k) return;
   const int64_t id = i / k;
   const int j = (int)(i - id * k);
-  dst[i] = src[(int64_t)j * V + id];
+  st1(dst + i, src[(int64_t)j * V + id]);
 }
 
-int launch_transpose_kmajor(hipStream_t s, const float* src_kv, int64_t V, int k, float* dst_vk) {
+int launch_transpose_kmajor(hipStream_t s, const float* src_kv, int64_t V, int k, void* dst_vk, int dt) {
   const int64_t tot = V * k;
   if (tot <= 0) return RMX_OK;
-  hipLaunchKernelGGL(transpose_kmajor_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src_kv, V,
-                     k, dst_vk);
+  if (dt == kBF16)
+    hipLaunchKernelGGL(transpose_kmajor_kernel<bf16_t>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src_kv,
+                       V, k, (bf16_t*)dst_vk);
+  else
+    hipLaunchKernelGGL(transpose_kmajor_kernel<float>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, src_kv,
+                       V, k, (float*)dst_vk);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -1,0 +1,491 @@
+// k_gemm.hpp -- the MFMA GEMM engine (fp32, and bf16 for the tower) behind the tower layers and the xDeepFM CIN (gfx950).
+//
+// Tower layer: BigDL Linear + ReLU chain, model/encoder/HigherOrderEncoder.scala:34-59
+// (Linear(in->out, W: out x in, y = b + x W^T) + ReLU per fcDim, then Linear(->1)) and the
+// output heads of DeepFM.scala:130-134 / XDeepFM / DCN / PNN (CAddTable + Sigmoid).
+// CIN layer: model/xdeepfm/CINEncoder.scala:36-58, 105-176 (+ SURVEY.md Appendix A for L > 1):
+//   x0[b,j,f] = e[b,f,j]; z[f*Hp + h] = x0[b,j,f] * u_{l-1}[b,j,h]  (MM(transB = true), :152)
+//   u_l[b,j,:] = ReLU(c_l + C_l z)                                   (Linear + ReLU, :154-155)
+// a GEMM with M = B*k rows (b, j), K = F * Hp, N = H whose A operand is generated in registers
+// (the reference materialises z: B*k x F*Hp floats, 2 GB per layer at B = 4096), and whose
+// epilogue folds the output Linear in: rowdot[b*k + j] (+)= sum_h u_l[b,j,h] * W_out[slice_l + h]
+// (sum_j sum_h == sum_h sum_j: the pooled pi_l . W_out, :159-176).
+//
+// All on v_mfma_f32_16x16x4_f32 (exact f32 FMA chain, 64 FLOP/clk/SIMD = the chip's fp32 peak).
+// Block = WM waves stacked on M; a wave owns MT*16 rows x all NT*16 columns of the block
+// (MT*NT accumulator tiles).  WM is a multiple of 4, so every SIMD carries the same number of
+// waves and the one barrier per K stage never waits on an overloaded SIMD.  K is consumed in
+// 16-wide chunks; inside a chunk lane group g = lane>>4 owns k = 4g..4g+3, so one ds_read_b128
+// per fragment feeds the 4 k-steps of the chunk.  LDS tiles are [rows][16] fp32 with a slot
+// XOR-swizzle that keeps the 16-row fragment reads conflict-free for all four ds_read_b128 lane
+// groups.  A stage holds BKC chunks; the next stage's global loads are issued before the MFMAs
+// of the current one and written to the idle LDS buffer after them (one barrier per stage).
+// A operand producers:
+//   kDenseA     activations of the previous layer, staged through LDS;
+//   kGatherK16  / kGatherAny: first layer, rows gathered straight from the embedding table
+//               (ids staged in LDS; x = Reshape(B, F*k) is never materialised);
+//   kCinOuter   CIN: a = x0[row][f] * u[row][h-chunk], computed in registers (x0 tile in LDS,
+//               u chunk in registers), only the weights go through LDS.
+#pragma once
+
+#include <algorithm>
+
+#include "rmx_models.hpp"
+
+namespace rmx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// physical 16-B slot of logical slot g in row `row` of a [rows][16] fp32 LDS tile
+__device__ __forceinline__ int swz_slot(int row, int g) { return g ^ ((4 - ((row >> 2) & 3)) & 3); }
+
+enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
+enum EpiMode : int { kEpiRelu = 0, kEpiOutput = 1, kEpiCin = 2 };
+
+struct GemmArgs {
+  int M, K, Kpad, Npad;
+  const float* A;  // kDenseA: [M][lda]
+  int lda;
+  AGatherArgs ga;  // gather modes (ids, table, F, k); kCinOuter: ids, table, F, k of x0
+  // kCinOuter
+  const float* u_prev;  // [M][ldu] previous CIN maps, nullptr for the first layer (u = x0)
+  int ldu, XS, cin_first;
+  const float* Wp;     // [Kpad/16][Npad][16]
+  const float* bias;   // [Npad]
+  float* C;            // kEpiRelu / kEpiCin (u_out, may be null): [M][ldc]
+  int ldc;
+  OutArgs oa;          // kEpiOutput
+  const float* wo;     // kEpiCin: [Npad] slice of the output Linear
+  float* rowdot;       // kEpiCin: [M]
+};
+
+// Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
+// tiles); the block spans BM = WM*MT*16 rows and BN = WN*NTW*16 columns.  BKC 16-wide K chunks per
+// LDS stage.  OCC = minimum waves per SIMD the register allocation must allow (launch bounds).
+template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_>
+struct Tile {
+  static constexpr int MT = MT_, NTW = NTW_, WM = WM_, WN = WN_, BKC = BKC_, OCC = OCC_;
+  static constexpr int NW = WM * WN, NTHR = NW * 64, NT = NTW * WN;
+  static constexpr int BM = WM * MT * 16, BN = NT * 16;
+};
+
+template <class T, int AMODE>
+struct StageGeom {
+  static constexpr int AROWS = AMODE != kCinOuter ? T::BM * T::BKC : 0;
+  static constexpr int ROWS = AROWS + T::BN * T::BKC;  // 64-B rows per stage
+  static constexpr int FLOATS = ROWS * 16;
+};
+
+// Epilogue slab geometry: each wave transposes NTH of its column tiles at a time through a
+// private [RW][LD] fp32 slab carved from the (then idle) stage buffers, or more LDS if needed.
+template <class T, int STAGE_FLOATS>
+struct EpiGeom {
+  static constexpr int RW = T::MT * 16;
+  static constexpr int WF = (2 * STAGE_FLOATS) / T::NW;
+  static constexpr int NTH0 = (WF / RW - 4) / 16;
+  static constexpr int NTH = NTH0 < T::NTW ? (NTH0 < 1 ? 1 : NTH0) : T::NTW;
+  static constexpr int LD = NTH * 16 + 4;  // == 4 mod 8: the two 16-lane halves of a write hit disjoint banks
+  static constexpr int FLOATS = RW * LD * T::NW;
+};
+
+template <class T, int AMODE, int EPI, bool BF>
+__global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
+  // BF: bf16 operands (v_mfma_f32_16x16x32_bf16, K chunk of 32 per 64-B row), fp32 accumulate,
+  // bf16 stored activations; otherwise fp32 throughout (v_mfma_f32_16x16x4_f32, K chunk 16).
+  constexpr int KC = BF ? 32 : 16, KS = KC / 4;  // elements per chunk row / per 16-B slot
+  static_assert(!BF || AMODE != kCinOuter, "CIN is fp32 only");
+  constexpr int MT = T::MT, NTW = T::NTW, WN = T::WN, BKC = T::BKC;
+  constexpr int BM = T::BM, BN = T::BN, NTHR = T::NTHR;
+  constexpr bool A_LDS = AMODE != kCinOuter;
+  using SG = StageGeom<T, AMODE>;
+  constexpr int AROWS = SG::AROWS, ROWS = SG::ROWS, STAGE = SG::FLOATS;
+  constexpr int ITEMS = ROWS * 4;  // float4 items per stage
+  constexpr int PER = (ITEMS + NTHR - 1) / NTHR;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* lds0 = smem;
+  float* lds1 = smem + STAGE;
+  float* extra = smem + 2 * STAGE;  // gather: int ids [BM][F]; CIN: x0 [BM][XS]
+  int* sids = reinterpret_cast<int*>(extra);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int M = p.M;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = p.Kpad / KC;
+  const int nstages = (nchunks + BKC - 1) / BKC;
+  const int F = p.ga.F;
+
+  if constexpr (AMODE == kGatherK16 || AMODE == kGatherAny) {
+    for (int i = tid; i < BM * F; i += NTHR) {
+      const int r = i / F, f = i - r * F;
+      const int m = m0 + r;
+      int id = 0;
+      if (m < M) id = p.ga.ids ? p.ga.ids[(int64_t)m * F + f] : m * F + f;
+      sids[i] = id;
+    }
+    __syncthreads();
+  }
+  if constexpr (AMODE == kCinOuter) {
+    // x0 tile: x0s[r][f] = e[b, f, j] for row m0 + r = b*k + j, zero padded to XS columns
+    const int k = p.ga.k, XS = p.XS;
+    for (int i = tid; i < BM * XS; i += NTHR) {
+      const int j = i % k;
+      const int rest = i / k;
+      const int f = rest % XS;
+      const int rb = rest / XS;
+      const int r = rb * k + j;
+      if (r >= BM) continue;
+      const int m = m0 + r;
+      float v = 0.f;
+      if (f < F && m < M) {
+        const int b = m / k;
+        const int id = p.ga.ids ? p.ga.ids[(int64_t)b * F + f] : b * F + f;
+        v = p.ga.table[(int64_t)id * k + j];
+      }
+      extra[r * XS + f] = v;
+    }
+    __syncthreads();
+  }
+
+  f32x4 acc[MT][NTW];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 stage[PER];
+  // item i of a stage: row = i >> 2 (A rows first: [BKC][BM], then B rows [BKC][BN]), slot g = i & 3
+  auto gload = [&](int st) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = tid + q * NTHR;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int row = i >> 2, g = i & 3;
+      if (row < AROWS) {
+        const int cc = row / BM, r = row - cc * BM;
+        const int c = st * BKC + cc;
+        const int m = m0 + r;
+        const int kk = c * KC + g * KS;
+        if (m < M && kk < p.K) {
+          if constexpr (AMODE == kGatherK16) {
+            // fp32: chunk c = field c; bf16: chunk c = fields 2c, 2c+1 (two 32-B rows)
+            const int f = BF ? 2 * c + (g >> 1) : c;
+            const int id = sids[r * F + f];
+            v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * 16 +
+                                                       (g & 1) * 8)
+                   : *reinterpret_cast<const float4*>(p.ga.table + (int64_t)id * 16 + g * 4);
+          } else if constexpr (AMODE == kGatherAny) {
+            const int f = kk / p.ga.k, j = kk - f * p.ga.k;
+            const int id = sids[r * F + f];
+            v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.ga.table) +
+                                                       (int64_t)id * p.ga.k + j)
+                   : *reinterpret_cast<const float4*>(p.ga.table + (int64_t)id * p.ga.k + j);
+          } else {
+            v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.A) + (int64_t)m * p.lda + kk)
+                   : *reinterpret_cast<const float4*>(p.A + (int64_t)m * p.lda + kk);
+          }
+        }
+      } else if (row < ROWS) {
+        const int rb = row - AROWS;
+        const int cc = rb / BN, n = rb - cc * BN;
+        const int c = st * BKC + cc;
+        if (c < nchunks)
+          v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.Wp) +
+                                                     ((int64_t)c * p.Npad + n0 + n) * 32 + g * 8)
+                 : *reinterpret_cast<const float4*>(p.Wp + ((int64_t)c * p.Npad + n0 + n) * 16 + g * 4);
+      }
+      stage[q] = v;
+    }
+  };
+  auto sstore = [&](float* buf) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int i = tid + q * NTHR;
+      const int row = i >> 2, g = i & 3;
+      if (row < ROWS) {
+        const int lrow = row < AROWS ? (row % BM) : ((row - AROWS) % BN);
+        *reinterpret_cast<float4*>(buf + row * 16 + swz_slot(lrow, g) * 4) = stage[q];
+      }
+    }
+  };
+
+  gload(0);
+  sstore(lds0);
+  __syncthreads();
+
+  const int g = lane >> 4, r16 = lane & 15;
+  int arow[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) arow[i] = wm * MT * 16 + i * 16 + r16;
+  const int bt0 = wn * NTW;  // first column tile of this wave
+
+  // kCinOuter: the row's u[h-chunk] for the current hc, reloaded when hc changes
+  float4 uf[MT];
+  int cur_hc = -1;
+  auto load_u = [&](int hc) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (p.cin_first) {
+        uf[i] = *reinterpret_cast<const float4*>(extra + arow[i] * p.XS + hc * 16 + g * 4);
+      } else {
+        const int m = m0 + arow[i];
+        uf[i] = m < M ? *reinterpret_cast<const float4*>(p.u_prev + (int64_t)m * p.ldu + hc * 16 + g * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    cur_hc = hc;
+  };
+
+  for (int st = 0; st < nstages; ++st) {
+    const float* cur = (st & 1) ? lds1 : lds0;
+    float* nxt = (st & 1) ? lds0 : lds1;
+    const bool more = st + 1 < nstages;
+    if (more) gload(st + 1);
+#pragma unroll
+    for (int cc = 0; cc < BKC; ++cc) {
+      const int c = st * BKC + cc;
+      if (BKC > 1 && c >= nchunks) break;
+      const float* Bt = cur + AROWS * 16 + cc * BN * 16;
+      f32x4 a[MT];
+      if constexpr (A_LDS) {
+        const float* At = cur + cc * BM * 16;
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          a[i] = *reinterpret_cast<const f32x4*>(At + arow[i] * 16 + swz_slot(arow[i], g) * 4);
+      } else {
+        const int hc = c / F, f = c - hc * F;
+        if (hc != cur_hc) load_u(hc);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const float xv = extra[arow[i] * p.XS + f];
+          a[i] = f32x4{xv * uf[i].x, xv * uf[i].y, xv * uf[i].z, xv * uf[i].w};
+        }
+      }
+      // groups of >= 4 independent accumulator tiles: consecutive MFMAs of one tile are a group
+      // apart (>= 128 cycles), past the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32
+      constexpr int NG = NTW >= 4 ? NTW / 4 : 1;
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) {
+        const int j0 = gi * NTW / NG, j1 = (gi + 1) * NTW / NG;
+        f32x4 b[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if (j0 + t < j1) {
+            const int row = (bt0 + j0 + t) * 16 + r16;
+            b[t] = *reinterpret_cast<const f32x4*>(Bt + row * 16 + swz_slot(row, g) * 4);
+          }
+        if constexpr (BF) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (j0 + t < j1)
+#pragma unroll
+              for (int i = 0; i < MT; ++i)
+                acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                    __builtin_bit_cast(bf16x8, a[i]), __builtin_bit_cast(bf16x8, b[t]), acc[i][j0 + t], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+              if (j0 + t < j1)
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+                  acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s4], b[t][s4], acc[i][j0 + t], 0, 0, 0);
+        }
+      }
+    }
+    if (more) sstore(nxt);
+    __syncthreads();
+  }
+
+  // C/D layout of 16x16 MFMA: lane holds rows 4*(lane>>4) + r (r = 0..3), column lane & 15.
+  // Stored activations go through LDS (each wave transposes its rows into a private slab of the
+  // now idle stage buffers) so the global stores are whole-row float4s instead of 4-B scatters.
+  auto store_rows = [&](float* dst, int ldd) {
+    using EG = EpiGeom<T, STAGE>;
+    constexpr int RW = EG::RW, NTH = EG::NTH, LD = EG::LD;
+    float* wbuf = smem + wid * RW * LD;
+#pragma unroll
+    for (int j0 = 0; j0 < NTW; j0 += NTH) {
+#pragma unroll
+      for (int t = 0; t < NTH; ++t) {
+        if (j0 + t >= NTW) break;
+        const float bn = p.bias[n0 + (bt0 + j0 + t) * 16 + r16];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[i][j0 + t][r] + bn;
+            wbuf[(i * 16 + g * 4 + r) * LD + t * 16 + r16] = v > 0.f ? v : 0.f;
+          }
+      }
+      __syncthreads();
+      const int nf4 = ((NTW - j0 < NTH) ? (NTW - j0) : NTH) * 4;
+      for (int q = lane; q < RW * nf4; q += 64) {
+        const int rr = q / nf4, c4 = q - rr * nf4;
+        const int m = m0 + wm * RW + rr;
+        if (m < M) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(wbuf + rr * LD + c4 * 4);
+          const int64_t o = (int64_t)m * ldd + n0 + (bt0 + j0) * 16 + c4 * 4;
+          if constexpr (BF)
+            *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(dst) + o) = __builtin_convertvector(v, bf16x4);
+          else
+            *reinterpret_cast<f32x4*>(dst + o) = v;
+        }
+      }
+      __syncthreads();
+    }
+  };
+  if constexpr (EPI == kEpiRelu) {
+    store_rows(p.C, p.ldc);
+  } else {
+    // row reduction sum_n ReLU(acc + b)[n] * w[n] over the block's (= the layer's) columns;
+    // with WN > 1 the waves of a row group add their partial sums through LDS
+    float* red = smem;  // [WN][BM], the stage buffers are idle after the last barrier
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int rl = wm * MT * 16 + i * 16 + g * 4;  // block-local first row of the lane group
+      float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int n = (bt0 + j) * 16 + r16;
+        const float bn = p.bias[n];
+        const float wv = EPI == kEpiOutput ? p.oa.wo[n] : p.wo[n];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bn;
+          v = v > 0.f ? v : 0.f;
+          part[r] += v * wv;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = part[r];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        part[r] = v;
+      }
+      if (r16 < 4) {
+        const float y = r16 == 0 ? part[0] : (r16 == 1 ? part[1] : (r16 == 2 ? part[2] : part[3]));
+        red[wn * BM + rl + r16] = y;
+      }
+    }
+    __syncthreads();
+    for (int rl = tid; rl < BM; rl += NTHR) {
+      const int m = m0 + rl;
+      if (m >= M) continue;
+      float y = red[rl];
+#pragma unroll
+      for (int w = 1; w < WN; ++w) y += red[w * BM + rl];
+      if constexpr (EPI == kEpiCin) {
+        p.rowdot[m] = p.cin_first ? y : p.rowdot[m] + y;
+      } else {
+        const OutArgs& oa = p.oa;
+        if (oa.has_bo) y = y + oa.bo;
+        if (oa.rowsum) {
+          float rs = 0.f;
+          for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
+          y = rs + y;
+        }
+        if (oa.pre2) y = oa.pre2[m] + y;
+        float t = oa.pre ? oa.pre[m] + y : y;
+        t = t + oa.beta;
+        oa.out[m] = 1.0f / (1.0f + expf(-t));
+      }
+    }
+    if constexpr (EPI == kEpiCin) {
+      if (p.C) {
+        __syncthreads();  // red[] lives in the slab area
+        store_rows(p.C, p.ldc);  // u_l for the next CIN layer
+      }
+    }
+  }
+}
+
+
+// -------------------------------------------------------------- dispatch ----
+
+// column tiles per block that have kernels (a layer's Npad is a multiple of one of them)
+constexpr int kNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16, 20, 25, 26};
+constexpr int kCinNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16};
+
+template <class T, int AMODE, int EPI, bool BF = false>
+int launch_cfg(hipStream_t s, GemmArgs& p) {
+  using SG = StageGeom<T, AMODE>;
+  size_t lds = sizeof(float) * 2 * SG::FLOATS;
+  if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * T::BM * p.ga.F;
+  if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
+  if (EPI != kEpiOutput) lds = std::max(lds, sizeof(float) * EpiGeom<T, SG::FLOATS>::FLOATS);
+  lds = std::max(lds, sizeof(float) * T::WN * T::BM);  // row-reduction partials
+  if (lds > 160 * 1024) {
+    set_error("gemm: LDS budget exceeded (" + std::to_string(lds) + " bytes)");
+    return RMX_E_INVALID;
+  }
+  if (p.Npad % T::BN) {
+    set_error("gemm: Npad " + std::to_string(p.Npad) + " is not a multiple of the block width");
+    return RMX_E_INVALID;
+  }
+  dim3 grid((p.M + T::BM - 1) / T::BM, p.Npad / T::BN);
+  auto kern = gemm_kernel<T, AMODE, EPI, BF>;
+  if (lds > 64 * 1024)
+    RMX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(kern, grid, dim3(T::NTHR), lds, s, p);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+template <class T, bool BF>
+int launch_epi(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
+#define RMX_EPI(AM)                                                          \
+  if (epi == Epi::kReluStore) return launch_cfg<T, AM, kEpiRelu, BF>(s, p); \
+  return launch_cfg<T, AM, kEpiOutput, BF>(s, p);
+  if (amode == kDenseA) { RMX_EPI(kDenseA) }
+  if (amode == kGatherK16) { RMX_EPI(kGatherK16) }
+  RMX_EPI(kGatherAny)
+#undef RMX_EPI
+}
+
+template <int NT, bool BF>
+int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
+  // Large batches: 8-wave blocks.  Knob "tower_variant":
+  //   0: 8 waves on M (BM 128) x all NT tiles per wave, 2 waves / SIMD (1 block per CU);
+  //   1: 4 x 2 waves (BM 64, NT/2 tiles per wave), one K chunk per stage, 4 waves / SIMD
+  //      (2 blocks per CU, their barriers interleave);
+  //   2: 8 x 2 waves (16 waves, BM 128), 4 waves / SIMD in one block.
+  // Variants 1 / 2 need an even NT (the model packs N = 400 as 26 tiles when tower_split = 1).
+  // Small batches: 4-wave blocks.
+  const int var = NT % 2 == 0 ? tuning_get("tower_variant", 0) : 0;
+  const bool dense = amode == kDenseA;
+  if (p.M >= 8192) {
+    if (var == 1) return launch_epi<Tile<1, (NT + 1) / 2, 4, 2, 1, 4>, BF>(s, p, amode, epi);
+    if (var == 2) {
+      if (dense) return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 2, 4>, BF>(s, p, amode, epi);
+      return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 1, 4>, BF>(s, p, amode, epi);
+    }
+    if (dense) return launch_epi<Tile<1, NT, 8, 1, 2, 1>, BF>(s, p, amode, epi);
+    return launch_epi<Tile<1, NT, 8, 1, 1, 1>, BF>(s, p, amode, epi);
+  }
+  return launch_epi<Tile<1, NT, 4, 1, 1, 1>, BF>(s, p, amode, epi);
+}
+
+template <int NT>
+int launch_cin_nt(hipStream_t s, GemmArgs& p) {
+  // knob "cin_variant": 0 = 8 waves x 16 rows, 2 chunks per stage, 4 waves / SIMD (two blocks
+  // per CU: 1.637 ms / layer at B = 4,096 vs 1.84 at 3 waves / SIMD); 1 = 8 waves x 32 rows.
+  // Small M always uses 4 waves x 16 rows.
+  const int var = tuning_get("cin_variant", 0);
+  if (p.M < 8192) return launch_cfg<Tile<1, NT, 4, 1, 2, 1>, kCinOuter, kEpiCin>(s, p);
+  if (var == 1) return launch_cfg<Tile<2, NT, 8, 1, 2, 1>, kCinOuter, kEpiCin>(s, p);
+  return launch_cfg<Tile<1, NT, 8, 1, 2, 4>, kCinOuter, kEpiCin>(s, p);
+}
+
+
+int launch_tower_bf16(hipStream_t s, GemmArgs& p, int nt, int amode, Epi epi);
+
+}  // namespace rmx

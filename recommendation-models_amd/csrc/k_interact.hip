@@ -23,8 +23,9 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+template <class T>
 __global__ __launch_bounds__(256) void cross_kernel(int B, int F, int k, int L, const int32_t* __restrict__ ids,
-                                                    const float* __restrict__ table,
+                                                    const T* __restrict__ table,
                                                     const float* __restrict__ cross_w,
                                                     const float* __restrict__ cross_b,
                                                     const float* __restrict__ wo_x, float* __restrict__ pre2) {
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(256) void cross_kernel(int B, int F, int k, int L, 
     if (d < D) {
       const int f = d / k, j = d - (d / k) * k;
       const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
-      v = table[(int64_t)id * k + j];
+      v = ld1(table + (int64_t)id * k + j);
     }
     x0[i] = v;
     xl[i] = v;
@@ -68,23 +69,29 @@ __global__ __launch_bounds__(256) void cross_kernel(int B, int F, int k, int L, 
   if (lane == 0) pre2[b] = y;
 }
 
-int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const float* table,
+int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const void* table, int dt,
                  const float* cross_w, const float* cross_b, const float* wo_x, float* pre2) {
   if (B <= 0) return RMX_OK;
   if (F * k > 64 * kCrossNPL) {
     set_error("cross: nFields * embeddingDim must be <= 1024");
     return RMX_E_INVALID;
   }
-  hipLaunchKernelGGL(cross_kernel, dim3((B + 3) / 4), dim3(256), 0, s, B, F, k, L, ids, table, cross_w, cross_b,
-                     wo_x, pre2);
+  if (dt == kBF16)
+    hipLaunchKernelGGL(cross_kernel<bf16_t>, dim3((B + 3) / 4), dim3(256), 0, s, B, F, k, L, ids,
+                       (const bf16_t*)table, cross_w, cross_b, wo_x, pre2);
+  else
+    hipLaunchKernelGGL(cross_kernel<float>, dim3((B + 3) / 4), dim3(256), 0, s, B, F, k, L, ids,
+                       (const float*)table, cross_w, cross_b, wo_x, pre2);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
 
+// T: table elements; X: [x | ip] row elements (bf16 rows feed the bf16 GEMM: ip rounded once)
+template <class T, class X>
 __global__ __launch_bounds__(256) void product_kernel(int B, int F, int k, const int32_t* __restrict__ ids,
-                                                      const float* __restrict__ table,
+                                                      const T* __restrict__ table,
                                                       const int32_t* __restrict__ pairs, int P,
-                                                      float* __restrict__ xbuf, int ldx) {
+                                                      X* __restrict__ xbuf, int ldx) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) float es[];
   const int D = F * k;
@@ -95,9 +102,9 @@ __global__ __launch_bounds__(256) void product_kernel(int B, int F, int k, const
     for (int d = lane; d < D; d += 64) {
       const int f = d / k, j = d - f * k;
       const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
-      const float v = table[(int64_t)id * k + j];
+      const float v = ld1(table + (int64_t)id * k + j);
       e[d] = v;
-      xbuf[(int64_t)b * ldx + d] = v;
+      st1(xbuf + (int64_t)b * ldx + d, v);
     }
   }
   __syncthreads();
@@ -106,23 +113,35 @@ __global__ __launch_bounds__(256) void product_kernel(int B, int F, int k, const
     const int i = pairs[2 * p], j = pairs[2 * p + 1];
     float acc = 0.f;
     for (int t = 0; t < k; ++t) acc += e[i * k + t] * e[j * k + t];
-    xbuf[(int64_t)b * ldx + D + p] = acc;
+    st1(xbuf + (int64_t)b * ldx + D + p, acc);
   }
-  for (int c = D + P + lane; c < ldx; c += 64) xbuf[(int64_t)b * ldx + c] = 0.f;
+  for (int c = D + P + lane; c < ldx; c += 64) st1(xbuf + (int64_t)b * ldx + c, 0.f);
 }
 
-int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table, const int32_t* pairs,
-                   int P, float* xbuf, int ldx) {
+int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt,
+                   const int32_t* pairs, int P, void* xbuf, int xdt, int ldx) {
   if (B <= 0) return RMX_OK;
   const size_t lds = sizeof(float) * 4 * (F * k + 1);
-  hipLaunchKernelGGL(product_kernel, dim3((B + 3) / 4), dim3(256), lds, s, B, F, k, ids, table, pairs, P, xbuf,
-                     ldx);
+  const dim3 grid((B + 3) / 4), blk(256);
+  if (dt == kBF16 && xdt == kBF16)
+    hipLaunchKernelGGL((product_kernel<bf16_t, bf16_t>), grid, blk, lds, s, B, F, k, ids, (const bf16_t*)table, pairs,
+                       P, (bf16_t*)xbuf, ldx);
+  else if (dt == kBF16)
+    hipLaunchKernelGGL((product_kernel<bf16_t, float>), grid, blk, lds, s, B, F, k, ids, (const bf16_t*)table, pairs,
+                       P, (float*)xbuf, ldx);
+  else if (xdt == kBF16)
+    hipLaunchKernelGGL((product_kernel<float, bf16_t>), grid, blk, lds, s, B, F, k, ids, (const float*)table, pairs,
+                       P, (bf16_t*)xbuf, ldx);
+  else
+    hipLaunchKernelGGL((product_kernel<float, float>), grid, blk, lds, s, B, F, k, ids, (const float*)table, pairs, P,
+                       (float*)xbuf, ldx);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
 
+template <class T, class X>
 __global__ void gather_x_kernel(int B, int F, int k, const int32_t* __restrict__ ids,
-                                const float* __restrict__ table, float* __restrict__ xbuf, int ldx) {
+                                const T* __restrict__ table, X* __restrict__ xbuf, int ldx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * ldx) return;
   const int64_t b = i / ldx;
@@ -131,17 +150,28 @@ __global__ void gather_x_kernel(int B, int F, int k, const int32_t* __restrict__
   if (d < F * k) {
     const int f = d / k, j = d - f * k;
     const int id = ids ? ids[b * F + f] : (int)(b * F + f);
-    v = table[(int64_t)id * k + j];
+    v = ld1(table + (int64_t)id * k + j);
   }
-  xbuf[i] = v;
+  st1(xbuf + i, v);
 }
 
-int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table, float* xbuf,
-                    int ldx) {
+int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt, void* xbuf,
+                    int xdt, int ldx) {
   const int64_t tot = (int64_t)B * ldx;
   if (tot <= 0) return RMX_OK;
-  hipLaunchKernelGGL(gather_x_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, B, F, k, ids, table,
-                     xbuf, ldx);
+  const dim3 grid((unsigned)((tot + 255) / 256)), blk(256);
+  if (dt == kBF16 && xdt == kBF16)
+    hipLaunchKernelGGL((gather_x_kernel<bf16_t, bf16_t>), grid, blk, 0, s, B, F, k, ids, (const bf16_t*)table,
+                       (bf16_t*)xbuf, ldx);
+  else if (dt == kBF16)
+    hipLaunchKernelGGL((gather_x_kernel<bf16_t, float>), grid, blk, 0, s, B, F, k, ids, (const bf16_t*)table,
+                       (float*)xbuf, ldx);
+  else if (xdt == kBF16)
+    hipLaunchKernelGGL((gather_x_kernel<float, bf16_t>), grid, blk, 0, s, B, F, k, ids, (const float*)table,
+                       (bf16_t*)xbuf, ldx);
+  else
+    hipLaunchKernelGGL((gather_x_kernel<float, float>), grid, blk, 0, s, B, F, k, ids, (const float*)table,
+                       (float*)xbuf, ldx);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

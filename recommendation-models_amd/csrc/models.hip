@@ -127,7 +127,8 @@ void dev_free(T*& p) {
   p = nullptr;
 }
 
-bool needs_gather_x(const rmx_model& m) { return m.k % 4 != 0; }
+// the GEMM gathers 16-B slots straight from table rows: k must be a multiple of 4 fp32 / 8 bf16
+bool needs_gather_x(const rmx_model& m) { return m.k % (m.precision == kBF16 ? 8 : 4) != 0; }
 
 }  // namespace
 
@@ -359,6 +360,7 @@ void model_release(rmx_model& m) {
   dev_free(m.mats_dev);
   for (auto& L : m.layers) {
     dev_free(L.W);
+    dev_free(L.W16);
     dev_free(L.b);
   }
   dev_free(m.wo);
@@ -381,6 +383,8 @@ void model_release(rmx_model& m) {
   dev_free(m.rowdot);
   dev_free(m.la_E);
   dev_free(m.la_w);
+  dev_free(m.la_E16);
+  dev_free(m.la_w16);
   dev_free(m.la_rowptr);
   dev_free(m.la_out);
   for (auto& p : m.pending) {
@@ -399,6 +403,33 @@ static int copy_slice(hipStream_t s, const float* src, int n, int npad, float* d
   if (npad <= 0) return RMX_OK;
   hipLaunchKernelGGL(copy_slice_kernel, dim3((npad + 255) / 256), dim3(256), 0, s, src, n, npad, dst);
   RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// Switch the parameter storage of the GEMM layers between fp32 and bf16 (before set_mats).
+int model_set_precision(rmx_model& m, int dtype) {
+  RMX_HIP(hipSetDevice(m.ctx->device));
+  RMX_HIP(hipStreamSynchronize(m.ctx->stream));
+  for (auto& L : m.layers) {
+    dev_free(L.W);
+    dev_free(L.W16);
+    L.Kpad = round_up(L.K, dtype == kBF16 ? 32 : kChunk);
+    if (dtype == kBF16) {
+      if (hipMalloc(&L.W16, sizeof(bf16_t) * (size_t)L.Kpad * L.Npad) != hipSuccess) {
+        set_error("out of device memory");
+        return RMX_E_NOMEM;
+      }
+    } else {
+      int st = dev_alloc(&L.W, (size_t)L.Kpad * L.Npad);
+      if (st) return st;
+    }
+  }
+  m.precision = dtype;
+  m.params_ready = false;
+  // workspaces depend on Kpad (PNN [x | ip] rows): rebuild on the next call
+  RMX_HIP(hipStreamSynchronize(m.ctx->stream));
+  dev_free(m.xbuf);
+  m.ws_B = 0;
   return RMX_OK;
 }
 
@@ -532,19 +563,19 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   if (m.type == RMX_MODEL_LR) {
     StageTimer t(m, s, "first_order_sigmoid");
     if (in.y1) return launch_sigmoid_out(s, B, in.y1, in.beta, in.out);
-    return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, F, 0, nullptr, &in.beta, in.out);
+    return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out);
   }
 
   // 1. first order (+ FM for DeepFM)
   const float* pre = nullptr;
   if (m.type == RMX_MODEL_DEEPFM) {
     StageTimer t(m, s, "encoder_fm");
-    st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, F, k, m.y12, nullptr, nullptr);
+    st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr);
     pre = m.y12;
   } else if (m.type != RMX_MODEL_DNN) {
     if (!in.y1) {
       StageTimer t(m, s, "first_order");
-      st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, F, k, m.y12, nullptr, nullptr);
+      st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr);
     }
     pre = m.y12;  // (the L-A irregular path already wrote y1 here)
   }
@@ -560,7 +591,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   oa.out = in.out;
   const float* A = nullptr;
   int lda = 0;
-  AGatherArgs ga{in.ids, in.table, F, k};
+  AGatherArgs ga{in.ids, (const float*)in.table, F, k};
   bool gather_first = !needs_gather_x(m);
 
   if (m.type == RMX_MODEL_XDEEPFM) {
@@ -569,7 +600,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
       StageTimer t(m, s, l == 0 ? "cin_layer1" : (l == 1 ? "cin_layer2" : "cin_layer3+"));
       const bool last = l + 1 == m.cin_layers.size();
       float* uout = last ? nullptr : m.ubuf[l & 1];
-      if ((st = launch_cin_layer(s, m.cin_layers[l], l == 0, last, B, F, k, in.ids, in.table, uprev, uout,
+      if ((st = launch_cin_layer(s, m.cin_layers[l], l == 0, last, B, F, k, in.ids, (const float*)in.table, uprev, uout,
                                  m.rowdot)))
         return st;
       uprev = uout;
@@ -578,13 +609,14 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     oa.rowsum_k = k;
   } else if (m.type == RMX_MODEL_DCN) {
     StageTimer t(m, s, "cross");
-    if ((st = launch_cross(s, B, F, k, m.cross_depth, in.ids, in.table, m.cross_w, m.cross_b, m.wo_x,
+    if ((st = launch_cross(s, B, F, k, m.cross_depth, in.ids, in.table, in.dtype, m.cross_w, m.cross_b, m.wo_x,
                            m.pre2)))
       return st;
     oa.pre2 = m.pre2;
   } else if (m.type == RMX_MODEL_PNN) {
     StageTimer t(m, s, "product");
-    if ((st = launch_product(s, B, F, k, in.ids, in.table, m.pairs, F * (F - 1) / 2, m.xbuf, m.layers[0].Kpad)))
+    if ((st = launch_product(s, B, F, k, in.ids, in.table, in.dtype, m.pairs, F * (F - 1) / 2, m.xbuf, m.precision,
+                              m.layers[0].Kpad)))
       return st;
     A = m.xbuf;
     lda = m.layers[0].Kpad;
@@ -592,7 +624,8 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   }
   if (m.type != RMX_MODEL_PNN && !gather_first) {
     StageTimer t(m, s, "gather_x");
-    if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, m.xbuf, m.layers[0].Kpad))) return st;
+    if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, in.dtype, m.xbuf, m.precision, m.layers[0].Kpad)))
+      return st;
     A = m.xbuf;
     lda = m.layers[0].Kpad;
   }
@@ -659,6 +692,26 @@ int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, b
       RMX_HIP(hipMemcpyAsync(m.la_w, weights, sizeof(float) * nnz, hipMemcpyHostToDevice, s));
     }
   }
+  if (m.precision == kBF16 && nnz > 0) {
+    // a bf16 model reads the caller's fp32 arrays as a bf16 table: round them once on the device
+    // (la_w in place too, so the Scatter first order below sums the rounded weights)
+    if (nnz * std::max(m.k, 1) > m.la16_cap) {
+      RMX_HIP(hipStreamSynchronize(s));
+      dev_free(m.la_E16);
+      dev_free(m.la_w16);
+      if (hipMalloc(&m.la_E16, sizeof(bf16_t) * nnz * std::max(m.k, 1)) != hipSuccess ||
+          hipMalloc(&m.la_w16, sizeof(bf16_t) * nnz) != hipSuccess) {
+        set_error("out of device memory");
+        return RMX_E_NOMEM;
+      }
+      m.la16_cap = nnz * std::max(m.k, 1);
+    }
+    if (m.type != RMX_MODEL_LR && (st = launch_convert_bf16(s, m.la_E, nnz * m.k, m.la_E16))) return st;
+    if (use_w) {
+      if ((st = launch_convert_bf16(s, m.la_w, nnz, m.la_w16))) return st;
+      if ((st = launch_widen_bf16(s, m.la_w16, nnz, m.la_w))) return st;
+    }
+  }
   if (csr) {
     if (sorted) {
       m.h_rowptr.assign(B + 1, 0);
@@ -673,6 +726,11 @@ int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, b
   in.ids = nullptr;
   in.table = m.la_E;
   in.wtab = m.la_w;
+  if (m.precision == kBF16) {
+    in.table = m.la_E16;
+    in.wtab = m.la_w16;
+    in.dtype = kBF16;
+  }
   in.y1 = csr ? m.y12 : nullptr;
   in.beta = bias;
   in.out = m.la_out;

@@ -11,6 +11,23 @@
 
 namespace rmx {
 
+typedef __bf16 bf16_t;
+
+// element types of tables / activations (include/rmx.h RMX_DTYPE_*)
+constexpr int kF32 = 0, kBF16 = 1;
+
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+// four consecutive elements as fp32 (bf16 -> fp32 is exact)
+__device__ __forceinline__ float4 load4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 load4(const bf16_t* p) {
+  const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(p);
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t* p) { return (float)*p; }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = (bf16_t)v; }  // RNE (v_cvt_pk_bf16_f32)
+
 void set_error(const std::string& msg);
 int tuning_get(const char* key, int def);  // rmx_set_tuning knobs (capi.hip)
 
@@ -35,7 +52,8 @@ struct DenseLayer {
   int K1 = -1;          // PNN: columns [0, K1) come from W at w_off (N x K1), [K1, K) from
   int64_t w_off2 = -1;  //      W2 at w_off2 (N x (K - K1)): Linear(x) + Linear(ip) as one GEMM
   int bias_mode = 1;    // 0 none, 1 per-output bias[N], 2 one scalar broadcast (CAdd(1))
-  float* W = nullptr;   // device, packed
+  float* W = nullptr;   // device, packed fp32 [Kpad/16][Npad][16]
+  bf16_t* W16 = nullptr;  // device, packed bf16 [Kpad/32][Npad][32] (bf16 models; W unused then)
   float* b = nullptr;   // device [Npad]
 };
 
@@ -47,7 +65,7 @@ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 // A operand producer for the first tower layer.
 struct AGatherArgs {
   const int32_t* ids;  // [M][F] or nullptr (implicit id = m*F + f, the L-A path)
-  const float* table;  // [rows][k]
+  const float* table;  // [rows][k] (bf16 elements for bf16 models: reinterpreted)
   int F, k;
 };
 
@@ -71,15 +89,17 @@ struct OutArgs {
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa);
 
-int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const float* table,
-                   const float* wtab, int F, int k, float* y, const float* beta, float* prob);
+int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table,
+                   const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob);
 int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y);
 int launch_sigmoid_out(hipStream_t s, int B, const float* y, float beta, float* out);
 int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids);
-int launch_fill_table(hipStream_t s, uint64_t seed, int64_t V, int k, float* w, float* emb);
-int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const float* wtab,
-                  const float* emb, int k, float* w_out, float* e_out);
+int launch_fill_table(hipStream_t s, uint64_t seed, int64_t V, int k, void* w, void* emb, int dt);
+int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const void* wtab,
+                  const void* emb, int dt, int k, float* w_out, float* e_out);
+int launch_convert_bf16(hipStream_t s, const float* src, int64_t n, bf16_t* dst);
+int launch_widen_bf16(hipStream_t s, const bf16_t* src, int64_t n, float* dst);
 int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L);
-int launch_transpose_kmajor(hipStream_t s, const float* src_kv, int64_t V, int k, float* dst_vk);
+int launch_transpose_kmajor(hipStream_t s, const float* src_kv, int64_t V, int k, void* dst_vk, int dt);
 
 }  // namespace rmx

@@ -17,8 +17,9 @@ struct rmx_table {
   rmx_ctx* ctx = nullptr;
   int64_t V = 0;
   int k = 0;
-  float* w = nullptr;    // [V]     first-order weights (Angel "weights" row 0)
-  float* emb = nullptr;  // [V][k]  embeddings, row-major (Angel "embedding" rows 0..k-1, transposed)
+  int dtype = 0;          // RMX_DTYPE_F32 / RMX_DTYPE_BF16 (elements of w and emb)
+  void* w = nullptr;      // [V]     first-order weights (Angel "weights" row 0)
+  void* emb = nullptr;    // [V][k]  embeddings, row-major (Angel "embedding" rows 0..k-1, transposed)
 };
 
 namespace rmx {
@@ -27,8 +28,9 @@ namespace rmx {
 struct FwdInputs {
   int B = 0;
   const int32_t* ids = nullptr;    // [B][F] or nullptr: implicit id = b*F + f (L-A path)
-  const float* table = nullptr;    // [rows][k]
-  const float* wtab = nullptr;     // [rows]
+  const void* table = nullptr;     // [rows][k]  (elements of dtype)
+  const void* wtab = nullptr;      // [rows]
+  int dtype = 0;                   // kF32 / kBF16
   const float* y1 = nullptr;       // precomputed first order (L-A irregular index) or nullptr
   float beta = 0.f;
   float* out = nullptr;            // [B]
@@ -69,6 +71,7 @@ struct rmx_model {
   float* cross_b = nullptr;                 // [L]
   float* wo_x = nullptr;                    // [D] slice of W_out for x_L
   int32_t* pairs = nullptr;                 // PNN (row, col) pairs [P][2]
+  int precision = 0;                        // kF32 / kBF16 (rmx_model_set_precision)
   bool params_ready = false;
   float beta = 0.f;
   bool beta_set = false;
@@ -88,6 +91,9 @@ struct rmx_model {
   float* la_w = nullptr;
   int64_t* la_rowptr = nullptr;
   float* la_out = nullptr;
+  rmx::bf16_t* la_E16 = nullptr;                 // bf16 models: the rounded L-A arrays
+  rmx::bf16_t* la_w16 = nullptr;
+  int64_t la16_cap = 0;
   std::vector<int64_t> h_rowptr;
   std::vector<float> h_wperm;
 
@@ -106,6 +112,7 @@ int model_build(rmx_model& m);
 void model_init_mats(const rmx_model& m, uint64_t seed, float* mats);
 void model_release(rmx_model& m);
 int model_load_mats(rmx_model& m, const float* host_mats, bool sync);
+int model_set_precision(rmx_model& m, int dtype);
 int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in);
 int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
                        float bias, const float* weights, const float* embedding, const float* mats,
@@ -129,12 +136,12 @@ int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L);
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
                      const int32_t* ids, const float* table, const float* u_prev, float* u_out,
                      float* rowdot);
-int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const float* table,
+int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const void* table, int dt,
                  const float* cross_w, const float* cross_b, const float* wo_x, float* pre2);
-int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table,
-                   const int32_t* pairs, int P, float* xbuf, int ldx);
-int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const float* table, float* xbuf,
-                    int ldx);
+int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt,
+                   const int32_t* pairs, int P, void* xbuf, int xdt, int ldx);
+int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt, void* xbuf,
+                    int xdt, int ldx);
 int tower_npad_for(int N);
 int cin_npad_for(int H);
 }  // namespace rmx

@@ -434,6 +434,10 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
     set_error("rmx_forward_ids_sharded: call rmx_model_set_bias first");
     return RMX_E_INVALID;
   }
+  if (m->precision != RMX_DTYPE_F32) {
+    set_error("rmx_forward_ids_sharded: sharded tables are fp32 (model precision must be RMX_DTYPE_F32)");
+    return RMX_E_INVALID;
+  }
   if (m->type != RMX_MODEL_LR && sh->k != m->k) {
     set_error("rmx_forward_ids_sharded: table embedding_dim differs from the model's");
     return RMX_E_SHAPE;
@@ -452,6 +456,7 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
   in.ids = sh->perm;
   in.table = sh->recv_emb;
   in.wtab = sh->recv_w;
+  in.dtype = kF32;
   in.beta = m->beta;
   in.out = d_out;
   st = model_forward(*m, s, in);

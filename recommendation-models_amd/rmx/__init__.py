@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT_K_MAJOR,  # noqa: F401
-                   LAYOUT_ROW_MAJOR, check, ptr)
+                   LAYOUT_ROW_MAJOR, DTYPE_F32, DTYPE_BF16, check, ptr)
 
 import ctypes
 
@@ -175,13 +175,16 @@ class EmbeddingTable:
     "weights" and "embedding" (ParRecModel.scala:74-105) and their pull + make* gather
     (ParRecModel.scala:165-199, 279-306)."""
 
-    def __init__(self, ctx, num_rows, embedding_dim):
+    def __init__(self, ctx, num_rows, embedding_dim, dtype=DTYPE_F32):
+        """dtype DTYPE_BF16: bf16 storage (fp32 uploads / the synthetic fill are rounded to nearest even)."""
         h = ctypes.c_void_p()
-        check(_lib.lib.rmx_table_create(ctx.handle, int(num_rows), int(embedding_dim), ctypes.byref(h)))
+        check(_lib.lib.rmx_table_create_ex(ctx.handle, int(num_rows), int(embedding_dim), int(dtype),
+                                           ctypes.byref(h)))
         self.handle = h
         self.ctx = ctx
         self.rows = int(num_rows)
         self.k = int(embedding_dim)
+        self.dtype = int(dtype)
 
     def upload(self, weights=None, embedding=None, layout=LAYOUT_ROW_MAJOR):
         """layout LAYOUT_K_MAJOR: embedding is the reference PS layout, k x V."""
@@ -373,6 +376,10 @@ class RecModel:
     def setMats(self, mats):
         mats = np.ascontiguousarray(mats, np.float32)
         check(_lib.lib.rmx_model_set_mats(self._device(), ptr(mats, ctypes.c_float), len(mats)))
+
+    def setPrecision(self, dtype):
+        """DTYPE_BF16: bf16 weights / activations on bf16 MFMA with fp32 accumulation (before setMats)."""
+        check(_lib.lib.rmx_model_set_precision(self._device(), int(dtype)))
 
     def setBias(self, bias):
         check(_lib.lib.rmx_model_set_bias(self._device(), float(np.asarray(bias).reshape(-1)[0])))

@@ -20,6 +20,8 @@ RMX_E_MATS = -7
 RMX_E_COMM = -8
 UNIQUE_ID_BYTES = 128
 
+DTYPE_F32 = 0
+DTYPE_BF16 = 1
 LAYOUT_K_MAJOR = 0
 LAYOUT_ROW_MAJOR = 1
 
@@ -66,6 +68,9 @@ SIGNATURES = [
     ("rmx_model_set_mats", c_int, [c_vp, P(c_f32), c_i64]),
     ("rmx_model_set_bias", c_int, [c_vp, c_f32]),
     ("rmx_table_create", c_int, [c_vp, c_i64, c_int, P(c_vp)]),
+    ("rmx_table_create_ex", c_int, [c_vp, c_i64, c_int, c_int, P(c_vp)]),
+    ("rmx_table_dtype", c_int, [c_vp]),
+    ("rmx_model_set_precision", c_int, [c_vp, c_int]),
     ("rmx_table_destroy", c_int, [c_vp]),
     ("rmx_table_upload", c_int, [c_vp, P(c_f32), P(c_f32), c_int]),
     ("rmx_table_fill_synthetic", c_int, [c_vp, c_u64]),

@@ -79,6 +79,7 @@ def lib():
     L.orc_first_order.restype = ctypes.c_int32
     L.orc_fm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, f32p, f32p]
     L.orc_fm.restype = ctypes.c_int32
+    L.orc_round_bf16.argtypes = [ctypes.c_int64, f32p, f32p]
     _lib = L
     return L
 
@@ -173,3 +174,11 @@ def fm(B, F, k, embedding):
     y2 = np.zeros(B, np.float32)
     lib().orc_fm(B, F, k, _p(e, ctypes.c_float), _p(y2, ctypes.c_float))
     return y2
+
+
+def round_bf16(x):
+    """bf16 round-to-nearest-even of an fp32 array (values stay fp32)."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty_like(x)
+    lib().orc_round_bf16(x.size, _p(x, ctypes.c_float), _p(y, ctypes.c_float))
+    return y

@@ -32,6 +32,8 @@ for s in $STEPS; do
     bench) run bench 400 python bench.py ;;
     benchx) run bench_xdeepfm 400 python bench.py --workload xdeepfm --no-cpu-baseline ;;
     benchs) run bench_sharded 400 python bench.py --workload deepfm_sharded --no-cpu-baseline ;;
+    benchb) run bench_dcn_bf16 400 python bench.py --workload dcn_bf16 --no-cpu-baseline &&
+            run bench_pnn_bf16 400 python bench.py --workload pnn_bf16 --no-cpu-baseline ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o deepfm -- \
             python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     profx) run profx 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx" -o xdeepfm -- \
