@@ -292,9 +292,20 @@ int launch_convert_bf16(hipStream_t s, const float* src, int64_t n, bf16_t* dst)
 
 // W (out x in row-major at mats + w_off) -> [Kpad/16][Npad][16]; bias -> [Npad].
 // (PNN: columns >= K1 come from a second matrix at w_off2; bias_mode 2 broadcasts one scalar.)
-__global__ void pack_linear_kernel(const float* __restrict__ mats, int64_t w_off, int64_t w_off2, int K1,
-                                   int64_t b_off, int bias_mode, int K, int N, int Kpad, int Npad,
-                                   float* __restrict__ Wp, float* __restrict__ bp) {
+// value of W[n][kx] of a packed layer (PNN: two matrices side by side; DCN: extra cross rows)
+__device__ __forceinline__ float layer_w(const float* __restrict__ mats, const DenseLayer& L, int n, int kx) {
+  if (n >= L.N || kx >= L.K) return 0.f;
+  if (L.N1 >= 0 && n >= L.N1) {
+    const int e = n - L.N1;
+    return e < L.nx ? mats[L.w_off_x + (int64_t)e * L.K + kx] : mats[L.w_off_o + kx];
+  }
+  if (L.K1 < 0) return mats[L.w_off + (int64_t)n * L.K + kx];
+  if (kx < L.K1) return mats[L.w_off + (int64_t)n * L.K1 + kx];
+  return mats[L.w_off2 + (int64_t)n * (L.K - L.K1) + (kx - L.K1)];
+}
+
+__global__ void pack_linear_kernel(const float* __restrict__ mats, DenseLayer L, int64_t b_off, int bias_mode,
+                                   int K, int N, int Kpad, int Npad, float* __restrict__ Wp, float* __restrict__ bp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot = (int64_t)Kpad * Npad;
   if (i < tot) {
@@ -303,25 +314,20 @@ __global__ void pack_linear_kernel(const float* __restrict__ mats, int64_t w_off
     const int n = (int)(rest % Npad);
     const int c = (int)(rest / Npad);
     const int kx = c * 16 + kk;
-    float v = 0.f;
-    if (n < N && kx < K) {
-      if (K1 < 0) v = mats[w_off + (int64_t)n * K + kx];
-      else if (kx < K1) v = mats[w_off + (int64_t)n * K1 + kx];
-      else v = mats[w_off2 + (int64_t)n * (K - K1) + (kx - K1)];
-    }
-    Wp[i] = v;
+    Wp[i] = layer_w(mats, L, n, kx);
   }
   if (i < Npad) {
+    const int nb = L.N1 >= 0 ? L.N1 : N;  // extra DCN rows have no bias
     float v = 0.f;
-    if (i < N && bias_mode == 1) v = mats[b_off + i];
-    if (i < N && bias_mode == 2) v = mats[b_off];
+    if (i < nb && bias_mode == 1) v = mats[b_off + i];
+    if (i < nb && bias_mode == 2) v = mats[b_off];
     bp[i] = v;
   }
 }
 
 // bf16 packing: [Kpad/32][Npad][32] (one 64-B row = 32 bf16 of one output column), RNE rounding
-__global__ void pack_linear_bf16_kernel(const float* __restrict__ mats, int64_t w_off, int64_t w_off2, int K1, int K,
-                                        int N, int Kpad, int Npad, bf16_t* __restrict__ Wp) {
+__global__ void pack_linear_bf16_kernel(const float* __restrict__ mats, DenseLayer L, int Kpad, int Npad,
+                                        bf16_t* __restrict__ Wp) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot = (int64_t)Kpad * Npad;
   if (i >= tot) return;
@@ -330,12 +336,7 @@ __global__ void pack_linear_bf16_kernel(const float* __restrict__ mats, int64_t 
   const int n = (int)(rest % Npad);
   const int c = (int)(rest / Npad);
   const int kx = c * 32 + kk;
-  float v = 0.f;
-  if (n < N && kx < K) {
-    if (K1 < 0) v = mats[w_off + (int64_t)n * K + kx];
-    else if (kx < K1) v = mats[w_off + (int64_t)n * K1 + kx];
-    else v = mats[w_off2 + (int64_t)n * (K - K1) + (kx - K1)];
-  }
+  const float v = layer_w(mats, L, n, kx);
   Wp[i] = (bf16_t)v;
 }
 
@@ -343,13 +344,12 @@ int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L) {
   const int64_t tot = (int64_t)L.Kpad * L.Npad;
   const int64_t n = tot > L.Npad ? tot : L.Npad;
   // bias (and, for fp32 layers, W)
-  hipLaunchKernelGGL(pack_linear_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mats_dev,
-                     L.w_off, L.w_off2, L.K1, L.b_off, L.b_off >= 0 ? L.bias_mode : 0, L.K, L.N, L.W16 ? 0 : L.Kpad,
-                     L.Npad, L.W, L.b);
+  hipLaunchKernelGGL(pack_linear_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mats_dev, L,
+                     L.b_off, L.b_off >= 0 ? L.bias_mode : 0, L.K, L.N, L.W16 ? 0 : L.Kpad, L.Npad, L.W, L.b);
   RMX_HIP(hipGetLastError());
   if (L.W16) {
-    hipLaunchKernelGGL(pack_linear_bf16_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats_dev,
-                       L.w_off, L.w_off2, L.K1, L.K, L.N, L.Kpad, L.Npad, L.W16);
+    hipLaunchKernelGGL(pack_linear_bf16_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats_dev, L,
+                       L.Kpad, L.Npad, L.W16);
     RMX_HIP(hipGetLastError());
   }
   return RMX_OK;

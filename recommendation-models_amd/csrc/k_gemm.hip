@@ -114,7 +114,7 @@ static int tower_nt_for(int Npad) {
 }
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
-                       const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa) {
+                       const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa, const XColArgs* xc) {
   if (M <= 0) return RMX_OK;
   const int nt = tower_nt_for(L.Npad);
   if (epi == Epi::kOutput && nt * 16 != L.Npad) {
@@ -123,7 +123,7 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
       set_error("bf16 tower: the last hidden layer must fit one block (N <= 416)");
       return RMX_E_INVALID;
     }
-    int st = launch_tower_layer(s, L, M, A, lda, ga, C, ldc, Epi::kReluStore, nullptr);
+    int st = launch_tower_layer(s, L, M, A, lda, ga, C, ldc, Epi::kReluStore, nullptr, nullptr);
     if (st != RMX_OK) return st;
     hipLaunchKernelGGL(tower_head_kernel, dim3((M + 3) / 4), dim3(256), 0, s, M, L.N, C, ldc, *oa);
     RMX_HIP(hipGetLastError());
@@ -142,6 +142,15 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
   p.C = C;
   p.ldc = ldc;
   if (oa) p.oa = *oa;
+  if (xc) {
+    if (epi != Epi::kReluStore) {
+      set_error("gemm: raw extra columns need the ReLU-store epilogue");
+      return RMX_E_INVALID;
+    }
+    p.xcol = xc->ptr;
+    p.xn_main = xc->n_main;
+    p.xld = xc->ld;
+  }
   const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
   if (L.W16) return launch_tower_bf16(s, p, nt, amode, epi);
   switch (nt) {

@@ -59,6 +59,8 @@ struct GemmArgs {
   OutArgs oa;          // kEpiOutput
   const float* wo;     // kEpiCin: [Npad] slice of the output Linear
   float* rowdot;       // kEpiCin: [M]
+  float* xcol;         // kEpiRelu: raw extra columns n >= xn_main -> xcol[m * xld + n - xn_main] (DCN cross)
+  int xn_main, xld;
 };
 
 // Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
@@ -341,6 +343,20 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     }
   };
   if constexpr (EPI == kEpiRelu) {
+    if (p.xcol) {  // DCN: the cross dot products ride along as extra raw columns
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int e = n0 + (bt0 + j) * 16 + r16 - p.xn_main;
+          if (e >= 0 && e < p.xld)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = m0 + wm * MT * 16 + i * 16 + g * 4 + r;
+              if (m < M) p.xcol[(int64_t)m * p.xld + e] = acc[i][j][r];
+            }
+        }
+    }
     store_rows(p.C, p.ldc);
   } else {
     // row reduction sum_n ReLU(acc + b)[n] * w[n] over the block's (= the layer's) columns;

@@ -90,6 +90,15 @@ std::vector<int32_t> mats_sizes(const rmx_model& m) {
   return s;
 }
 
+float bf16_round_host(float f) {  // round to nearest even, finite values
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  u &= 0xFFFF0000u;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
 uint64_t splitmix64_h(uint64_t x) {
   x += 0x9E3779B97F4A7C15ULL;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -237,14 +246,26 @@ int model_build(rmx_model& m) {
       m.cross_w_off = 0;
       m.cross_b_off = (int64_t)m.cross_depth * D;
       off = m.cross_b_off + m.cross_depth;
+      // fcDims >= 2: the cross dots x0.w_l and x0.W_out[0:D] ride along tower layer 1 (same A = x0)
+      // as L + 1 raw extra columns, and the cross stack collapses to a per-row closed form
+      m.dcn_fused = m.fc.size() >= 2 && m.cross_depth <= kMaxFusedCross;
       int prev = D;
       for (int d : m.fc) {
-        m.layers.push_back(make_layer(prev, d, off, off + (int64_t)prev * d));
+        const bool first = m.layers.empty();
+        DenseLayer L = make_layer(prev, first && m.dcn_fused ? d + m.cross_depth + 1 : d, off,
+                                  off + (int64_t)prev * d);
+        if (first && m.dcn_fused) {
+          L.N1 = d;
+          L.nx = m.cross_depth;
+          L.w_off_x = m.cross_w_off;
+        }
+        m.layers.push_back(L);
         off += (int64_t)prev * d + d;
         prev = d;
       }
       m.wo_x_off = off;
       m.wo_off = off + D;
+      if (m.dcn_fused) m.layers[0].w_off_o = m.wo_x_off;
       m.has_bo = false;
       break;
     }
@@ -377,6 +398,7 @@ void model_release(rmx_model& m) {
   dev_free(m.h[1]);
   dev_free(m.y12);
   dev_free(m.pre2);
+  dev_free(m.xcol);
   dev_free(m.xbuf);
   dev_free(m.ubuf[0]);
   dev_free(m.ubuf[1]);
@@ -455,6 +477,20 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   }
   if (m.type == RMX_MODEL_DCN) {
     const int D = m.F * m.k;
+    if (m.dcn_fused) {
+      // closed-form scalars; the extra GEMM columns use the packed (bf16-rounded for bf16 models)
+      // vectors, so the sums are taken over the same values
+      auto rv = [&](float v) { return m.precision == kBF16 ? bf16_round_host(v) : v; };
+      for (int l = 0; l < m.cross_depth; ++l) {
+        double ws = 0.0;
+        for (int d = 0; d < D; ++d) ws += rv(host_mats[m.cross_w_off + (int64_t)l * D + d]);
+        m.cross_scalars.wsum[l] = (float)ws;
+        m.cross_scalars.beta[l] = host_mats[m.cross_b_off + l];
+      }
+      double wo = 0.0;
+      for (int d = 0; d < D; ++d) wo += rv(host_mats[m.wo_x_off + d]);
+      m.cross_scalars.wo_sum = (float)wo;
+    }
     RMX_HIP(hipMemcpyAsync(m.cross_w, m.mats_dev + m.cross_w_off, sizeof(float) * m.cross_depth * D,
                            hipMemcpyDeviceToDevice, s));
     RMX_HIP(hipMemcpyAsync(m.cross_b, m.mats_dev + m.cross_b_off, sizeof(float) * m.cross_depth,
@@ -475,6 +511,7 @@ int ensure_ws(rmx_model& m, int B) {
   dev_free(m.h[1]);
   dev_free(m.y12);
   dev_free(m.pre2);
+  dev_free(m.xcol);
   dev_free(m.xbuf);
   dev_free(m.ubuf[0]);
   dev_free(m.ubuf[1]);
@@ -488,6 +525,7 @@ int ensure_ws(rmx_model& m, int B) {
   }
   if ((st = dev_alloc(&m.y12, B))) return st;
   if ((st = dev_alloc(&m.pre2, B))) return st;
+  if (m.dcn_fused && (st = dev_alloc(&m.xcol, (size_t)B * (m.cross_depth + 1)))) return st;
   if (m.type == RMX_MODEL_PNN || (m.type != RMX_MODEL_LR && needs_gather_x(m))) {
     if ((st = dev_alloc(&m.xbuf, (size_t)B * m.layers[0].Kpad))) return st;
   }
@@ -608,10 +646,12 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     oa.rowsum = m.rowdot;
     oa.rowsum_k = k;
   } else if (m.type == RMX_MODEL_DCN) {
-    StageTimer t(m, s, "cross");
-    if ((st = launch_cross(s, B, F, k, m.cross_depth, in.ids, in.table, in.dtype, m.cross_w, m.cross_b, m.wo_x,
-                           m.pre2)))
-      return st;
+    if (!m.dcn_fused) {
+      StageTimer t(m, s, "cross");
+      if ((st = launch_cross(s, B, F, k, m.cross_depth, in.ids, in.table, in.dtype, m.cross_w, m.cross_b, m.wo_x,
+                             m.pre2)))
+        return st;
+    }
     oa.pre2 = m.pre2;
   } else if (m.type == RMX_MODEL_PNN) {
     StageTimer t(m, s, "product");
@@ -637,9 +677,13 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     const DenseLayer& L = m.layers[i];
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
+    XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
     st = launch_tower_layer(s, L, B, A, lda, (i == 0 && gather_first) ? &ga : nullptr, C, L.Npad,
-                            last ? Epi::kOutput : Epi::kReluStore, last ? &oa : nullptr);
+                            last ? Epi::kOutput : Epi::kReluStore, last ? &oa : nullptr,
+                            (i == 0 && m.dcn_fused) ? &xc : nullptr);
     if (st) return st;
+    if (i == 0 && m.dcn_fused && (st = launch_cross_finish(s, B, m.cross_depth, m.xcol, m.cross_scalars, m.pre2)))
+      return st;
     A = C;
     lda = L.Npad;
   }

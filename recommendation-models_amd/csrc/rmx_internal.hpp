@@ -52,6 +52,11 @@ struct DenseLayer {
   int K1 = -1;          // PNN: columns [0, K1) come from W at w_off (N x K1), [K1, K) from
   int64_t w_off2 = -1;  //      W2 at w_off2 (N x (K - K1)): Linear(x) + Linear(ip) as one GEMM
   int bias_mode = 1;    // 0 none, 1 per-output bias[N], 2 one scalar broadcast (CAdd(1))
+  // DCN: extra output rows appended after the N1 layer rows, read raw (no bias / ReLU) by the
+  // epilogue: rows [N1, N1 + nx) = the cross vectors w_l at w_off_x (nx x K), row N1 + nx = W_out[0:D]
+  // at w_off_o.  N = N1 + nx + 1 then.  -1: none.
+  int N1 = -1, nx = 0;
+  int64_t w_off_x = -1, w_off_o = -1;
   float* W = nullptr;   // device, packed fp32 [Kpad/16][Npad][16]
   bf16_t* W16 = nullptr;  // device, packed bf16 [Kpad/32][Npad][32] (bf16 models; W unused then)
   float* b = nullptr;   // device [Npad]
@@ -86,8 +91,15 @@ struct OutArgs {
   float* out;            // [M] probabilities
 };
 
+// Raw extra columns of a layer (DenseLayer::N1): written unrounded in fp32 to ptr[m * ld + (n - n_main)].
+struct XColArgs {
+  float* ptr;
+  int n_main, ld;
+};
+
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
-                       const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa);
+                       const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa,
+                       const XColArgs* xc = nullptr);
 
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table,
                    const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob);

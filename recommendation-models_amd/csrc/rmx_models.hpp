@@ -36,6 +36,14 @@ struct FwdInputs {
   float* out = nullptr;            // [B]
 };
 
+// DCN cross stack scalars for the fused closed form (k_interact.hip cross_finish_kernel)
+constexpr int kMaxFusedCross = 8;
+struct CrossScalars {
+  float wsum[kMaxFusedCross];  // sum_d w_l[d]
+  float beta[kMaxFusedCross];  // beta_l
+  float wo_sum;                // sum_d W_out[d], d < D
+};
+
 // CIN layer (xDeepFM): C_l (H x F*Hp) packed [Hp_pad/16][F][Npad][16], bias, output slice.
 struct CinLayer {
   int Hp = 0, Hp_pad = 0, H = 0, Npad = 0;
@@ -70,6 +78,9 @@ struct rmx_model {
   float* cross_w = nullptr;                 // [L][D]
   float* cross_b = nullptr;                 // [L]
   float* wo_x = nullptr;                    // [D] slice of W_out for x_L
+  bool dcn_fused = false;                   // cross dots fused into tower layer 1 (fcDims >= 2)
+  rmx::CrossScalars cross_scalars{};
+  float* xcol = nullptr;                    // [B][L + 1] raw fused cross dots
   int32_t* pairs = nullptr;                 // PNN (row, col) pairs [P][2]
   int precision = 0;                        // kF32 / kBF16 (rmx_model_set_precision)
   bool params_ready = false;
@@ -136,6 +147,7 @@ int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L);
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
                      const int32_t* ids, const float* table, const float* u_prev, float* u_out,
                      float* rowdot);
+int launch_cross_finish(hipStream_t s, int B, int L, const float* xcol, const CrossScalars& cs, float* pre2);
 int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const void* table, int dt,
                  const float* cross_w, const float* cross_b, const float* wo_x, float* pre2);
 int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt,
