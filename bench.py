@@ -231,7 +231,15 @@ def main():
         roof = {"bound": "mfma", "achieved": round(work / avg_s / 1e12, 2), "peak": peak_tf,
                 "unit": "TFLOP/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
+    # (FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_summary.py --stages); null when not profiled
     roof["traffic"] = None
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        ent = json.load(open(tpath)).get(args.workload, {}).get(dom if not dom.startswith("cin") else "cin_layer")
+        if ent and ent.get("batch") == B:
+            roof["traffic"] = ent["hbm_bytes"]
+            roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
     roof["kernel"] = dom
     roof["algorithmic_per_launch"] = work
 

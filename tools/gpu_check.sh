@@ -46,6 +46,16 @@ for s in $STEPS; do
             python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
          run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
             python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc:*) wl=${s#pmc:}
+         run pmc_${wl}_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$wl/fetch" -o fetch -- \
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline &&
+         run pmc_${wl}_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_$wl/write" -o write -- \
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline ;;
+    prof:*) wl=${s#prof:}
+         run prof_$wl 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o $wl -- \
+            python3 bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline ;;
+    bench:*) wl=${s#bench:}
+         run bench_$wl 400 python bench.py --workload $wl ;;
   esac
 done
 echo "== all done"

@@ -21,8 +21,18 @@ import re
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name)
-    return name.replace("void ", "").replace("rmx::", "")
+    if name.startswith("_ZN3rmx"):
+        # c++filt here does not know the bf16 mangling (DF16b): keep the identifier and the first
+        # integer template argument, e.g. _ZN3rmx18encoder_k16_kernelILi0EDF16b... -> encoder_k16_kernel<0, bf16>
+        m = re.match(r"_ZN3rmx(\d+)", name)
+        n = int(m.group(1))
+        ident = name[m.end():m.end() + n]
+        rest = name[m.end() + n:]
+        t = re.match(r"ILi(\d+)E", rest)
+        bf = "bf16" if "DF16b" in rest else "float"
+        return "%s<%s%s>" % (ident, (t.group(1) + ", ") if t else "", bf)
+    name = re.sub(r"\((int|long|unsigned|float|rmx::|void)[^()]*\)$", "", name)
+    return name.replace("void ", "").replace("rmx::", "").replace("__bf16", "bf16")
 
 
 def load(d):
@@ -41,10 +51,32 @@ def load(d):
     return vals, dur, stats
 
 
+def stage_of(kernel):
+    """bench.py stage name of a kernel (template signature -> stage)."""
+    m = re.search(r"gemm_kernel<Tile<[^>]*>, (\d+), (\d+), (true|false)>", kernel)
+    if m:
+        amode, epi = int(m.group(1)), int(m.group(2))
+        if amode == 3:
+            return "cin_layer"
+        if amode in (1, 2):
+            return "tower_layer1"
+        return "tower_layer3" if epi == 1 else "tower_layer2"
+    for pat, st in (("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
+                    ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
+                    ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
+                    ("route_", "shard_exchange"), ("owner_gather", "shard_exchange")):
+        if kernel.startswith(pat):
+            return st
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--json")
+    ap.add_argument("--stages", nargs=2, metavar=("TRAFFIC_JSON", "WORKLOAD"),
+                    help="merge per-stage HBM bytes per launch into TRAFFIC_JSON under WORKLOAD")
+    ap.add_argument("--batch", type=int, default=0, help="rows per launch of the profiled run")
     a = ap.parse_args()
     vals, dur, stats = load(a.dir)
     out = {}
@@ -86,6 +118,18 @@ def main():
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
         json.dump(out, open(a.json, "w"), indent=1, sort_keys=True)
+    if a.stages:
+        path, wl = a.stages
+        db = json.load(open(path)) if os.path.exists(path) else {}
+        st = {}
+        for k, e in out.items():
+            name = stage_of(k)
+            if name and "hbm_bytes" in e:
+                st[name] = {"hbm_bytes": round(e["hbm_bytes"]), "fetch_bytes_x2": round(e["fetch_bytes_x2"]),
+                            "write_bytes": round(e["write_bytes"]), "kernel": k, "batch": a.batch}
+        db[wl] = st
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        json.dump(db, open(path, "w"), indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
