@@ -478,7 +478,8 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // Small batches: 4-wave blocks.
   const int var = NT % 2 == 0 ? tuning_get("tower_variant", 0) : 0;
   const bool dense = amode == kDenseA;
-  if (p.M >= 8192) {
+  // 8-wave blocks (BM 128) only when they still give >= 2 blocks per CU; else 4-wave blocks
+  if (p.M >= 65536) {
     if (var == 1) return launch_epi<Tile<1, (NT + 1) / 2, 4, 2, 1, 4>, BF>(s, p, amode, epi);
     if (var == 2) {
       if (dense) return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 2, 4>, BF>(s, p, amode, epi);
