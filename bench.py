@@ -38,8 +38,8 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded", "dcn_bf16", "pnn_bf16"],
                     default="deepfm")
     ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")

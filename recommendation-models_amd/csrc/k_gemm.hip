@@ -83,7 +83,7 @@ int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L) {
 // to minimise padding (ties: the wider block).
 int tower_npad_for(int N) {
   const int nt = (N + 15) / 16;
-  const bool even = tuning_get("tower_split", 0) != 0 && nt >= 8;  // variants 1/2 split NT in halves
+  const bool even = tuning_get("tower_split", 1) != 0 && nt >= 8;  // tower variants 2/3 split NT in halves
   int best = -1, best_pad = 1 << 30;
   for (int c : kNTs) {
     if (even && c % 2) continue;

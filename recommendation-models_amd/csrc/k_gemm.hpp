@@ -41,6 +41,21 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // physical 16-B slot of logical slot g in row `row` of a [rows][16] fp32 LDS tile
 __device__ __forceinline__ int swz_slot(int row, int g) { return g ^ ((4 - ((row >> 2) & 3)) & 3); }
 
+// 16 zero bytes: the LDS-DMA source of out-of-range rows / K padding (a DMA always writes its slot)
+static __device__ __attribute__((aligned(16))) float g_rmx_zero16[4];
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+#define RMX_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    RMX_VMW(0) RMX_VMW(1) RMX_VMW(2) RMX_VMW(3) RMX_VMW(4) RMX_VMW(5) RMX_VMW(6) RMX_VMW(7)
+    RMX_VMW(8) RMX_VMW(9) RMX_VMW(10) RMX_VMW(11) RMX_VMW(12) RMX_VMW(13) RMX_VMW(14) RMX_VMW(15)
+#undef RMX_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
 enum EpiMode : int { kEpiRelu = 0, kEpiOutput = 1, kEpiCin = 2 };
 
@@ -66,9 +81,12 @@ struct GemmArgs {
 // Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
 // tiles); the block spans BM = WM*MT*16 rows and BN = WN*NTW*16 columns.  BKC 16-wide K chunks per
 // LDS stage.  OCC = minimum waves per SIMD the register allocation must allow (launch bounds).
-template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_>
+template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_, int RING_ = 0>
 struct Tile {
-  static constexpr int MT = MT_, NTW = NTW_, WM = WM_, WN = WN_, BKC = BKC_, OCC = OCC_;
+  // RING > 0: LDS-DMA (global_load_lds_dwordx4) ring of RING one-chunk stages, RING - 1 chunks in
+  // flight, counted vmcnt + one raw barrier per chunk (needs BKC == 1); 0: register-staged double buffer
+  static constexpr int MT = MT_, NTW = NTW_, WM = WM_, WN = WN_, BKC = BKC_, OCC = OCC_, RING = RING_;
+  static constexpr int NBUF = RING > 0 ? RING : 2;  // stage buffers in LDS
   static constexpr int NW = WM * WN, NTHR = NW * 64, NT = NTW * WN;
   static constexpr int BM = WM * MT * 16, BN = NT * 16;
 };
@@ -85,7 +103,7 @@ struct StageGeom {
 template <class T, int STAGE_FLOATS>
 struct EpiGeom {
   static constexpr int RW = T::MT * 16;
-  static constexpr int WF = (2 * STAGE_FLOATS) / T::NW;
+  static constexpr int WF = (T::NBUF * STAGE_FLOATS) / T::NW;
   static constexpr int NTH0 = (WF / RW - 4) / 16;
   static constexpr int NTH = NTH0 < T::NTW ? (NTH0 < 1 ? 1 : NTH0) : T::NTW;
   static constexpr int LD = NTH * 16 + 4;  // == 4 mod 8: the two 16-lane halves of a write hit disjoint banks
@@ -106,10 +124,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   constexpr int ITEMS = ROWS * 4;  // float4 items per stage
   constexpr int PER = (ITEMS + NTHR - 1) / NTHR;
 
+  constexpr int RING = T::RING;
+  static_assert(RING == 0 || BKC == 1, "the LDS-DMA ring stages one K chunk at a time");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* lds0 = smem;
   float* lds1 = smem + STAGE;
-  float* extra = smem + 2 * STAGE;  // gather: int ids [BM][F]; CIN: x0 [BM][XS]
+  float* extra = smem + T::NBUF * STAGE;  // gather: int ids [BM][F]; CIN: x0 [BM][XS]
   int* sids = reinterpret_cast<int*>(extra);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -215,10 +235,6 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     }
   };
 
-  gload(0);
-  sstore(lds0);
-  __syncthreads();
-
   const int g = lane >> 4, r16 = lane & 15;
   int arow[MT];
 #pragma unroll
@@ -242,15 +258,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     cur_hc = hc;
   };
 
-  for (int st = 0; st < nstages; ++st) {
-    const float* cur = (st & 1) ? lds1 : lds0;
-    float* nxt = (st & 1) ? lds0 : lds1;
-    const bool more = st + 1 < nstages;
-    if (more) gload(st + 1);
-#pragma unroll
-    for (int cc = 0; cc < BKC; ++cc) {
-      const int c = st * BKC + cc;
-      if (BKC > 1 && c >= nchunks) break;
+  // one K chunk c of the stage image at `cur` (chunk slot cc inside the stage)
+  auto compute_chunk = [&](const float* cur, int cc, int c) {
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
       f32x4 a[MT];
       if constexpr (A_LDS) {
@@ -299,8 +308,79 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                   acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s4], b[t][s4], acc[i][j0 + t], 0, 0, 0);
         }
       }
+  };
+
+  if constexpr (RING == 0) {
+    gload(0);
+    sstore(lds0);
+    __syncthreads();
+    for (int st = 0; st < nstages; ++st) {
+      const float* cur = (st & 1) ? lds1 : lds0;
+      float* nxt = (st & 1) ? lds0 : lds1;
+      const bool more = st + 1 < nstages;
+      if (more) gload(st + 1);
+#pragma unroll
+      for (int cc = 0; cc < BKC; ++cc) {
+        const int c = st * BKC + cc;
+        if (BKC > 1 && c >= nchunks) break;
+        compute_chunk(cur, cc, c);
+      }
+      if (more) sstore(nxt);
+      __syncthreads();
     }
-    if (more) sstore(nxt);
+  } else {
+    // LDS-DMA ring: wave-instruction ins of a chunk fills stage rows [16 ins, 16 ins + 16) (1 KiB);
+    // lane L writes physical slot L&3 of row L>>2, so it loads logical slot (L&3) ^ key(row): the
+    // swizzle goes on the source address, the LDS image stays lane-linear (guide rule 21).
+    constexpr int NW = T::NW;
+    constexpr int NINS = ROWS / 16;
+    constexpr int IPW = (NINS + NW - 1) / NW;
+    const int my_n = wid < NINS ? (NINS - 1 - wid) / NW + 1 : 0;  // DMAs this wave issues per chunk
+    auto issue = [&](int c) {
+      float* buf = smem + (c % RING) * STAGE;
+#pragma unroll
+      for (int q = 0; q < IPW; ++q) {
+        const int ins = wid + q * NW;
+        if (ins < NINS) {
+          const int row = ins * 16 + (lane >> 2), ps = lane & 3;
+          const void* src = g_rmx_zero16;
+          if (row < AROWS) {
+            const int r = row, g = swz_slot(r, ps), m = m0 + r, kk = c * KC + g * KS;
+            if (m < M && kk < p.K) {
+              if constexpr (AMODE == kGatherK16) {
+                const int f = BF ? 2 * c + (g >> 1) : c;
+                const int id = sids[r * F + f];
+                src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * 16 + (g & 1) * 8)
+                         : (const void*)(p.ga.table + (int64_t)id * 16 + g * 4);
+              } else if constexpr (AMODE == kGatherAny) {
+                const int f = kk / p.ga.k, j = kk - f * p.ga.k;
+                const int id = sids[r * F + f];
+                src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * p.ga.k + j)
+                         : (const void*)(p.ga.table + (int64_t)id * p.ga.k + j);
+              } else {
+                src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + (int64_t)m * p.lda + kk)
+                         : (const void*)(p.A + (int64_t)m * p.lda + kk);
+              }
+            }
+          } else {
+            const int n = row - AROWS, g = swz_slot(n, ps);
+            src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.Wp) + ((int64_t)c * p.Npad + n0 + n) * 32 + g * 8)
+                     : (const void*)(p.Wp + ((int64_t)c * p.Npad + n0 + n) * 16 + g * 4);
+          }
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
+        }
+      }
+    };
+    for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
+    for (int c = 0; c < nchunks; ++c) {
+      const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
+      vm_wait(younger * my_n);                             // this wave's DMAs of chunk c have landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // and its reads of chunk c - 1 are done
+      __builtin_amdgcn_s_barrier();                        // ... for every wave
+      if (c + RING - 1 < nchunks) issue(c + RING - 1);     // refills the buffer of chunk c - 1
+      compute_chunk(smem + (c % RING) * STAGE, 0, c);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
@@ -434,7 +514,7 @@ constexpr int kCinNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16};
 template <class T, int AMODE, int EPI, bool BF = false>
 int launch_cfg(hipStream_t s, GemmArgs& p) {
   using SG = StageGeom<T, AMODE>;
-  size_t lds = sizeof(float) * 2 * SG::FLOATS;
+  size_t lds = sizeof(float) * T::NBUF * SG::FLOATS;
   if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * T::BM * p.ga.F;
   if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
   if (EPI != kEpiOutput) lds = std::max(lds, sizeof(float) * EpiGeom<T, SG::FLOATS>::FLOATS);
@@ -469,23 +549,23 @@ int launch_epi(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 
 template <int NT, bool BF>
 int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
-  // Large batches: 8-wave blocks.  Knob "tower_variant":
-  //   0: 8 waves on M (BM 128) x all NT tiles per wave, 2 waves / SIMD (1 block per CU);
-  //   1: 4 x 2 waves (BM 64, NT/2 tiles per wave), one K chunk per stage, 4 waves / SIMD
-  //      (2 blocks per CU, their barriers interleave);
-  //   2: 8 x 2 waves (16 waves, BM 128), 4 waves / SIMD in one block.
-  // Variants 1 / 2 need an even NT (the model packs N = 400 as 26 tiles when tower_split = 1).
-  // Small batches: 4-wave blocks.
-  const int var = NT % 2 == 0 ? tuning_get("tower_variant", 0) : 0;
-  const bool dense = amode == kDenseA;
-  // 8-wave blocks (BM 128) only when they still give >= 2 blocks per CU; else 4-wave blocks
+  // Large batches (M >= 65536, >= 2 blocks of 128 rows per CU).  Knob "tower_variant":
+  //   0: register-staged double buffer, 8 waves on M x all NT tiles per wave (2 waves / SIMD);
+  //   1: LDS-DMA ring (4 chunks), same tiling;
+  //   2: LDS-DMA ring (3 chunks), 4 x 2 waves of 32 rows x NT/2 tiles;
+  //   3: LDS-DMA ring (3 chunks), 8 x 2 waves of 16 rows x NT/2 tiles, 4 waves / SIMD in one
+  //      16-wave block -- the default for even NT >= 8 (the model pads N = 400 to 26 tiles):
+  //      N = 400, M = 65536, fp32: 0.289 ms/layer vs 0.315 (variant 0); bf16 0.063 vs 0.092.
+  // Variants 2 / 3 need an even NT.  Small batches: 4-wave blocks, register-staged.
+  constexpr bool kEven = NT % 2 == 0 && NT >= 8;
+  int var = tuning_get("tower_variant", kEven ? 3 : 0);
   if (p.M >= 65536) {
-    if (var == 1) return launch_epi<Tile<1, (NT + 1) / 2, 4, 2, 1, 4>, BF>(s, p, amode, epi);
-    if (var == 2) {
-      if (dense) return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 2, 4>, BF>(s, p, amode, epi);
-      return launch_epi<Tile<1, (NT + 1) / 2, 8, 2, 1, 4>, BF>(s, p, amode, epi);
+    if constexpr (kEven) {
+      if (var == 2) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 1, 3>, BF>(s, p, amode, epi);
+      if (var == 3) return launch_epi<Tile<1, NT / 2, 8, 2, 1, 4, 3>, BF>(s, p, amode, epi);
     }
-    if (dense) return launch_epi<Tile<1, NT, 8, 1, 2, 1>, BF>(s, p, amode, epi);
+    if (var == 1) return launch_epi<Tile<1, NT, 8, 1, 1, 1, 4>, BF>(s, p, amode, epi);
+    if (amode == kDenseA) return launch_epi<Tile<1, NT, 8, 1, 2, 1>, BF>(s, p, amode, epi);
     return launch_epi<Tile<1, NT, 8, 1, 1, 1>, BF>(s, p, amode, epi);
   }
   return launch_epi<Tile<1, NT, 4, 1, 1, 1>, BF>(s, p, amode, epi);

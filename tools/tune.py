@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--bf16", action="store_true", help="bf16 tables and tower (not xdeepfm)")
     ap.add_argument("--set", default="", help="extra knobs applied before building the models, k=v,k=v")
     a = ap.parse_args()
     vals = [int(v) for v in a.values.split(",")]
@@ -50,10 +51,12 @@ def main():
     for v in vals:  # a model per variant: knobs read at model build (packing) apply too
         rmx.set_tuning(a.knob, v)
         m, B = build()
+        if a.bf16:
+            m.setPrecision(rmx.DTYPE_BF16)
         m.setMats(m.initMats(0x3A75))
         m.setBias(0.01)
         models[v] = m
-    t = rmx.EmbeddingTable(ctx, V, K)
+    t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16 if a.bf16 else rmx.DTYPE_F32)
     t.fill_synthetic(0x7AB1E)
     ids = rmx.DeviceArray(ctx, B * F, np.int32)
     rmx.gen_ids(ctx, 0x5EED2026, 0, B, F, V, ids)
