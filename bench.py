@@ -44,6 +44,9 @@ def parse():
                     default="deepfm")
     ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="Zipf exponent of the ids within a field (SURVEY.md §8d secondary; 0 = uniform)")
+    ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -114,6 +117,29 @@ def cpu_baseline(workload, budget_s, threads):
                       % (done, done // B, B, workload, t_tot)}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_sweep(workload, budget_s, threads):
+    """All-core baseline (the reported value) + 1 and 2 threads (Spark local[1] / local[2]
+    analogues) on shorter bounded samples."""
+    res = cpu_baseline(workload, budget_s, threads)
+    res["by_threads"] = {str(threads): round(res["value"], 1)}
+    for t in (1, 2):
+        if t < threads:
+            res["by_threads"][str(t)] = round(cpu_baseline(workload, max(2.0, budget_s * 0.3), t)["value"], 1)
+    res["cpu_model"] = cpu_model()
+    res["nproc"] = os.cpu_count()
+    return res
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -150,6 +176,7 @@ def main():
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
         table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
+        table.set_dedupe(not args.no_dedupe)
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
     table.fill_synthetic(SEED_TAB)
@@ -157,7 +184,7 @@ def main():
     model.setBias(0.01)
     nrows = max(ROWS, B)
     ids = rmx.DeviceArray(ctx, nrows * F, np.int32)
-    rmx.gen_ids(ctx, SEED_IDS, rank * nrows, nrows, F, Vw, ids)
+    rmx.gen_ids(ctx, SEED_IDS, rank * nrows, nrows, F, Vw, ids, zipf=args.zipf)
     out = rmx.DeviceArray(ctx, nrows, np.float32)
     ctx.sync()
     nb = nrows // B
@@ -246,7 +273,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(args.workload, args.cpu_seconds, threads)
+        cpu = cpu_baseline_sweep(args.workload, args.cpu_seconds, threads)
 
     if rank == 0:
         line = {
@@ -267,7 +294,10 @@ def main():
                 ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
                 {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(args.workload, ""), B),
                 "global_batch": world * B, "rows_per_gpu_set": nrows,
+                "ids": ("zipf%g" % args.zipf) if args.zipf else "uniform",
                 "parallelism": ("hashshard%d_rccl" % world) if sharded else "replicas%d" % world},
+            **({"exchange": {"dedupe": not args.no_dedupe, "ids_sent_last_step": table.last_sent(),
+                             "nnz_per_step": B * F}} if sharded else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages": per_stage,

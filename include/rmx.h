@@ -163,6 +163,10 @@ int rmx_table_device_ptrs(const rmx_table* t, void** d_weights, void** d_embeddi
 /* Synthetic field-partitioned ids into device memory, bit-identical to orc_gen_ids. */
 int rmx_gen_ids(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,
                 int64_t num_rows, int32_t* d_ids, void* stream);
+/* Zipf-like ids (SURVEY.md §8d secondary): rank r of field f drawn with P(r) ~ (r+1)^-exponent
+ * (continuous power-law inversion, double precision), id = f * (num_rows / n_fields) + r. */
+int rmx_gen_ids_zipf(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,
+                     int64_t num_rows, double exponent, int32_t* d_ids, void* stream);
 
 /* Debug gather: d_w[n] = weights[ids[n]], d_emb[n*k+j] = emb[ids[n]][j] (makeWeights /
  * makeEmbeddings, ParRecModel.scala:279-306).  Bit-exact copies (as fp32 for a bf16 table). */
@@ -202,6 +206,11 @@ int rmx_shard_destroy(rmx_shard* sh);
 /* Owned rows from the same generator as rmx_table_fill_synthetic (bit-identical rows). */
 int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);
 int64_t rmx_shard_local_rows(const rmx_shard* sh);
+/* Step 0 of the exchange on/off (default on): send each DISTINCT id of the batch once, as
+ * ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull; results are identical. */
+int rmx_shard_set_dedupe(rmx_shard* sh, int on);
+/* Ids this rank sent to owners in its last exchange (the distinct ids when deduplicating). */
+int64_t rmx_shard_last_sent(const rmx_shard* sh);
 /* Collective (every rank calls it): d_w[i] = w[ids[i]], d_emb[i*k+j] = emb[ids[i]][j] gathered
  * from the owners (makeWeights / makeEmbeddings through the exchange).  Bit-exact copies. */
 int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,

@@ -366,6 +366,14 @@ extern "C" int rmx_gen_ids(rmx_ctx* c, uint64_t seed, int64_t row0, int32_t B, i
   return launch_gen_ids(stream ? (hipStream_t)stream : c->stream, seed, row0, B, F, V, d_ids);
 }
 
+extern "C" int rmx_gen_ids_zipf(rmx_ctx* c, uint64_t seed, int64_t row0, int32_t B, int32_t F, int64_t V,
+                                double exponent, int32_t* d_ids, void* stream) {
+  CHECK_ARG(c && d_ids && B >= 0 && F > 0 && V >= F && exponent > 0.0 && exponent != 1.0,
+            "rmx_gen_ids_zipf: bad args (exponent > 0, != 1)");
+  RMX_HIP(hipSetDevice(c->device));
+  return launch_gen_ids_zipf(stream ? (hipStream_t)stream : c->stream, seed, row0, B, F, V, exponent, d_ids);
+}
+
 extern "C" int rmx_gather(const rmx_table* t, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
                           void* stream) {
   CHECK_ARG(t && d_ids && n >= 0, "rmx_gather: bad args");

@@ -202,6 +202,34 @@ __global__ void gen_ids_kernel(uint64_t seed, int64_t row0, int B, int F, uint64
   ids[i] = (int32_t)((uint64_t)f * per + splitmix64(seed ^ cnt) % per);
 }
 
+// Zipf-like ids (SURVEY.md §8d secondary distribution): rank r in field f with P(r) ~ (r+1)^-s,
+// drawn by inverting the continuous power law on [1, per + 1) in double precision.
+__global__ void gen_ids_zipf_kernel(uint64_t seed, int64_t row0, int B, int F, uint64_t per, double a, double span,
+                                    int32_t* ids) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * F) return;
+  const int64_t b = i / F;
+  const int f = (int)(i - b * F);
+  const uint64_t cnt = (uint64_t)(row0 + b) * (uint64_t)F + (uint64_t)f;
+  const double u = (double)(splitmix64(seed ^ cnt) >> 11) * 0x1.0p-53;
+  int64_t r = (int64_t)floor(pow(1.0 + u * span, 1.0 / a)) - 1;
+  r = r < 0 ? 0 : (r >= (int64_t)per ? (int64_t)per - 1 : r);
+  ids[i] = (int32_t)((uint64_t)f * per + (uint64_t)r);
+}
+
+int launch_gen_ids_zipf(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, double zs,
+                        int32_t* ids) {
+  const int64_t n = (int64_t)B * F;
+  if (n <= 0) return RMX_OK;
+  const uint64_t per = (uint64_t)(V / F);
+  const double a = 1.0 - zs;
+  const double span = pow((double)per + 1.0, a) - 1.0;
+  hipLaunchKernelGGL(gen_ids_zipf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, seed, row0, B, F, per,
+                     a, span, ids);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
 int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids) {
   const int64_t n = (int64_t)B * F;
   if (n <= 0) return RMX_OK;

@@ -575,7 +575,8 @@ template <int NT>
 int launch_cin_nt(hipStream_t s, GemmArgs& p) {
   // knob "cin_variant": 0 = 8 waves x 16 rows, 2 chunks per stage, 4 waves / SIMD (two blocks
   // per CU: 1.637 ms / layer at B = 4,096 vs 1.84 at 3 waves / SIMD); 1 = 8 waves x 32 rows.
-  // Small M always uses 4 waves x 16 rows.
+  // Small M always uses 4 waves x 16 rows.  (An LDS-DMA ring for the weight chunks measured 4-8 %
+  // slower: the A operand is built in registers, so the register-staged W stage is cheap.)
   const int var = tuning_get("cin_variant", 0);
   if (p.M < 8192) return launch_cfg<Tile<1, NT, 4, 1, 2, 1>, kCinOuter, kEpiCin>(s, p);
   if (var == 1) return launch_cfg<Tile<2, NT, 8, 1, 2, 1>, kCinOuter, kEpiCin>(s, p);

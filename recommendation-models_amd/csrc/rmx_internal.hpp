@@ -106,6 +106,8 @@ int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const voi
 int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y);
 int launch_sigmoid_out(hipStream_t s, int B, const float* y, float beta, float* out);
 int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids);
+int launch_gen_ids_zipf(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, double zs,
+                        int32_t* ids);
 int launch_fill_table(hipStream_t s, uint64_t seed, int64_t V, int k, void* w, void* emb, int dt);
 int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const void* wtab,
                   const void* emb, int dt, int k, float* w_out, float* e_out);

@@ -7,6 +7,11 @@
 // Partitioning: owner(id) = id mod N, local row = id div N (Criteo ids are feature hashes, so
 // modulo partitioning balances; it is a bijection [0, V) -> [N] x [ceil(V/N)]).
 // One exchange step per batch on the caller's stream:
+//   0. dedupe  : (default on; rmx_shard_set_dedupe) the batch's distinct ids, as
+//                ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull: an
+//                open-addressing hash set in HBM (atomicCAS insert, linear probing) gives every
+//                nnz its set slot; steps 1-5 then move one row per DISTINCT id and the final
+//                perm[n] = slot of the distinct id of nnz n.
 //   1. route   : per id, owner o and a slot in o's send bucket (block-local LDS histogram + one
 //                global atomic per (block, owner) to reserve a range); send_ids[slot] = local row,
 //                perm[n] = slot.  Copies only, so the bucket order inside a range is irrelevant.
@@ -59,70 +64,124 @@ struct rmx_shard {
   float* send_w = nullptr;              // [recv]
   float* recv_emb = nullptr;            // [nnz][k] rows for this rank's batch (bucket order)
   float* recv_w = nullptr;              // [nnz]
+  // dedupe (step 0)
+  bool dedupe = true;
+  int64_t cap_hash = 0;                 // hash-set slots (power of two >= 2 nnz)
+  int32_t* hkeys = nullptr;             // [cap_hash] distinct ids (-1 = empty)
+  int32_t* hvals = nullptr;             // [cap_hash] bucket slot of the distinct id
+  int32_t* hslot = nullptr;             // [nnz] set slot of id n
+  int64_t last_sent = 0;                // ids sent by the last exchange (distinct ids when deduped)
+  int32_t* bcnt = nullptr;              // [N][tiles] per-tile owner counts -> tile start offsets
+  int64_t cap_tiles = 0;
 };
 
 namespace rmx {
 
 namespace {
 
-constexpr int kRouteThreads = 256, kRoutePer = 8, kMaxRanks = 64;
+constexpr int kRouteThreads = 256, kRoutePer = 8, kRouteTile = kRouteThreads * kRoutePer, kMaxRanks = 64;
 
-// counts[o] += number of ids owned by o (block histogram in LDS, one global atomic per owner)
-__global__ __launch_bounds__(kRouteThreads) void route_count_kernel(int64_t nnz, int N, const int32_t* __restrict__ ids,
-                                                                   int32_t* __restrict__ counts) {
+// Wave-aggregated bucket reservation: the lanes of a wave holding owner o (o >= 0) take
+// consecutive ranks from one LDS atomic by the first such lane (one atomic per distinct owner in the
+// wave instead of one per id: at N = 1 every id would hit the same LDS counter).
+__device__ __forceinline__ int wave_reserve(int o, int* h) {
+  const int lane = threadIdx.x & 63;
+  uint64_t active = __ballot(o >= 0);
+  int rank = 0;
+  while (active) {
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    const int lo = __shfl(o, leader);
+    const uint64_t m = __ballot(o == lo);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&h[lo], __popcll(m));
+    base = __shfl(base, leader);
+    if (o == lo) rank = base + __popcll(m & ((1ull << lane) - 1));
+    active &= ~m;
+  }
+  return rank;
+}
+
+// Routing = count -> scan -> scatter with no global atomics: block b histograms its tile of
+// kRouteTile ids by owner into bcnt[o][b] (wave-aggregated LDS counters), one block per owner scans
+// its column into the tile's start offset, and the scatter pass recomputes the in-tile ranks.
+__device__ __forceinline__ int route_owner(const int32_t* ids, int64_t n, int64_t nnz, int N, int* loc) {
+  if (n >= nnz) return -1;
+  const int id = ids[n];
+  if (id < 0) return -1;  // an empty hash-set slot (dedupe)
+  *loc = id / N;
+  return id % N;
+}
+
+__global__ __launch_bounds__(kRouteThreads) void route_count_kernel(int64_t nnz, int N, int nb,
+                                                                   const int32_t* __restrict__ ids,
+                                                                   int32_t* __restrict__ bcnt) {
   __shared__ int h[kMaxRanks];
   for (int i = threadIdx.x; i < N; i += blockDim.x) h[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kRouteThreads * kRoutePer;
+  const int64_t base = (int64_t)blockIdx.x * kRouteTile;
+  int own[kRoutePer], loc;
 #pragma unroll
-  for (int u = 0; u < kRoutePer; ++u) {
-    const int64_t n = base + u * kRouteThreads + threadIdx.x;
-    if (n < nnz) atomicAdd(&h[ids[n] % N], 1);
-  }
+  for (int u = 0; u < kRoutePer; ++u) own[u] = route_owner(ids, base + u * kRouteThreads + threadIdx.x, nnz, N, &loc);
+#pragma unroll
+  for (int u = 0; u < kRoutePer; ++u) (void)wave_reserve(own[u], h);
   __syncthreads();
-  for (int i = threadIdx.x; i < N; i += blockDim.x)
-    if (h[i]) atomicAdd(&counts[i], h[i]);
+  for (int o = threadIdx.x; o < N; o += blockDim.x) bcnt[(int64_t)o * nb + blockIdx.x] = h[o];
 }
 
-// slot of id n = exclusive_scan(counts)[o] + (range reserved by this block for o) + rank in block
-__global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nnz, int N, const int32_t* __restrict__ ids,
+// block o: exclusive scan of bcnt[o][0..nb) in place; counts[o] = the column total
+__global__ __launch_bounds__(1024) void route_scan_kernel(int nb, int32_t* __restrict__ bcnt,
+                                                          int32_t* __restrict__ counts) {
+  __shared__ int part[1024];
+  int32_t* col = bcnt + (int64_t)blockIdx.x * nb;
+  const int per = (nb + 1023) / 1024;
+  const int t = threadIdx.x, i0 = t * per;
+  int sum = 0;
+  for (int i = i0; i < i0 + per && i < nb; ++i) sum += col[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the thread sums
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int i = i0; i < i0 + per && i < nb; ++i) {
+    const int c = col[i];
+    col[i] = run;
+    run += c;
+  }
+  if (t == 1023) counts[blockIdx.x] = part[1023];
+}
+
+// slot of id n = owner offset + tile start for o + rank in the tile
+__global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nnz, int N, int nb,
+                                                                     const int32_t* __restrict__ ids,
                                                                      const int32_t* __restrict__ counts,
-                                                                     int32_t* __restrict__ cursor,
+                                                                     const int32_t* __restrict__ bstart,
                                                                      int32_t* __restrict__ send_ids,
                                                                      int32_t* __restrict__ perm) {
-  __shared__ int h[kMaxRanks], start[kMaxRanks], off[kMaxRanks];
-  for (int i = threadIdx.x; i < N; i += blockDim.x) h[i] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kRouteThreads * kRoutePer;
-  int own[kRoutePer], loc[kRoutePer], rk[kRoutePer];
-#pragma unroll
-  for (int u = 0; u < kRoutePer; ++u) {
-    const int64_t n = base + u * kRouteThreads + threadIdx.x;
-    own[u] = -1;
-    if (n < nnz) {
-      const int id = ids[n];
-      own[u] = id % N;
-      loc[u] = id / N;
-      rk[u] = atomicAdd(&h[own[u]], 1);
-    }
-  }
-  __syncthreads();
+  __shared__ int h[kMaxRanks], start[kMaxRanks];
   if (threadIdx.x == 0) {
     int s = 0;
     for (int o = 0; o < N; ++o) {
-      off[o] = s;
+      start[o] = s + bstart[(int64_t)o * nb + blockIdx.x];
+      h[o] = 0;
       s += counts[o];
     }
   }
-  for (int o = threadIdx.x; o < N; o += blockDim.x) start[o] = h[o] ? atomicAdd(&cursor[o], h[o]) : 0;
   __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kRouteTile;
+  int own[kRoutePer], loc[kRoutePer];
+#pragma unroll
+  for (int u = 0; u < kRoutePer; ++u) own[u] = route_owner(ids, base + u * kRouteThreads + threadIdx.x, nnz, N, &loc[u]);
 #pragma unroll
   for (int u = 0; u < kRoutePer; ++u) {
-    const int64_t n = base + u * kRouteThreads + threadIdx.x;
+    const int rk = wave_reserve(own[u], h);
     if (own[u] >= 0) {
-      const int slot = off[own[u]] + start[own[u]] + rk[u];
+      const int slot = start[own[u]] + rk;
       send_ids[slot] = loc[u];
-      perm[n] = slot;
+      perm[base + u * kRouteThreads + threadIdx.x] = slot;
     }
   }
 }
@@ -145,6 +204,38 @@ __global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, int k, con
   const int r = rows[t];
   for (int j = 0; j < k; ++j) out_emb[t * k + j] = emb[(int64_t)r * k + j];
   out_w[t] = w[r];
+}
+
+// step 0: insert ids[n] into the hash set; hslot[n] = its slot (first inserter claims an empty one)
+__global__ __launch_bounds__(256) void dedupe_insert_kernel(int64_t nnz, const int32_t* __restrict__ ids,
+                                                           uint32_t mask, int shift, int32_t* __restrict__ keys,
+                                                           int32_t* __restrict__ hslot) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= nnz) return;
+  const int32_t id = ids[n];
+  // Fibonacci hashing: the TOP bits of the 64-bit product (the low bits of id * odd depend only on
+  // the low bits of id, which clusters field-structured ids into long probe chains)
+  uint32_t h = (uint32_t)(((uint64_t)(uint32_t)id * 0x9E3779B97F4A7C15ull) >> shift);
+  while (true) {
+    // a slot changes only once (-1 -> id): a plain read that already shows an id is final, so
+    // repeated ids (skewed batches) mostly skip the device-scope atomic
+    const int32_t seen = __builtin_nontemporal_load(&keys[h]);
+    if (seen == id) break;
+    if (seen == -1) {
+      const int32_t old = atomicCAS(&keys[h], -1, id);
+      if (old == -1 || old == id) break;
+    }
+    h = (h + 1) & mask;  // load factor <= 1/2: terminates
+  }
+  hslot[n] = (int32_t)h;
+}
+
+// perm[n] = bucket slot of the distinct id of nnz n
+__global__ __launch_bounds__(256) void dedupe_perm_kernel(int64_t nnz, const int32_t* __restrict__ hslot,
+                                                         const int32_t* __restrict__ hvals,
+                                                         int32_t* __restrict__ perm) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < nnz) perm[n] = hvals[hslot[n]];
 }
 
 __device__ __forceinline__ uint64_t splitmix64_d(uint64_t x) {
@@ -190,12 +281,26 @@ int realloc_dev(T** p, int64_t n) {
 // [nnz]-sized buffers of this rank's batch
 int ensure_batch(rmx_shard& sh, int64_t nnz) {
   if (nnz <= sh.cap_send) return RMX_OK;
-  RMX_HIP(hipStreamSynchronize(sh.ctx->stream));
+  RMX_HIP(hipDeviceSynchronize());  // in-flight work on any stream may still use the old buffers
   int st;
+  int64_t hc = 1024;
+  while (hc < 2 * nnz) hc <<= 1;
   if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.perm, nnz)) ||
-      (st = realloc_dev(&sh.recv_emb, nnz * sh.k)) || (st = realloc_dev(&sh.recv_w, nnz)))
+      (st = realloc_dev(&sh.recv_emb, nnz * sh.k)) || (st = realloc_dev(&sh.recv_w, nnz)) ||
+      (st = realloc_dev(&sh.hslot, nnz)) || (st = realloc_dev(&sh.hkeys, hc)) || (st = realloc_dev(&sh.hvals, hc)))
     return st;
   sh.cap_send = nnz;
+  sh.cap_hash = hc;
+  return RMX_OK;
+}
+
+// [N][tiles] routing scratch
+int ensure_tiles(rmx_shard& sh, int64_t tiles) {
+  if (tiles <= sh.cap_tiles) return RMX_OK;
+  RMX_HIP(hipDeviceSynchronize());
+  int st;
+  if ((st = realloc_dev(&sh.bcnt, tiles * sh.N))) return st;
+  sh.cap_tiles = tiles;
   return RMX_OK;
 }
 
@@ -277,7 +382,8 @@ int shard_destroy(rmx_shard* sh) {
     (void)hipFree(sh->w[i]);
   }
   for (void* p : {(void*)sh->counts, (void*)sh->send_ids, (void*)sh->perm, (void*)sh->recv_ids,
-                  (void*)sh->send_emb, (void*)sh->send_w, (void*)sh->recv_emb, (void*)sh->recv_w})
+                  (void*)sh->send_emb, (void*)sh->send_w, (void*)sh->recv_emb, (void*)sh->recv_w,
+                  (void*)sh->hkeys, (void*)sh->hvals, (void*)sh->hslot, (void*)sh->bcnt})
     if (p) (void)hipFree(p);
   if (sh->h_counts) (void)hipHostFree(sh->h_counts);
   delete sh;
@@ -306,21 +412,44 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   if ((st = ensure_batch(sh, nnz))) return st;
   int32_t* cnt = sh.counts;           // [N] send counts
   int32_t* rcnt = sh.counts + N;      // [N] recv counts
-  int32_t* cursor = sh.counts + 2 * N;
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
   if (nnz > 0) {
-    const unsigned nb = (unsigned)((nnz + kRouteThreads * kRoutePer - 1) / (kRouteThreads * kRoutePer));
-    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, nnz, N, d_ids, cnt);
+    // route the batch's ids, or (dedupe) the distinct ids held by the hash set's slots
+    const int32_t* rids = d_ids;
+    int64_t rn = nnz;
+    int32_t* rslot = sh.perm;
+    if (sh.dedupe) {
+      RMX_HIP(hipMemsetAsync(sh.hkeys, 0xFF, sizeof(int32_t) * sh.cap_hash, s));
+      hipLaunchKernelGGL(dedupe_insert_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, d_ids,
+                         (uint32_t)(sh.cap_hash - 1), 64 - __builtin_ctzll((unsigned long long)sh.cap_hash),
+                         sh.hkeys, sh.hslot);
+      RMX_HIP(hipGetLastError());
+      rids = sh.hkeys;
+      rn = sh.cap_hash;
+      rslot = sh.hvals;
+    }
+    const int nb = (int)((rn + kRouteTile - 1) / kRouteTile);
+    if ((st = ensure_tiles(sh, nb))) return st;
+    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, sh.bcnt);
     RMX_HIP(hipGetLastError());
-    hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, nnz, N, d_ids, cnt, cursor,
-                       sh.send_ids, sh.perm);
+    hipLaunchKernelGGL(route_scan_kernel, dim3(N), dim3(1024), 0, s, nb, sh.bcnt, cnt);
     RMX_HIP(hipGetLastError());
+    hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, cnt, sh.bcnt,
+                       sh.send_ids, rslot);
+    RMX_HIP(hipGetLastError());
+    if (sh.dedupe) {
+      hipLaunchKernelGGL(dedupe_perm_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, sh.hslot,
+                         sh.hvals, sh.perm);
+      RMX_HIP(hipGetLastError());
+    }
   }
   if (!sh.comm) {
     // loopback: partition o serves bucket o in place
     RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * N, hipMemcpyDeviceToHost, s));
     RMX_HIP(hipStreamSynchronize(s));
     int64_t off = 0;
+    sh.last_sent = 0;
+    for (int o = 0; o < N; ++o) sh.last_sent += sh.h_counts[o];
     for (int o = 0; o < N; ++o) {
       const int64_t c = sh.h_counts[o];
       if ((st = launch_owner_gather(s, c, k, sh.send_ids + off, sh.emb[o], sh.w[o], sh.recv_emb + off * k,
@@ -342,7 +471,11 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   const int32_t* hc = sh.h_counts;
   const int32_t* hr = sh.h_counts + N;
   int64_t nrecv = 0;
-  for (int o = 0; o < N; ++o) nrecv += hr[o];
+  sh.last_sent = 0;
+  for (int o = 0; o < N; ++o) {
+    nrecv += hr[o];
+    sh.last_sent += hc[o];
+  }
   if ((st = ensure_recv(sh, nrecv))) return st;
   // 3. ids to owners
   RMX_NCCL(ncclGroupStart());
@@ -405,6 +538,17 @@ extern "C" int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed) {
 }
 
 extern "C" int64_t rmx_shard_local_rows(const rmx_shard* sh) { return sh ? sh->rows_per : -1; }
+
+extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
+  if (!sh) {
+    set_error("rmx_shard_set_dedupe: NULL shard");
+    return RMX_E_INVALID;
+  }
+  sh->dedupe = on != 0;
+  return RMX_OK;
+}
+
+extern "C" int64_t rmx_shard_last_sent(const rmx_shard* sh) { return sh ? sh->last_sent : -1; }
 
 extern "C" int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
                                 void* stream) {

@@ -250,6 +250,14 @@ class ShardedTable:
     def local_rows(self):
         return int(_lib.lib.rmx_shard_local_rows(self.handle))
 
+    def set_dedupe(self, on):
+        """Send each distinct id of a batch once (default on; ParRecModel.distinctIntIndices)."""
+        check(_lib.lib.rmx_shard_set_dedupe(self.handle, 1 if on else 0))
+
+    def last_sent(self):
+        """Ids this rank sent to owners in its last exchange."""
+        return int(_lib.lib.rmx_shard_last_sent(self.handle))
+
     def gather(self, ids_dev, n, w_out, emb_out, stream=None):
         """Collective: rows of ids_dev from their owners (bit-exact copies)."""
         check(_lib.lib.rmx_shard_gather(self.handle, int(n), ids_dev.ptr, w_out.ptr, emb_out.ptr, stream))
@@ -266,8 +274,13 @@ class ShardedTable:
             pass
 
 
-def gen_ids(ctx, seed, row0, batch, n_fields, num_rows, ids_dev, stream=None):
-    """Synthetic field-partitioned ids straight into HBM (SURVEY.md §8d generator)."""
+def gen_ids(ctx, seed, row0, batch, n_fields, num_rows, ids_dev, stream=None, zipf=0.0):
+    """Synthetic field-partitioned ids straight into HBM (SURVEY.md §8d generator): uniform within
+    the field (bit-identical to oracle orc_gen_ids), or Zipf-like with exponent `zipf` > 0."""
+    if zipf:
+        check(_lib.lib.rmx_gen_ids_zipf(ctx.handle, int(seed), int(row0), int(batch), int(n_fields),
+                                        int(num_rows), float(zipf), ids_dev.ptr, stream))
+        return
     check(_lib.lib.rmx_gen_ids(ctx.handle, int(seed), int(row0), int(batch), int(n_fields), int(num_rows),
                                ids_dev.ptr, stream))
 

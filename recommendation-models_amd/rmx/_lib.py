@@ -77,6 +77,7 @@ SIGNATURES = [
     ("rmx_table_rows", c_i64, [c_vp]),
     ("rmx_table_device_ptrs", c_int, [c_vp, P(c_vp), P(c_vp)]),
     ("rmx_gen_ids", c_int, [c_vp, c_u64, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp]),
+    ("rmx_gen_ids_zipf", c_int, [c_vp, c_u64, c_i64, c_i32, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     ("rmx_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_forward_ids", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
     ("rmx_model_set_timing", c_int, [c_vp, c_int]),
@@ -87,6 +88,8 @@ SIGNATURES = [
     ("rmx_shard_destroy", c_int, [c_vp]),
     ("rmx_shard_fill_synthetic", c_int, [c_vp, c_u64]),
     ("rmx_shard_local_rows", c_i64, [c_vp]),
+    ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),
+    ("rmx_shard_last_sent", c_i64, [c_vp]),
     ("rmx_shard_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_forward_ids_sharded", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
 ]

@@ -28,7 +28,17 @@ def route(ids, N):
     return counts, send_ids, perm
 
 
-def exchange(dist, torch, ids, w_loc, e_loc, N, k):
+def dedupe(ids):
+    """Step 0 (ParRecModel.distinctIntIndices, ParRecModel.scala:337-345): distinct ids + inverse."""
+    uniq, inv = np.unique(ids, return_inverse=True)
+    return uniq, inv
+
+
+def exchange(dist, torch, ids, w_loc, e_loc, N, k, use_dedupe=True):
+    if use_dedupe:
+        uniq, inv = dedupe(ids)
+        w_u, e_u = exchange(dist, torch, uniq, w_loc, e_loc, N, k, use_dedupe=False)
+        return w_u[inv], e_u[inv]
     counts, send_ids, perm = route(ids, N)
     rc = torch.zeros(N, dtype=torch.int64)
     dist.all_to_all_single(rc, torch.from_numpy(counts))
@@ -52,8 +62,11 @@ def worker(rank, world, port, V, k, B, F, out_dir):
     wt, et = oc.gen_table(0x7AB1E, V, k)
     w_loc, e_loc = partition(wt, et, world, rank)
     ids = oc.gen_ids(0x5EED2026, rank * B, B, F, V).astype(np.int64)
+    ids[::3] = ids[0]  # repeated ids: the dedupe step has work to do
     w, e = exchange(dist, torch, ids, w_loc, e_loc, world, k)
-    ok_rows = np.array_equal(w, wt[ids]) and np.array_equal(e, et[ids])
+    w2, e2 = exchange(dist, torch, ids, w_loc, e_loc, world, k, use_dedupe=False)
+    ok_rows = (np.array_equal(w, wt[ids]) and np.array_equal(e, et[ids]) and np.array_equal(w2, w)
+               and np.array_equal(e2, e))
     m = oc.make_model(oc.DEEPFM, F, k, fc=(16,))
     mats = oc.init_mats(m, 3)
     index = np.repeat(np.arange(B, dtype=np.int64), F)

@@ -48,32 +48,59 @@ def test_route_is_a_bijection():
 
 
 # ------------------------------------------------------------------ GPU ----
-def _setup(ctx, V, B, seed_row=0):
+def _setup(ctx, V, B, seed_row=0, zipf=0.0):
     import rmx
     table = rmx.EmbeddingTable(ctx, V, K)
     table.fill_synthetic(SEED_TAB)
     ids = rmx.DeviceArray(ctx, B * F, np.int32)
-    rmx.gen_ids(ctx, SEED_IDS, seed_row, B, F, V, ids)
+    rmx.gen_ids(ctx, SEED_IDS, seed_row, B, F, V, ids, zipf=zipf)
     return table, ids
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dedupe", [True, False])
+@pytest.mark.parametrize("zipf", [0.0, 1.1])
 @pytest.mark.parametrize("N", [1, 2, 3, 8])
-def test_loopback_shard_gather_bit_exact(N):
+def test_loopback_shard_gather_bit_exact(N, zipf, dedupe):
     import rmx
     ctx = rmx.default_context()
     V, B = 100_003, 300
-    _, ids = _setup(ctx, V, B)
+    _, ids = _setup(ctx, V, B, zipf=zipf)
     sh = rmx.ShardedTable(ctx, V, K, N)
+    sh.set_dedupe(dedupe)
     sh.fill_synthetic(SEED_TAB)
     n = B * F
     w = rmx.DeviceArray(ctx, n, np.float32)
     e = rmx.DeviceArray(ctx, n * K, np.float32)
     sh.gather(ids, n, w, e)
     ctx.sync()
+    h_ids = ids.numpy().astype(np.int64)
     wt, et = oc.gen_table(SEED_TAB, V, K)
-    w_ref, e_ref = oc.gather(wt, et, 1, ids.numpy().astype(np.int64))
+    w_ref, e_ref = oc.gather(wt, et, 1, h_ids)
     assert np.array_equal(w.numpy(), w_ref) and np.array_equal(e.numpy(), e_ref)
+    # step 0 sends each distinct id once
+    assert sh.last_sent() == (len(np.unique(h_ids)) if dedupe else n)
+
+
+@pytest.mark.gpu
+def test_gen_ids_zipf_shape():
+    """Zipf-like ids: inside each field's range, deterministic, rank 0 the most frequent."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 1_000_000, 4096
+    per = V // F
+    a = rmx.DeviceArray(ctx, B * F, np.int32)
+    b = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, a, zipf=1.1)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, b, zipf=1.1)
+    ctx.sync()
+    x = a.numpy().reshape(B, F).astype(np.int64)
+    assert np.array_equal(x, b.numpy().reshape(B, F))
+    r = x - np.arange(F)[None, :] * per
+    assert r.min() >= 0 and r.max() < per
+    cnt = np.bincount(r.ravel(), minlength=per)
+    assert cnt[0] == cnt.max() and cnt[0] > 0.05 * B * F
+    assert len(np.unique(x)) < 0.5 * B * F  # heavy reuse (the point of the dedupe step)
 
 
 def _models():
@@ -90,16 +117,18 @@ def _models():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn", "pnn", "lr"])
-@pytest.mark.parametrize("N", [1, 4, 8])
-def test_sharded_forward_bitwise_equals_replicated(kind, N):
+@pytest.mark.parametrize("N,zipf,dedupe", [(1, 0.0, True), (4, 0.0, True), (8, 0.0, True), (8, 1.1, True),
+                                           (4, 1.1, False)])
+def test_sharded_forward_bitwise_equals_replicated(kind, N, zipf, dedupe):
     import rmx
     ctx = rmx.default_context()
     V, B = 100_003, 1000
-    table, ids = _setup(ctx, V, B, seed_row=11)
+    table, ids = _setup(ctx, V, B, seed_row=11, zipf=zipf)
     m = _models()[kind]()
     m.setMats(m.initMats(SEED_MATS))
     m.setBias(0.01)
     sh = rmx.ShardedTable(ctx, V, K, N)
+    sh.set_dedupe(dedupe)
     sh.fill_synthetic(SEED_TAB)
     ref = rmx.DeviceArray(ctx, B, np.float32)
     got = rmx.DeviceArray(ctx, B, np.float32)
