@@ -93,6 +93,15 @@ int32_t orc_forward(const orc_model* m, int32_t B, int64_t nnz, const int64_t* i
  * y1[B] first order (Scatter), y2[B] FM second order (DeepFM only, else 0). */
 int32_t orc_first_order(int32_t B, int64_t nnz, const int64_t* index, const float* weights, float* y1);
 int32_t orc_fm(int32_t B, int32_t F, int32_t k, const float* embedding, float* y2);
+/* ---- backward (RecModel.backward, yr/model/RecModel.scala:65-115; oracle/rmx_oracle_train.c) ----
+ * Same inputs as orc_forward plus targets[B] (label > 0 -> 1).  Writes the gradients the
+ * reference writes back into the caller's arrays (yr/util/GradUtil.scala, BackwardUtil.scala):
+ * g_bias[1], g_weights[nnz], g_embedding[nnz*k], g_mats[mats_len], and the mean BCE loss.
+ * f64 throughout; arrays a model type does not use may be NULL. */
+int32_t orc_backward(const orc_model* m, int32_t B, int64_t nnz, const int64_t* index, const float* bias,
+                     const float* weights, const float* embedding, const float* mats, const float* targets,
+                     float* g_bias, float* g_weights, float* g_embedding, float* g_mats, double* loss_out);
+
 /* bf16 round-to-nearest-even of n fp32 values (the device's v_cvt_pk_bf16_f32 for finite values) */
 void orc_round_bf16(int64_t n, const float* x, float* y);
 

@@ -53,8 +53,9 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+    srcs = [os.path.join(ORACLE_DIR, f) for f in os.listdir(ORACLE_DIR) if f.endswith((".c", ".h"))]
+    if not os.path.exists(LIB_PATH) or max(os.path.getmtime(f) for f in srcs) > os.path.getmtime(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-B", "-C", ORACLE_DIR])
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.POINTER
     f32p, i64p, i32p = P(ctypes.c_float), P(ctypes.c_int64), P(ctypes.c_int32)
@@ -80,6 +81,9 @@ def lib():
     L.orc_fm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, f32p, f32p]
     L.orc_fm.restype = ctypes.c_int32
     L.orc_round_bf16.argtypes = [ctypes.c_int64, f32p, f32p]
+    L.orc_backward.argtypes = [P(OrcModel), ctypes.c_int32, ctypes.c_int64, i64p, f32p, f32p, f32p, f32p, f32p,
+                               f32p, f32p, f32p, f32p, P(ctypes.c_double)]
+    L.orc_backward.restype = ctypes.c_int32
     _lib = L
     return L
 
@@ -182,3 +186,27 @@ def round_bf16(x):
     y = np.empty_like(x)
     lib().orc_round_bf16(x.size, _p(x, ctypes.c_float), _p(y, ctypes.c_float))
     return y
+
+
+def backward(m, B, index, bias, weights, embedding, mats, targets):
+    """RecModel.backward restated (f64): returns dict(loss, bias, weights, embedding, mats) of the
+    gradients the reference writes back into the caller's arrays."""
+    index = np.ascontiguousarray(index, np.int64)
+    bias = np.ascontiguousarray(bias, np.float32).reshape(-1)
+    weights = None if weights is None else np.ascontiguousarray(weights, np.float32)
+    embedding = None if embedding is None else np.ascontiguousarray(embedding, np.float32).reshape(-1)
+    mats = None if mats is None else np.ascontiguousarray(mats, np.float32)
+    targets = np.ascontiguousarray(targets, np.float32)
+    nnz = len(index)
+    gb = np.zeros(1, np.float32)
+    gw = np.zeros(nnz, np.float32) if weights is not None else None
+    ge = np.zeros(embedding.size, np.float32) if embedding is not None else None
+    gm = np.zeros(mats.size, np.float32) if mats is not None else None
+    loss = ctypes.c_double()
+    st = lib().orc_backward(ctypes.byref(m), B, nnz, _p(index, ctypes.c_int64), _p(bias, ctypes.c_float),
+                            _p(weights, ctypes.c_float), _p(embedding, ctypes.c_float), _p(mats, ctypes.c_float),
+                            _p(targets, ctypes.c_float), _p(gb, ctypes.c_float), _p(gw, ctypes.c_float),
+                            _p(ge, ctypes.c_float), _p(gm, ctypes.c_float), ctypes.byref(loss))
+    if st != 0:
+        raise ValueError("oracle backward status %d" % st)
+    return {"loss": loss.value, "bias": gb, "weights": gw, "embedding": ge, "mats": gm}
