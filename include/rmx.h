@@ -130,6 +130,17 @@ int rmx_forward(rmx_model* m, int32_t batch_size, int64_t nnz, const int64_t* in
                 const float* embedding, int32_t embedding_dim, const float* mats,
                 const int32_t* mat_sizes, int32_t n_sizes, const int64_t* fields, float* out);
 
+/* L-A backward: RecModel.backward(batchSize, batch, bias, weights, embeddings, embeddingDim,
+ *        mats, matSizes[, fields], targets): Float                RecModel.scala:65-115
+ * Same arrays and checks as rmx_forward plus targets[batch_size] (label > 0 -> 1).  On return the
+ * caller's bias / weights / embedding / mats arrays hold the GRADIENTS, as the reference writes
+ * them back in place (yr/util/GradUtil.scala:7-42, BackwardUtil.scala:6-30), and *loss the mean
+ * BCE loss (BigDL BCECriterion, sizeAverage).  fp32 models; LR, DeepFM and DNN so far. */
+int rmx_backward(rmx_model* m, int32_t batch_size, int64_t nnz, const int64_t* index,
+                 const int64_t* feats, float* bias, float* weights, float* embedding,
+                 int32_t embedding_dim, float* mats, const int32_t* mat_sizes, int32_t n_sizes,
+                 const int64_t* fields, const float* targets, float* loss);
+
 /* Deterministic synthetic mats (Xavier-uniform weights, U(-0.01, 0.01) biases), bit-identical
  * to oracle/orc_init_mats; works on host-only models (ctx == NULL). */
 int rmx_model_init_mats(const rmx_model* m, uint64_t seed, float* mats);
@@ -163,6 +174,15 @@ int rmx_table_device_ptrs(const rmx_table* t, void** d_weights, void** d_embeddi
 /* Synthetic field-partitioned ids into device memory, bit-identical to orc_gen_ids. */
 int rmx_gen_ids(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,
                 int64_t num_rows, int32_t* d_ids, void* stream);
+/* L-B backward on the device-resident table: one training pass (forward with stored
+ * activations, BCE, gradients) over ids [B][F].  Device outputs, each may be NULL: g_bias[1],
+ * g_weights[B*F] (per nonzero, Scatter backward), g_embedding[B*F*k] (per nonzero),
+ * g_mats[mats_len] (getMatsSize layout), loss[1].  The sparse per-nonzero gradients are what the
+ * reference hands to makeGrad/push (ParRecModel.scala:439-478). */
+int rmx_backward_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32_t* d_ids,
+                     const float* d_targets, float* d_g_bias, float* d_g_weights, float* d_g_embedding,
+                     float* d_g_mats, float* d_loss, void* stream);
+
 /* Zipf-like ids (SURVEY.md §8d secondary): rank r of field f drawn with P(r) ~ (r+1)^-exponent
  * (continuous power-law inversion, double precision), id = f * (num_rows / n_fields) + r. */
 int rmx_gen_ids_zipf(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,

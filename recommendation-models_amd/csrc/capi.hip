@@ -427,16 +427,11 @@ extern "C" int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
   return launch_encoder(s, mode, B, d_ids, t->emb, t->w, t->dtype, m->F, t->k, d_y, nullptr, nullptr);
 }
 
-extern "C" int rmx_forward(rmx_model* m, int32_t B, int64_t nnz, const int64_t* index, const int64_t* feats,
-                           const float* bias, const float* weights, const float* embedding,
-                           int32_t embedding_dim, const float* mats, const int32_t* mat_sizes,
-                           int32_t n_sizes, const int64_t* fields, float* out) {
-  (void)feats;
-  (void)fields;  // no reference model reads "fields" (SURVEY.md §0.5)
-  CHECK_ARG(m, "rmx_forward: model is NULL");
-  CHECK_ARG(m->ctx, "rmx_forward: host-only model (created without a context)");
-  CHECK_ARG(out || B == 0, "rmx_forward: out is NULL");
-  CHECK_ARG(B >= 0 && nnz >= 0, "rmx_forward: negative batch_size / nnz");
+// The params-map contract shared by RecModel.forward / backward (RecModel.scala:130-155):
+// required keys per RecModelType, Reshape(B, F, k), matSizes, Scatter's index bound.
+static int check_la(rmx_model* m, int32_t B, int64_t nnz, const int64_t* index, const float* bias,
+                    const float* weights, const float* embedding, int32_t embedding_dim, const float* mats,
+                    const int32_t* mat_sizes, int32_t n_sizes, bool* pregular, bool* psorted) {
   // params-map keys required by the model's RecModelType (NoSuchElementException in the reference)
   if (!bias) { set_error("key not found: bias"); return RMX_E_INVALID; }
   const bool needs_w = m->type != RMX_MODEL_DNN;
@@ -475,7 +470,142 @@ extern "C" int rmx_forward(rmx_model* m, int32_t B, int64_t nnz, const int64_t* 
     if (regular && ix != (int32_t)(n / m->F)) regular = false;
     if (n > 0 && ix < (int32_t)index[n - 1]) sorted = false;
   }
+  *pregular = regular;
+  *psorted = sorted;
+  return RMX_OK;
+}
+
+extern "C" int rmx_forward(rmx_model* m, int32_t B, int64_t nnz, const int64_t* index, const int64_t* feats,
+                           const float* bias, const float* weights, const float* embedding,
+                           int32_t embedding_dim, const float* mats, const int32_t* mat_sizes,
+                           int32_t n_sizes, const int64_t* fields, float* out) {
+  (void)feats;
+  (void)fields;  // no reference model reads "fields" (SURVEY.md §0.5)
+  CHECK_ARG(m, "rmx_forward: model is NULL");
+  CHECK_ARG(m->ctx, "rmx_forward: host-only model (created without a context)");
+  CHECK_ARG(out || B == 0, "rmx_forward: out is NULL");
+  CHECK_ARG(B >= 0 && nnz >= 0, "rmx_forward: negative batch_size / nnz");
+  bool regular = false, sorted = false;
+  int st = check_la(m, B, nnz, index, bias, weights, embedding, embedding_dim, mats, mat_sizes, n_sizes, &regular,
+                    &sorted);
+  if (st) return st;
   if (B == 0) return RMX_OK;
   RMX_HIP(hipSetDevice(m->ctx->device));
   return model_forward_host(*m, B, nnz, index, regular, sorted, bias[0], weights, embedding, mats, out);
+}
+
+// ------------------------------------------------------------- backward --
+
+extern "C" int rmx_backward_ids(rmx_model* m, const rmx_table* t, int32_t B, const int32_t* d_ids,
+                                const float* d_targets, float* d_g_bias, float* d_g_weights, float* d_g_embedding,
+                                float* d_g_mats, float* d_loss, void* stream) {
+  CHECK_ARG(m && t && B >= 0, "rmx_backward_ids: bad args");
+  CHECK_ARG(m->ctx, "rmx_backward_ids: host-only model (created without a context)");
+  CHECK_ARG((d_ids && d_targets) || B == 0, "rmx_backward_ids: ids / targets is NULL");
+  if (!m->params_ready && m->mats_len > 0) {
+    set_error("rmx_backward_ids: call rmx_model_set_mats first");
+    return RMX_E_INVALID;
+  }
+  if (!m->beta_set) {
+    set_error("rmx_backward_ids: call rmx_model_set_bias first");
+    return RMX_E_INVALID;
+  }
+  if (m->type != RMX_MODEL_LR && t->k != m->k) {
+    set_error("rmx_backward_ids: table embedding_dim differs from the model's");
+    return RMX_E_SHAPE;
+  }
+  if (t->dtype != RMX_DTYPE_F32) {
+    set_error("rmx_backward_ids: fp32 tables only");
+    return RMX_E_INVALID;
+  }
+  RMX_HIP(hipSetDevice(m->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  FwdInputs in;
+  in.B = B;
+  in.ids = d_ids;
+  in.table = t->emb;
+  in.wtab = t->w;
+  in.dtype = t->dtype;
+  in.beta = m->beta;
+  TrainOutputs o;
+  o.targets = d_targets;
+  o.nnz = (int64_t)B * m->F;
+  o.g_bias = d_g_bias;
+  o.g_w = d_g_weights;
+  o.g_emb = m->type == RMX_MODEL_LR ? nullptr : d_g_embedding;
+  o.g_mats = d_g_mats;
+  o.loss = d_loss;
+  return model_train(*m, s, in, o);
+}
+
+extern "C" int rmx_backward(rmx_model* m, int32_t B, int64_t nnz, const int64_t* index, const int64_t* feats,
+                            float* bias, float* weights, float* embedding, int32_t embedding_dim, float* mats,
+                            const int32_t* mat_sizes, int32_t n_sizes, const int64_t* fields, const float* targets,
+                            float* loss) {
+  (void)feats;
+  (void)fields;
+  CHECK_ARG(m, "rmx_backward: model is NULL");
+  CHECK_ARG(m->ctx, "rmx_backward: host-only model (created without a context)");
+  CHECK_ARG(B >= 0 && nnz >= 0, "rmx_backward: negative batch_size / nnz");
+  if (!targets && B > 0) { set_error("key not found: targets"); return RMX_E_INVALID; }
+  bool regular = false, sorted = false;
+  int st = check_la(m, B, nnz, index, bias, weights, embedding, embedding_dim, mats, mat_sizes, n_sizes, &regular,
+                    &sorted);
+  if (st) return st;
+  if (B == 0) {
+    if (loss) *loss = 0.f;
+    return RMX_OK;
+  }
+  RMX_HIP(hipSetDevice(m->ctx->device));
+  hipStream_t s = m->ctx->stream;
+  FwdInputs in;
+  if ((st = model_stage_host(*m, B, nnz, index, regular, sorted, bias[0], weights, embedding, mats, &in))) return st;
+  rmx_model::LaGrad* lb = &m->la_grad;
+  const bool use_w = m->type != RMX_MODEL_DNN, use_e = m->type != RMX_MODEL_LR;
+  if (nnz > lb->nnz || B > lb->B || m->mats_len > lb->ml) {
+    RMX_HIP(hipStreamSynchronize(s));
+    for (void* p : {(void*)lb->gw, (void*)lb->ge, (void*)lb->gm, (void*)lb->gb, (void*)lb->tg, (void*)lb->idx})
+      if (p) (void)hipFree(p);
+    *lb = rmx_model::LaGrad{};
+    const int64_t n1 = std::max<int64_t>(nnz, 1);
+    if (hipMalloc(&lb->gw, sizeof(float) * n1) != hipSuccess ||
+        hipMalloc(&lb->ge, sizeof(float) * n1 * std::max(m->k, 1)) != hipSuccess ||
+        hipMalloc(&lb->gm, sizeof(float) * std::max<int64_t>(m->mats_len, 1)) != hipSuccess ||
+        hipMalloc(&lb->gb, sizeof(float) * 2) != hipSuccess || hipMalloc(&lb->tg, sizeof(float) * B) != hipSuccess ||
+        hipMalloc(&lb->idx, sizeof(int32_t) * n1) != hipSuccess) {
+      set_error("rmx_backward: out of device memory");
+      return RMX_E_NOMEM;
+    }
+    lb->nnz = nnz;
+    lb->B = B;
+    lb->ml = m->mats_len;
+  }
+  RMX_HIP(hipMemcpyAsync(lb->tg, targets, sizeof(float) * B, hipMemcpyHostToDevice, s));
+  std::vector<int32_t> idx32;
+  if (use_w && !regular) {
+    idx32.resize(nnz);
+    for (int64_t n = 0; n < nnz; ++n) idx32[n] = (int32_t)index[n];
+    RMX_HIP(hipMemcpyAsync(lb->idx, idx32.data(), sizeof(int32_t) * nnz, hipMemcpyHostToDevice, s));
+  }
+  TrainOutputs o;
+  o.targets = lb->tg;
+  o.index = (use_w && !regular) ? lb->idx : nullptr;
+  o.nnz = nnz;
+  o.g_bias = lb->gb;
+  o.g_w = use_w ? lb->gw : nullptr;
+  o.g_emb = use_e ? lb->ge : nullptr;
+  o.g_mats = m->mats_len > 0 ? lb->gm : nullptr;
+  o.loss = lb->gb + 1;
+  if ((st = model_train(*m, s, in, o))) return st;
+  // RecModel.backward's write-back: the caller's arrays now hold the gradients (GradUtil.scala)
+  float hb[2];
+  RMX_HIP(hipMemcpyAsync(hb, lb->gb, sizeof(float) * 2, hipMemcpyDeviceToHost, s));
+  if (use_w && nnz > 0) RMX_HIP(hipMemcpyAsync(weights, lb->gw, sizeof(float) * nnz, hipMemcpyDeviceToHost, s));
+  if (use_e && nnz > 0)
+    RMX_HIP(hipMemcpyAsync(embedding, lb->ge, sizeof(float) * nnz * m->k, hipMemcpyDeviceToHost, s));
+  if (m->mats_len > 0) RMX_HIP(hipMemcpyAsync(mats, lb->gm, sizeof(float) * m->mats_len, hipMemcpyDeviceToHost, s));
+  RMX_HIP(hipStreamSynchronize(s));
+  bias[0] = hb[0];
+  if (loss) *loss = hb[1];
+  return RMX_OK;
 }

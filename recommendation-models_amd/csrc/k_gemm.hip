@@ -55,6 +55,13 @@ __global__ __launch_bounds__(256) void tower_head_kernel(int M, int N, const flo
   oa.out[m] = 1.0f / (1.0f + expf(-t));
 }
 
+int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa) {
+  if (M <= 0) return RMX_OK;
+  hipLaunchKernelGGL(tower_head_kernel, dim3((M + 3) / 4), dim3(256), 0, s, M, N, h, ldh, oa);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
 // C_l (H x F*Hp row-major, column f*Hp + h) -> [Hp_pad/16][F][Npad][16]
 __global__ void pack_cin_kernel(const float* __restrict__ C, int F, int Hp, int H, int Npad, int64_t tot,
                                 float* __restrict__ Wp) {

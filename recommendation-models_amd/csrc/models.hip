@@ -375,6 +375,11 @@ void model_init_mats(const rmx_model& m, uint64_t seed, float* mats) {
 }
 
 void model_release(rmx_model& m) {
+  train_release(m);
+  for (void* p : {(void*)m.la_grad.gw, (void*)m.la_grad.ge, (void*)m.la_grad.gm, (void*)m.la_grad.gb,
+                  (void*)m.la_grad.tg, (void*)m.la_grad.idx})
+    if (p) (void)hipFree(p);
+  m.la_grad = rmx_model::LaGrad{};
   if (!m.ctx) return;
   (void)hipSetDevice(m.ctx->device);
   (void)hipStreamSynchronize(m.ctx->stream);
@@ -544,6 +549,8 @@ int ensure_ws(rmx_model& m, int B) {
 
 }  // namespace
 
+int model_ensure_ws(rmx_model& m, int B) { return ensure_ws(m, B); }
+
 static hipEvent_t take_event(rmx_model& m) {
   if (!m.ev_pool.empty()) {
     hipEvent_t e = m.ev_pool.back();
@@ -691,9 +698,10 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
 }
 
 // L-A: the reference's host-array contract.
-int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
-                       float bias, const float* weights, const float* embedding, const float* mats,
-                       float* out) {
+// Stages the L-A host arrays on the device (mats packed, E / w uploaded, irregular first order
+// precomputed) and describes them as one forward's inputs (implicit ids b*F + f).
+int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
+                     float bias, const float* weights, const float* embedding, const float* mats, FwdInputs* pin) {
   hipStream_t s = m.ctx->stream;
   int st;
   if (nnz > m.la_nnz) {
@@ -778,6 +786,17 @@ int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, b
   in.y1 = csr ? m.y12 : nullptr;
   in.beta = bias;
   in.out = m.la_out;
+  *pin = in;
+  return RMX_OK;
+}
+
+int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
+                       float bias, const float* weights, const float* embedding, const float* mats,
+                       float* out) {
+  hipStream_t s = m.ctx->stream;
+  FwdInputs in;
+  int st = model_stage_host(m, B, nnz, index, regular, sorted, bias, weights, embedding, mats, &in);
+  if (st) return st;
   if ((st = model_forward(m, s, in))) return st;
   RMX_HIP(hipMemcpyAsync(out, m.la_out, sizeof(float) * B, hipMemcpyDeviceToHost, s));
   RMX_HIP(hipStreamSynchronize(s));

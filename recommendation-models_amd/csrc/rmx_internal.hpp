@@ -101,6 +101,8 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
                        const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa,
                        const XColArgs* xc = nullptr);
 
+// logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
+int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table,
                    const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob);
 int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y);

@@ -24,6 +24,8 @@ struct rmx_table {
 
 namespace rmx {
 
+struct TrainState;  // train.hip: backward workspace + rocBLAS handle
+
 // One forward's inputs, already on the device.
 struct FwdInputs {
   int B = 0;
@@ -108,6 +110,13 @@ struct rmx_model {
   std::vector<int64_t> h_rowptr;
   std::vector<float> h_wperm;
 
+  rmx::TrainState* train = nullptr;          // backward (train.hip), created on first use
+  struct LaGrad {                            // L-A backward staging (rmx_backward), grown on demand
+    int64_t nnz = 0, B = 0, ml = 0;
+    float *gw = nullptr, *ge = nullptr, *gm = nullptr, *gb = nullptr, *tg = nullptr;
+    int32_t* idx = nullptr;
+  } la_grad;
+
   // ---- stage timing ----
   bool timing = false;
   int timed_calls = 0;
@@ -129,6 +138,25 @@ int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, b
                        float bias, const float* weights, const float* embedding, const float* mats,
                        float* out);
 int model_collect_timing(rmx_model& m);
+int model_ensure_ws(rmx_model& m, int B);  // inference workspace (y12, h, ...) for batches <= B
+int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
+                     float bias, const float* weights, const float* embedding, const float* mats, FwdInputs* in);
+
+// Backward (train.hip).  One training pass over a batch: forward with stored activations, BCE
+// loss, and the gradients RecModel.backward writes back (all device pointers; g_w / g_emb may be
+// null).  index: device int32 COO rows of the nnz weights (null: n / F).  loss: device [1].
+struct TrainOutputs {
+  const float* targets = nullptr;   // [B]
+  const int32_t* index = nullptr;   // [nnz] or null
+  int64_t nnz = 0;
+  float* g_bias = nullptr;          // [1]
+  float* g_w = nullptr;             // [nnz]
+  float* g_emb = nullptr;           // [nnz * k]
+  float* g_mats = nullptr;          // [mats_len]
+  float* loss = nullptr;            // [1]
+};
+int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOutputs& o);
+void train_release(rmx_model& m);
 
 // Records HIP events around a stage on stream s when the model's timing is enabled.
 struct StageTimer {

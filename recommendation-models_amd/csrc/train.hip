@@ -1,0 +1,379 @@
+// train.hip -- RecModel.backward on the device: BCE loss + the gradients the reference writes
+// back into the caller's arrays.
+//
+// Reference: yr/model/deepfm/DeepFM.scala:83-124 (and the other models' backward halves),
+// bnn/Scatter.scala:38-59, yr/util/GradUtil.scala:7-42, yr/util/BackwardUtil.scala:6-30
+// (paths under /root/reference/src/main/scala/, yr/ = io/yaochi/recommendation/,
+// bnn/ = com/intel/analytics/bigdl/nn/).  BigDL BCECriterion (sizeAverage, eps = 1e-12) and
+// Sigmoid backward as published (oracle/rmx_oracle_train.c states the math).
+//
+// Pass structure (fp32, one stream):
+//   forward   same kernels as the inference path, but every hidden activation h_l [B][Npad_l]
+//             is stored (ReLU-store epilogue), the tower input x = Reshape(E) is materialised,
+//             and the logit head runs over the stored last hidden layer;
+//   loss      bce_kernel: p -> dL/dz per row + per-block partial sums (deterministic tree);
+//   tower     per layer, from the top: dW = dPre^T x_in and dx_in = dPre W are plain fp32 GEMMs
+//             (rocBLAS: the library path for plain GEMMs), db = dPre^T 1 (GEMV); the ReLU mask
+//             of the layer below is applied by a streaming kernel;
+//   encoders  emb_grad_kernel: dL/dE = dx (tower) + FM term dz (s_j - e_fj) / k; dL/dw[n] =
+//             dz[index[n]] (Scatter backward).
+#include <rocblas/rocblas.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "rmx_models.hpp"
+
+#define RMX_BLAS(expr)                                                                      \
+  do {                                                                                      \
+    rocblas_status _s = (expr);                                                             \
+    if (_s != rocblas_status_success) {                                                     \
+      ::rmx::set_error(std::string("rocBLAS error ") + rocblas_status_to_string(_s) + " at " \
+                       __FILE__ ":" + std::to_string(__LINE__) + ": " #expr);              \
+      return RMX_E_HIP;                                                                     \
+    }                                                                                       \
+  } while (0)
+
+namespace rmx {
+
+struct TrainState {
+  rocblas_handle blas = nullptr;
+  int B = 0;
+  int ldx = 0;                  // row stride of x / dx
+  float* x = nullptr;           // [B][ldx] tower input (Reshape(B, F*k) of the gathered rows)
+  std::vector<float*> h;        // per tower layer [B][Npad]
+  float* g[2] = {nullptr, nullptr};  // [B][maxld] dPre / dx ping-pong
+  float* p = nullptr;           // [B] probabilities
+  float* dz = nullptr;          // [B] dL/dlogit
+  float* ones = nullptr;        // [B]
+  double* part = nullptr;       // [2 * kMaxParts] loss / dz partial sums
+  int64_t cap_idx = 0;
+  int32_t* idx = nullptr;       // L-A index (int32) staging
+};
+
+namespace {
+
+constexpr int kRedThreads = 256, kMaxParts = 1024;
+
+template <class T>
+void tfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+int talloc(float** p, size_t n) {
+  if (hipMalloc((void**)p, sizeof(float) * std::max<size_t>(n, 1)) != hipSuccess) {
+    set_error("backward: out of device memory (" + std::to_string(n * sizeof(float)) + " bytes)");
+    return RMX_E_NOMEM;
+  }
+  return RMX_OK;
+}
+
+__global__ void fill_kernel(int n, float v, float* __restrict__ y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = v;
+}
+
+// BCECriterion + Sigmoid backward, per row; block partial sums of the loss terms and of dz.
+__global__ __launch_bounds__(kRedThreads) void bce_kernel(int B, const float* __restrict__ p,
+                                                          const float* __restrict__ targets, float* __restrict__ dz,
+                                                          int per_block, double* __restrict__ part) {
+  __shared__ double sl[kRedThreads], sg[kRedThreads];
+  const float eps = 1e-12f, norm = 1.0f / (float)B;
+  double l = 0.0, gsum = 0.0;
+  const int b0 = blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  for (int b = b0 + threadIdx.x; b < b1; b += kRedThreads) {
+    const float x = p[b];
+    const float t = targets[b] > 0.f ? 1.f : 0.f;  // DeepFM.scala:106
+    l += -((double)t * log((double)x + eps) + (1.0 - t) * log(1.0 - (double)x + eps));
+    const float gp = -(t - x) * norm / ((1.f - x + eps) * (x + eps));  // dL/dp
+    const float g = gp * (1.f - x) * x;                                 // Sigmoid backward
+    dz[b] = g;
+    gsum += g;
+  }
+  sl[threadIdx.x] = l;
+  sg[threadIdx.x] = gsum;
+  __syncthreads();
+  for (int o = kRedThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sl[threadIdx.x] += sl[threadIdx.x + o];
+      sg[threadIdx.x] += sg[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = sl[0];
+    part[kMaxParts + blockIdx.x] = sg[0];
+  }
+}
+
+// loss = sum(part_l) / B; every non-null target of the bias gradient = sum(part_g)
+__global__ void bce_finish_kernel(int nparts, int B, const double* __restrict__ part, float* __restrict__ loss,
+                                  float* __restrict__ gbias, float* __restrict__ gbias2) {
+  if (threadIdx.x != 0) return;
+  double l = 0.0, g = 0.0;
+  for (int i = 0; i < nparts; ++i) {
+    l += part[i];
+    g += part[kMaxParts + i];
+  }
+  if (loss) *loss = (float)(l / B);
+  if (gbias) *gbias = (float)g;
+  if (gbias2) *gbias2 = (float)g;
+}
+
+// dPre of the last hidden layer: g[b][n] = dz[b] * wo[n] masked by ReLU (h > 0)
+__global__ void head_back_kernel(int B, int N, const float* __restrict__ h, int ldh, const float* __restrict__ dz,
+                                 const float* __restrict__ wo, float* __restrict__ g, int ldg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * N) return;
+  const int64_t b = i / N;
+  const int n = (int)(i - b * N);
+  g[b * ldg + n] = h[b * ldh + n] > 0.f ? dz[b] * wo[n] : 0.f;
+}
+
+// BigDL ReLU backward (Threshold(0, 0)): g *= (h > 0), in place
+__global__ void relu_back_kernel(int B, int N, const float* __restrict__ h, int ldh, float* __restrict__ g,
+                                 int ldg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * N) return;
+  const int64_t b = i / N;
+  const int n = (int)(i - b * N);
+  if (!(h[b * ldh + n] > 0.f)) g[b * ldg + n] = 0.f;
+}
+
+// dL/dE[b][f][j] = dx[b][f*k + j] (+ FM: dz[b] * (s_j - e[b][f][j]) / k), thread per (b, j)
+__global__ void emb_grad_kernel(int B, int F, int k, const float* __restrict__ x, int ldx,
+                                const float* __restrict__ dx, int lddx, const float* __restrict__ dz, int fm,
+                                float* __restrict__ gE) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * k) return;
+  const int64_t b = i / k;
+  const int j = (int)(i - b * k);
+  const float* xr = x + b * ldx;
+  float s = 0.f;
+  if (fm)
+    for (int f = 0; f < F; ++f) s += xr[f * k + j];
+  const float gz = fm ? dz[b] : 0.f;
+  for (int f = 0; f < F; ++f) {
+    float v = dx ? dx[b * lddx + f * k + j] : 0.f;
+    if (fm) v += gz * (s - xr[f * k + j]) / (float)k;
+    gE[(b * F + f) * k + j] = v;
+  }
+}
+
+// Scatter backward: dL/dw[n] = dz[index[n]] (index null: n / F)
+__global__ void w_grad_kernel(int64_t nnz, int F, const int32_t* __restrict__ index, const float* __restrict__ dz,
+                              float* __restrict__ gw) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= nnz) return;
+  gw[n] = dz[index ? index[n] : (int)(n / F)];
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int ensure_train(rmx_model& m, int B) {
+  if (!m.train) m.train = new TrainState();
+  TrainState& T = *m.train;
+  if (!T.blas) {
+    RMX_BLAS(rocblas_create_handle(&T.blas));
+    RMX_BLAS(rocblas_set_pointer_mode(T.blas, rocblas_pointer_mode_host));
+  }
+  if (B <= T.B) return RMX_OK;
+  RMX_HIP(hipDeviceSynchronize());
+  tfree(T.x);
+  for (auto& p : T.h) tfree(p);
+  T.h.clear();
+  tfree(T.g[0]);
+  tfree(T.g[1]);
+  tfree(T.p);
+  tfree(T.dz);
+  tfree(T.ones);
+  if (T.part) (void)hipFree(T.part);
+  T.part = nullptr;
+  int st;
+  T.ldx = m.layers.empty() ? 0 : m.layers[0].Kpad;
+  int maxld = std::max(T.ldx, 16);
+  if (!m.layers.empty() && (st = talloc(&T.x, (size_t)B * T.ldx))) return st;
+  for (auto& L : m.layers) {
+    T.h.push_back(nullptr);
+    if ((st = talloc(&T.h.back(), (size_t)B * L.Npad))) return st;
+    maxld = std::max(maxld, L.Npad);
+  }
+  if (!m.layers.empty()) {
+    if ((st = talloc(&T.g[0], (size_t)B * maxld))) return st;
+    if ((st = talloc(&T.g[1], (size_t)B * maxld))) return st;
+  }
+  if ((st = talloc(&T.p, B)) || (st = talloc(&T.dz, B)) || (st = talloc(&T.ones, B))) return st;
+  if (hipMalloc(&T.part, sizeof(double) * 2 * kMaxParts) != hipSuccess) {
+    set_error("backward: out of device memory");
+    return RMX_E_NOMEM;
+  }
+  hipLaunchKernelGGL(fill_kernel, dim3(nblk(B)), dim3(256), 0, m.ctx->stream, B, 1.0f, T.ones);
+  RMX_HIP(hipGetLastError());
+  T.B = B;
+  return RMX_OK;
+}
+
+// Linear-layer backward on dPre [B][ldd] (N columns) with input x_in [B][ldin] (K columns):
+// dW (N x K row-major, into gW), db (N, into gb, may be null), dx_in = dPre W (into dxin [B][lddx],
+// skipped when null).
+int linear_back(TrainState& T, int B, int N, int K, const float* W, const float* dpre, int ldd, const float* xin,
+                int ldin, float* gW, float* gb, float* dxin, int lddx) {
+  const float one = 1.f, zero = 0.f;
+  RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, K, N, B, &one, xin, ldin, dpre,
+                         ldd, &zero, gW, K));
+  if (gb) RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, dpre, ldd, T.ones, 1, &zero, gb, 1));
+  if (dxin)
+    RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, K, B, N, &one, W, K, dpre, ldd,
+                           &zero, dxin, lddx));
+  return RMX_OK;
+}
+
+}  // namespace
+
+void train_release(rmx_model& m) {
+  if (!m.train) return;
+  TrainState& T = *m.train;
+  (void)hipDeviceSynchronize();
+  tfree(T.x);
+  for (auto& p : T.h) tfree(p);
+  tfree(T.g[0]);
+  tfree(T.g[1]);
+  tfree(T.p);
+  tfree(T.dz);
+  tfree(T.ones);
+  if (T.part) (void)hipFree(T.part);
+  if (T.idx) (void)hipFree(T.idx);
+  if (T.blas) rocblas_destroy_handle(T.blas);
+  delete m.train;
+  m.train = nullptr;
+}
+
+int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOutputs& o) {
+  const int B = in.B;
+  const int t = m.type;
+  if (m.precision != kF32) {
+    set_error("backward: fp32 models only (rmx_model_set_precision(RMX_DTYPE_F32))");
+    return RMX_E_INVALID;
+  }
+  if (t != RMX_MODEL_LR && t != RMX_MODEL_DEEPFM && t != RMX_MODEL_DNN) {
+    set_error("backward: not implemented for this model type yet");
+    return RMX_E_INVALID;
+  }
+  if (B <= 0) return RMX_OK;
+  int st = model_ensure_ws(m, B);  // y12 (first order + FM) lives in the inference workspace
+  if (st) return st;
+  if ((st = ensure_train(m, B))) return st;
+  TrainState& T = *m.train;
+  RMX_BLAS(rocblas_set_stream(T.blas, s));
+  const int F = m.F, k = m.k;
+
+  // ---- forward with stored activations ----
+  if (t == RMX_MODEL_LR) {
+    StageTimer tm(m, s, "first_order_sigmoid");
+    if (in.y1) st = launch_sigmoid_out(s, B, in.y1, in.beta, T.p);
+    else st = launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, T.p);
+    if (st) return st;
+  } else {
+    const float* pre = nullptr;
+    if (t == RMX_MODEL_DEEPFM) {
+      StageTimer tm(m, s, "encoder_fm");
+      if ((st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr,
+                               nullptr)))
+        return st;
+      pre = m.y12;
+    }
+    {
+      StageTimer tm(m, s, "gather_x");
+      if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, in.dtype, T.x, kF32, T.ldx))) return st;
+    }
+    const float* A = T.x;
+    int lda = T.ldx;
+    static const char* names[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
+    for (size_t i = 0; i < m.layers.size(); ++i) {
+      const DenseLayer& L = m.layers[i];
+      StageTimer tm(m, s, names[std::min<size_t>(i, 3)]);
+      if ((st = launch_tower_layer(s, L, B, A, lda, nullptr, T.h[i], L.Npad, Epi::kReluStore, nullptr, nullptr)))
+        return st;
+      A = T.h[i];
+      lda = L.Npad;
+    }
+    OutArgs oa{};
+    oa.wo = m.wo;
+    oa.bo = m.bo;
+    oa.has_bo = m.has_bo ? 1 : 0;
+    oa.pre = pre;
+    oa.beta = in.beta;
+    oa.out = T.p;
+    StageTimer tm(m, s, "tower_head");
+    if ((st = launch_tower_head(s, B, m.layers.back().N, A, lda, oa))) return st;
+  }
+
+  // ---- loss, dL/dz, bias gradient ----
+  {
+    StageTimer tm(m, s, "bce");
+    const int nparts = std::min(kMaxParts, (B + kRedThreads - 1) / kRedThreads);
+    const int per = (B + nparts - 1) / nparts;
+    hipLaunchKernelGGL(bce_kernel, dim3(nparts), dim3(kRedThreads), 0, s, B, T.p, o.targets, T.dz, per, T.part);
+    RMX_HIP(hipGetLastError());
+    float* gbo = (m.has_bo && o.g_mats) ? o.g_mats + m.bo_off : nullptr;  // output Linear bias: same sum
+    hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, nparts, B, T.part, o.loss, o.g_bias, gbo);
+    RMX_HIP(hipGetLastError());
+  }
+  if (o.g_w && t != RMX_MODEL_DNN && o.nnz > 0) {
+    hipLaunchKernelGGL(w_grad_kernel, dim3(nblk(o.nnz)), dim3(256), 0, s, o.nnz, F, o.index, T.dz, o.g_w);
+    RMX_HIP(hipGetLastError());
+  }
+  if (t == RMX_MODEL_LR) return RMX_OK;
+
+  // ---- tower backward ----
+  const float one = 1.f, zero = 0.f;
+  const int nl = (int)m.layers.size();
+  const DenseLayer& last = m.layers.back();
+  {
+    StageTimer tm(m, s, "head_back");
+    if (o.g_mats)
+      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, last.N, B, &one, T.h[nl - 1], last.Npad, T.dz, 1, &zero,
+                             o.g_mats + m.wo_off, 1));
+    hipLaunchKernelGGL(head_back_kernel, dim3(nblk((int64_t)B * last.N)), dim3(256), 0, s, B, last.N, T.h[nl - 1],
+                       last.Npad, T.dz, m.wo, T.g[0], last.Npad);
+    RMX_HIP(hipGetLastError());
+  }
+  int cur = 0;
+  static const char* bnames[] = {"tower_back1", "tower_back2", "tower_back3", "tower_back4+"};
+  for (int l = nl - 1; l >= 0; --l) {
+    const DenseLayer& L = m.layers[l];
+    StageTimer tm(m, s, bnames[std::min(l, 3)]);
+    const float* xin = l == 0 ? T.x : T.h[l - 1];
+    const int ldin = l == 0 ? T.ldx : m.layers[l - 1].Npad;
+    float* dxin = T.g[cur ^ 1];
+    const bool need_dx = l > 0 || o.g_emb;
+    float* gW = o.g_mats ? o.g_mats + L.w_off : nullptr;
+    float* gb = o.g_mats ? o.g_mats + L.b_off : nullptr;
+    if (gW) {
+      if ((st = linear_back(T, B, L.N, L.K, m.mats_dev + L.w_off, T.g[cur], L.Npad, xin, ldin, gW, gb,
+                            need_dx ? dxin : nullptr, ldin)))
+        return st;
+    } else if (need_dx) {
+      RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, L.K, B, L.N, &one,
+                             m.mats_dev + L.w_off, L.K, T.g[cur], L.Npad, &zero, dxin, ldin));
+    }
+    if (l > 0) {
+      const DenseLayer& P = m.layers[l - 1];
+      hipLaunchKernelGGL(relu_back_kernel, dim3(nblk((int64_t)B * P.N)), dim3(256), 0, s, B, P.N, T.h[l - 1], P.Npad,
+                         dxin, P.Npad);
+      RMX_HIP(hipGetLastError());
+    }
+    cur ^= 1;
+  }
+  // ---- embedding gradients (tower + FM) ----
+  if (o.g_emb) {
+    StageTimer tm(m, s, "emb_grad");
+    hipLaunchKernelGGL(emb_grad_kernel, dim3(nblk((int64_t)B * k)), dim3(256), 0, s, B, F, k, T.x, T.ldx, T.g[cur],
+                       T.ldx, T.dz, t == RMX_MODEL_DEEPFM ? 1 : 0, o.g_emb);
+    RMX_HIP(hipGetLastError());
+  }
+  return RMX_OK;
+}
+
+}  // namespace rmx

@@ -382,8 +382,50 @@ class RecModel:
             0 if sizes is None else len(sizes), ptr(fl, ctypes.c_int64), ptr(out, ctypes.c_float)))
         return out
 
-    def backward(self, *args, **kwargs):
-        raise NotImplementedError("backward is out of scope for this round (SURVEY.md §8f rank 1)")
+    def backward(self, batchSize, batch, bias, weights, *rest):
+        """RecModel.backward overloads (RecModel.scala:65-115), targets last:
+        backward(B, batch, bias, weights, targets)
+        backward(B, batch, bias, weights, embeddings, embeddingDim, targets)
+        backward(B, batch, bias, weights, embeddings, embeddingDim, mats, matSizes[, fields], targets)
+        As in the reference, bias / weights / embeddings / mats are overwritten IN PLACE with their
+        gradients (pass contiguous np.float32 arrays); returns the mean BCE loss."""
+        if not rest:
+            raise TypeError("backward: targets missing")
+        targets = np.ascontiguousarray(rest[-1], np.float32)
+        rest = rest[:-1]
+        embeddings = rest[0] if len(rest) > 0 else None
+        embeddingDim = rest[1] if len(rest) > 1 else None
+        mats = rest[2] if len(rest) > 2 else None
+        matSizes = rest[3] if len(rest) > 3 else None
+        fields = rest[4] if len(rest) > 4 else None
+        if not isinstance(batch, CooLongFloatMatrix):
+            batch = CooLongFloatMatrix(*batch)
+        index = batch.getRowIndices()
+        feats = batch.getColIndices()
+        for name, a in (("bias", bias), ("weights", weights), ("embeddings", embeddings), ("mats", mats)):
+            if a is not None and not (isinstance(a, np.ndarray) and a.dtype == np.float32 and a.flags.c_contiguous):
+                raise TypeError("backward writes gradients into %s in place: pass a contiguous np.float32 array"
+                                % name)
+        sizes = None if matSizes is None else np.ascontiguousarray(matSizes, np.int32)
+        fl = None if fields is None else np.ascontiguousarray(fields, np.int64)
+        if embeddingDim is None:
+            embeddingDim = self.getEmbeddingDim()
+        loss = ctypes.c_float()
+        check(_lib.lib.rmx_backward(
+            self._device(), int(batchSize), len(index), ptr(index, ctypes.c_int64), ptr(feats, ctypes.c_int64),
+            ptr(bias, ctypes.c_float), ptr(weights, ctypes.c_float), ptr(embeddings, ctypes.c_float),
+            int(embeddingDim), ptr(mats, ctypes.c_float), ptr(sizes, ctypes.c_int32),
+            0 if sizes is None else len(sizes), ptr(fl, ctypes.c_int64), ptr(targets, ctypes.c_float),
+            ctypes.byref(loss)))
+        return loss.value
+
+    def backward_ids(self, table, batch, ids_dev, targets_dev, g_bias=None, g_weights=None, g_embedding=None,
+                     g_mats=None, loss=None, stream=None):
+        """L-B backward: DeviceArrays for ids [batch*F] int32, targets [batch] and the gradient outputs
+        (g_bias [1], g_weights [batch*F], g_embedding [batch*F*k], g_mats [mats_len], loss [1])."""
+        p = lambda a: None if a is None else a.ptr
+        check(_lib.lib.rmx_backward_ids(self._device(), table.handle, int(batch), ids_dev.ptr, targets_dev.ptr,
+                                        p(g_bias), p(g_weights), p(g_embedding), p(g_mats), p(loss), stream))
 
     # -- device-resident path (replaces ParRecModel.pull* + make*)
     def setMats(self, mats):

@@ -76,6 +76,9 @@ SIGNATURES = [
     ("rmx_table_fill_synthetic", c_int, [c_vp, c_u64]),
     ("rmx_table_rows", c_i64, [c_vp]),
     ("rmx_table_device_ptrs", c_int, [c_vp, P(c_vp), P(c_vp)]),
+    ("rmx_backward", c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp,
+                             c_vp, c_vp]),
+    ("rmx_backward_ids", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_gen_ids", c_int, [c_vp, c_u64, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp]),
     ("rmx_gen_ids_zipf", c_int, [c_vp, c_u64, c_i64, c_i32, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
     ("rmx_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),

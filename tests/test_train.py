@@ -90,3 +90,105 @@ def test_oracle_backward_irregular_lr_index():
     assert np.allclose(g["weights"], gz[index], rtol=1e-6, atol=1e-9)
     assert np.isclose(g["bias"][0], gz.sum(), rtol=1e-6, atol=1e-9)
     assert np.isclose(g["loss"], _bce(p, t), rtol=1e-9)
+
+
+# ------------------------------------------------------------------ GPU ----
+GPU_KINDS = ["lr", "deepfm", "dnn"]
+SEED_IDS, SEED_TAB, SEED_MATS = 0x5EED2026, 0x7AB1E, 0x3A75
+
+
+def _gpu_model(rmx, kind, V, F, K, fc):
+    return {"lr": lambda: rmx.LR(V, F), "deepfm": lambda: rmx.DeepFM(V, F, K, list(fc)),
+            "dnn": lambda: rmx.DNN(V, F, K, list(fc))}[kind]()
+
+
+def _close(got, ref, rel=2e-5):
+    ref = np.asarray(ref, np.float64)
+    return float(np.abs(np.asarray(got, np.float64) - ref).max()) <= rel * max(float(np.abs(ref).max()), 1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", GPU_KINDS)
+@pytest.mark.parametrize("B,fc", [(512, (400, 400, 400)), (37, (24, 8))])
+def test_backward_ids_matches_oracle(kind, B, fc):
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K = 20_000, 39, 16
+    m = _gpu_model(rmx, kind, V, F, K, fc)
+    mats = m.initMats(SEED_MATS) if kind != "lr" else np.zeros(0, np.float32)
+    if kind != "lr":
+        m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 3, B, F, V, ids)
+    tg = (np.random.default_rng(5).random(B) > 0.7).astype(np.float32)
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload(tg)
+    ml = len(mats)
+    g_b = rmx.DeviceArray(ctx, 1, np.float32)
+    g_w = rmx.DeviceArray(ctx, B * F, np.float32)
+    g_e = rmx.DeviceArray(ctx, B * F * K, np.float32)
+    g_m = rmx.DeviceArray(ctx, max(ml, 1), np.float32)
+    loss = rmx.DeviceArray(ctx, 1, np.float32)
+    m.backward_ids(t, B, ids, targets, g_b, g_w, g_e, g_m if ml else None, loss)
+    ctx.sync()
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    h_ids = ids.numpy().astype(np.int64)
+    w, e = oc.gather(wt, et, 1, h_ids)
+    om = oc.make_model(KINDS[kind], F, K, fc=fc if kind != "lr" else ())
+    index = np.repeat(np.arange(B), F).astype(np.int64)
+    ref = oc.backward(om, B, index, np.array([0.01], np.float32), w if kind != "dnn" else None,
+                      e if kind != "lr" else None, mats if kind != "lr" else None, tg)
+    assert abs(loss.numpy()[0] - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    assert _close(g_b.numpy(), ref["bias"])
+    if kind != "dnn":
+        assert _close(g_w.numpy(), ref["weights"])
+    if kind != "lr":
+        assert _close(g_e.numpy(), ref["embedding"])
+        assert _close(g_m.numpy()[:ml], ref["mats"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", GPU_KINDS)
+def test_backward_host_arrays_in_place(kind):
+    """L-A RecModel.backward: the caller's arrays come back holding the gradients."""
+    import rmx
+    B, F, K, fc = 64, 6, 8, (32, 16)
+    rng = np.random.default_rng(11)
+    m = _gpu_model(rmx, kind, 1000, F, K, fc)
+    nnz = B * F
+    index = np.repeat(np.arange(B), F).astype(np.int64)
+    if kind == "lr":  # irregular, unsorted COO rows (Scatter semantics)
+        index = rng.integers(0, B, nnz).astype(np.int64)
+    feats = rng.integers(0, 1000, nnz).astype(np.int64)
+    w = rng.uniform(-0.1, 0.1, nnz).astype(np.float32)
+    e = rng.uniform(-0.1, 0.1, nnz * K).astype(np.float32)
+    mats = m.initMats(7) if kind != "lr" else None
+    bias = np.array([0.02], np.float32)
+    tg = (rng.random(B) > 0.5).astype(np.float32)
+    om = oc.make_model(KINDS[kind], F, K, fc=fc if kind != "lr" else ())
+    ref = oc.backward(om, B, index, bias, w if kind != "dnn" else None, e if kind != "lr" else None, mats, tg)
+    args = [B, (index, feats), bias, w if kind != "dnn" else None]
+    if kind != "lr":
+        args += [e, K, mats, m.getMatsSize()]
+    loss = m.backward(*args, tg)
+    assert abs(loss - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    assert _close(bias, ref["bias"])
+    if kind != "dnn":
+        assert _close(w, ref["weights"])
+    if kind != "lr":
+        assert _close(e, ref["embedding"]) and _close(mats, ref["mats"])
+
+
+@pytest.mark.gpu
+def test_backward_unsupported_raises():
+    import rmx
+    m = rmx.XDeepFM(1000, 4, 16, [8], [4])
+    m.setMats(m.initMats(1))
+    m.setBias(0.0)
+    with pytest.raises(rmx.RmxError):
+        m.backward(2, (np.repeat(np.arange(2), 4), np.arange(8)), np.zeros(1, np.float32),
+                   np.zeros(8, np.float32), np.zeros(8 * 16, np.float32), 16, m.initMats(1), m.getMatsSize(),
+                   np.ones(2, np.float32))
