@@ -482,9 +482,9 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   }
   if (m.type == RMX_MODEL_DCN) {
     const int D = m.F * m.k;
-    if (m.dcn_fused) {
-      // closed-form scalars; the extra GEMM columns use the packed (bf16-rounded for bf16 models)
-      // vectors, so the sums are taken over the same values
+    if (m.cross_depth <= kMaxFusedCross) {
+      // closed-form scalars (the fused forward and the backward); the extra GEMM columns use the
+      // packed (bf16-rounded for bf16 models) vectors, so the sums are taken over the same values
       auto rv = [&](float v) { return m.precision == kBF16 ? bf16_round_host(v) : v; };
       for (int l = 0; l < m.cross_depth; ++l) {
         double ws = 0.0;

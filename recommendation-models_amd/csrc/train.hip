@@ -47,8 +47,13 @@ struct TrainState {
   float* dz = nullptr;          // [B] dL/dlogit
   float* ones = nullptr;        // [B]
   double* part = nullptr;       // [2 * kMaxParts] loss / dz partial sums
-  int64_t cap_idx = 0;
-  int32_t* idx = nullptr;       // L-A index (int32) staging
+  // DCN (cross stack in closed form, k_interact.hip cross_finish_kernel)
+  float* xcol = nullptr;        // [B][L + 1] u_l = w_l . x0, v = W_out[0:D] . x0
+  float* wc = nullptr;          // [L + 1][D] rows w_0 .. w_{L-1}, W_out[0:D]
+  float* coef = nullptr;        // [B][L + 1] x0-coefficients of the cross gradients
+  float* cst = nullptr;         // [B][2L + 1] per-row constants (see cross_back_kernel)
+  float* gwc = nullptr;         // [L + 1][D] gradient of wc before the constant parts
+  float* tmp = nullptr;         // [max(Npad, 2L + 1)] column sums
 };
 
 namespace {
@@ -169,7 +174,93 @@ __global__ void w_grad_kernel(int64_t nnz, int F, const int32_t* __restrict__ in
   gw[n] = dz[index ? index[n] : (int)(n / F)];
 }
 
+// DCN cross stack backward, per row, in the closed form x_l = a_l x0 + c_l 1 (a_0 = 1, c_0 = 0,
+// s_l = w_l . x_l = a_l u_l + c_l sum(w_l), a_{l+1} = a_l + s_l, c_{l+1} = c_l + beta_l;
+// y = a_L v + c_L sum(W_out[0:D])).  With g = dL/dz, going down the stack the gradient of x_l is
+// g W_out + sum_{m >= l} gs_m w_m, where gs_l = g v + sum_{m > l} gs_m u_m (scalar).  Hence
+//   dL/dx0   = g a_L W_out + sum_m gs_m a_m w_m                 -> coef[b] = [gs_0 a_0 .. | g a_L]
+//   dL/dw_m  = sum_b gs_m (a_m x0 + c_m)                         -> coef^T x0 + cst sums
+//   dL/dW_out[0:D] = sum_b g (a_L x0 + c_L)
+//   dL/dbeta_l = sum_b (g sum(W_out) + sum_{m > l} gs_m sum(w_m))
+// cst[b] = [gs_0 c_0 .. gs_{L-1} c_{L-1}, g c_L, gb_0 .. gb_{L-1}]  (summed over b by a GEMV).
+__global__ void cross_back_kernel(int B, int L, const float* __restrict__ xcol, CrossScalars cs,
+                                  const float* __restrict__ dz, float* __restrict__ coef, float* __restrict__ cst) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* u = xcol + (int64_t)b * (L + 1);
+  float a[kMaxFusedCross + 1], c[kMaxFusedCross + 1];
+  a[0] = 1.f;
+  c[0] = 0.f;
+  for (int l = 0; l < L; ++l) {
+    const float sl = a[l] * u[l] + c[l] * cs.wsum[l];
+    a[l + 1] = a[l] + sl;
+    c[l + 1] = c[l] + cs.beta[l];
+  }
+  const float g = dz[b];
+  float* cf = coef + (int64_t)b * (L + 1);
+  float* ct = cst + (int64_t)b * (2 * L + 1);
+  cf[L] = g * a[L];
+  ct[L] = g * c[L];
+  float run = g * u[L];              // g v + sum_{m > l} gs_m u_m
+  float gbr = g * cs.wo_sum;         // g sum(W_out) + sum_{m > l} gs_m sum(w_m)
+  for (int l = L - 1; l >= 0; --l) {
+    const float gs = run;
+    ct[L + 1 + l] = gbr;
+    cf[l] = gs * a[l];
+    ct[l] = gs * c[l];
+    run += gs * u[l];
+    gbr += gs * cs.wsum[l];
+  }
+}
+
+// gwc[r][d] + colsum[r] -> the mats slots: rows < L at w_off + r*D, row L at wo_off
+__global__ void cross_wgrad_kernel(int L, int D, const float* __restrict__ gwc, const float* __restrict__ csum,
+                                   float* __restrict__ gw, float* __restrict__ gwo) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (L + 1) * D) return;
+  const int r = i / D, d = i - r * D;
+  const float v = gwc[i] + csum[r];
+  if (r < L) gw[(int64_t)r * D + d] = v;
+  else gwo[d] = v;
+}
+
+__global__ void copy_kernel(int n, const float* __restrict__ x, float* __restrict__ y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = x[i];
+}
+
+// y[0] = sum_i x[i] (one thread, fixed order)
+__global__ void sum_kernel(int n, const float* __restrict__ x, float* __restrict__ y) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += x[i];
+  *y = (float)s;
+}
+
+// PNN: dL/dE[b][f][j] = dx[b][f*k + j] + sum_{g != f} dip[b][pair(f, g)] * e[b][g][j]
+// (DotProduct2 backward, ProductEncoder.scala:43-70), pairs (i < j) lexicographic.
+__global__ void pnn_emb_grad_kernel(int B, int F, int k, const float* __restrict__ x, int ldx,
+                                    const float* __restrict__ dx, int lddx, float* __restrict__ gE) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * F * k) return;
+  const int64_t b = i / (F * k);
+  const int r = (int)(i - b * F * k), f = r / k, j = r - f * k;
+  const float* xr = x + b * ldx;
+  const float* dip = dx + b * lddx + F * k;
+  float v = dx[b * lddx + r];
+  for (int g = 0; g < F; ++g) {
+    if (g == f) continue;
+    const int lo = f < g ? f : g, hi = f < g ? g : f;
+    const int p = lo * (2 * F - lo - 1) / 2 + (hi - lo - 1);
+    v += dip[p] * xr[g * k + j];
+  }
+  gE[i] = v;
+}
+
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+// output columns of a tower layer that belong to the layer (DCN fused extra columns excluded)
+inline int eff_n(const DenseLayer& L) { return L.N1 >= 0 ? L.N1 : L.N; }
 
 int ensure_train(rmx_model& m, int B) {
   if (!m.train) m.train = new TrainState();
@@ -188,6 +279,12 @@ int ensure_train(rmx_model& m, int B) {
   tfree(T.p);
   tfree(T.dz);
   tfree(T.ones);
+  tfree(T.tmp);
+  tfree(T.xcol);
+  tfree(T.wc);
+  tfree(T.coef);
+  tfree(T.cst);
+  tfree(T.gwc);
   if (T.part) (void)hipFree(T.part);
   T.part = nullptr;
   int st;
@@ -204,6 +301,14 @@ int ensure_train(rmx_model& m, int B) {
     if ((st = talloc(&T.g[1], (size_t)B * maxld))) return st;
   }
   if ((st = talloc(&T.p, B)) || (st = talloc(&T.dz, B)) || (st = talloc(&T.ones, B))) return st;
+  if ((st = talloc(&T.tmp, std::max(maxld, 2 * m.cross_depth + 1)))) return st;
+  if (m.type == RMX_MODEL_DCN) {
+    const int L = m.cross_depth, D = m.F * m.k;
+    if ((st = talloc(&T.xcol, (size_t)B * (L + 1))) || (st = talloc(&T.wc, (size_t)(L + 1) * D)) ||
+        (st = talloc(&T.coef, (size_t)B * (L + 1))) || (st = talloc(&T.cst, (size_t)B * (2 * L + 1))) ||
+        (st = talloc(&T.gwc, (size_t)(L + 1) * D)))
+      return st;
+  }
   if (hipMalloc(&T.part, sizeof(double) * 2 * kMaxParts) != hipSuccess) {
     set_error("backward: out of device memory");
     return RMX_E_NOMEM;
@@ -211,21 +316,6 @@ int ensure_train(rmx_model& m, int B) {
   hipLaunchKernelGGL(fill_kernel, dim3(nblk(B)), dim3(256), 0, m.ctx->stream, B, 1.0f, T.ones);
   RMX_HIP(hipGetLastError());
   T.B = B;
-  return RMX_OK;
-}
-
-// Linear-layer backward on dPre [B][ldd] (N columns) with input x_in [B][ldin] (K columns):
-// dW (N x K row-major, into gW), db (N, into gb, may be null), dx_in = dPre W (into dxin [B][lddx],
-// skipped when null).
-int linear_back(TrainState& T, int B, int N, int K, const float* W, const float* dpre, int ldd, const float* xin,
-                int ldin, float* gW, float* gb, float* dxin, int lddx) {
-  const float one = 1.f, zero = 0.f;
-  RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, K, N, B, &one, xin, ldin, dpre,
-                         ldd, &zero, gW, K));
-  if (gb) RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, dpre, ldd, T.ones, 1, &zero, gb, 1));
-  if (dxin)
-    RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, K, B, N, &one, W, K, dpre, ldd,
-                           &zero, dxin, lddx));
   return RMX_OK;
 }
 
@@ -242,8 +332,13 @@ void train_release(rmx_model& m) {
   tfree(T.p);
   tfree(T.dz);
   tfree(T.ones);
+  tfree(T.tmp);
+  tfree(T.xcol);
+  tfree(T.wc);
+  tfree(T.coef);
+  tfree(T.cst);
+  tfree(T.gwc);
   if (T.part) (void)hipFree(T.part);
-  if (T.idx) (void)hipFree(T.idx);
   if (T.blas) rocblas_destroy_handle(T.blas);
   delete m.train;
   m.train = nullptr;
@@ -256,8 +351,12 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     set_error("backward: fp32 models only (rmx_model_set_precision(RMX_DTYPE_F32))");
     return RMX_E_INVALID;
   }
-  if (t != RMX_MODEL_LR && t != RMX_MODEL_DEEPFM && t != RMX_MODEL_DNN) {
-    set_error("backward: not implemented for this model type yet");
+  if (t == RMX_MODEL_XDEEPFM) {
+    set_error("backward: not implemented for xDeepFM yet");
+    return RMX_E_INVALID;
+  }
+  if (t == RMX_MODEL_DCN && m.cross_depth > kMaxFusedCross) {
+    set_error("backward: DCN crossDepth must be <= " + std::to_string(kMaxFusedCross));
     return RMX_E_INVALID;
   }
   if (B <= 0) return RMX_OK;
@@ -266,7 +365,8 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   if ((st = ensure_train(m, B))) return st;
   TrainState& T = *m.train;
   RMX_BLAS(rocblas_set_stream(T.blas, s));
-  const int F = m.F, k = m.k;
+  const int F = m.F, k = m.k, D = F * k, Lc = m.cross_depth;
+  const float one = 1.f, zero = 0.f;
 
   // ---- forward with stored activations ----
   if (t == RMX_MODEL_LR) {
@@ -282,8 +382,19 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
                                nullptr)))
         return st;
       pre = m.y12;
+    } else if (t != RMX_MODEL_DNN) {
+      if (!in.y1) {
+        StageTimer tm(m, s, "first_order");
+        if ((st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr)))
+          return st;
+      }
+      pre = m.y12;
     }
-    {
+    if (t == RMX_MODEL_PNN) {
+      StageTimer tm(m, s, "product");
+      if ((st = launch_product(s, B, F, k, in.ids, in.table, in.dtype, m.pairs, F * (F - 1) / 2, T.x, kF32, T.ldx)))
+        return st;
+    } else {
       StageTimer tm(m, s, "gather_x");
       if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, in.dtype, T.x, kF32, T.ldx))) return st;
     }
@@ -293,12 +404,26 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     for (size_t i = 0; i < m.layers.size(); ++i) {
       const DenseLayer& L = m.layers[i];
       StageTimer tm(m, s, names[std::min<size_t>(i, 3)]);
-      if ((st = launch_tower_layer(s, L, B, A, lda, nullptr, T.h[i], L.Npad, Epi::kReluStore, nullptr, nullptr)))
+      XColArgs xc{T.xcol, L.N1, Lc + 1};
+      const bool fused = i == 0 && m.dcn_fused;
+      if ((st = launch_tower_layer(s, L, B, A, lda, nullptr, T.h[i], L.Npad, Epi::kReluStore, nullptr,
+                                   fused ? &xc : nullptr)))
         return st;
       A = T.h[i];
       lda = L.Npad;
     }
     OutArgs oa{};
+    if (t == RMX_MODEL_DCN) {
+      StageTimer tm(m, s, "cross");
+      // wc = [w_0 .. w_{L-1}; W_out[0:D]]; the unfused case gets u / v from one GEMM
+      RMX_HIP(hipMemcpyAsync(T.wc, m.cross_w, sizeof(float) * Lc * D, hipMemcpyDeviceToDevice, s));
+      RMX_HIP(hipMemcpyAsync(T.wc + (int64_t)Lc * D, m.wo_x, sizeof(float) * D, hipMemcpyDeviceToDevice, s));
+      if (!m.dcn_fused)
+        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_transpose, rocblas_operation_none, Lc + 1, B, D, &one, T.wc,
+                               D, T.x, T.ldx, &zero, T.xcol, Lc + 1));
+      if ((st = launch_cross_finish(s, B, Lc, T.xcol, m.cross_scalars, m.pre2))) return st;
+      oa.pre2 = m.pre2;
+    }
     oa.wo = m.wo;
     oa.bo = m.bo;
     oa.has_bo = m.has_bo ? 1 : 0;
@@ -306,7 +431,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     oa.beta = in.beta;
     oa.out = T.p;
     StageTimer tm(m, s, "tower_head");
-    if ((st = launch_tower_head(s, B, m.layers.back().N, A, lda, oa))) return st;
+    if ((st = launch_tower_head(s, B, eff_n(m.layers.back()), A, lda, oa))) return st;
   }
 
   // ---- loss, dL/dz, bias gradient ----
@@ -327,50 +452,98 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   if (t == RMX_MODEL_LR) return RMX_OK;
 
   // ---- tower backward ----
-  const float one = 1.f, zero = 0.f;
   const int nl = (int)m.layers.size();
-  const DenseLayer& last = m.layers.back();
   {
+    const DenseLayer& last = m.layers.back();
+    const int N = eff_n(last);
     StageTimer tm(m, s, "head_back");
     if (o.g_mats)
-      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, last.N, B, &one, T.h[nl - 1], last.Npad, T.dz, 1, &zero,
+      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, T.h[nl - 1], last.Npad, T.dz, 1, &zero,
                              o.g_mats + m.wo_off, 1));
-    hipLaunchKernelGGL(head_back_kernel, dim3(nblk((int64_t)B * last.N)), dim3(256), 0, s, B, last.N, T.h[nl - 1],
-                       last.Npad, T.dz, m.wo, T.g[0], last.Npad);
+    hipLaunchKernelGGL(head_back_kernel, dim3(nblk((int64_t)B * N)), dim3(256), 0, s, B, N, T.h[nl - 1], last.Npad,
+                       T.dz, m.wo, T.g[0], last.Npad);
     RMX_HIP(hipGetLastError());
   }
   int cur = 0;
   static const char* bnames[] = {"tower_back1", "tower_back2", "tower_back3", "tower_back4+"};
   for (int l = nl - 1; l >= 0; --l) {
     const DenseLayer& L = m.layers[l];
+    const int N = eff_n(L);
     StageTimer tm(m, s, bnames[std::min(l, 3)]);
     const float* xin = l == 0 ? T.x : T.h[l - 1];
     const int ldin = l == 0 ? T.ldx : m.layers[l - 1].Npad;
+    const float* dpre = T.g[cur];
     float* dxin = T.g[cur ^ 1];
-    const bool need_dx = l > 0 || o.g_emb;
-    float* gW = o.g_mats ? o.g_mats + L.w_off : nullptr;
-    float* gb = o.g_mats ? o.g_mats + L.b_off : nullptr;
-    if (gW) {
-      if ((st = linear_back(T, B, L.N, L.K, m.mats_dev + L.w_off, T.g[cur], L.Npad, xin, ldin, gW, gb,
-                            need_dx ? dxin : nullptr, ldin)))
-        return st;
-    } else if (need_dx) {
-      RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, L.K, B, L.N, &one,
-                             m.mats_dev + L.w_off, L.K, T.g[cur], L.Npad, &zero, dxin, ldin));
+    const bool need_dx = l > 0 || o.g_emb || t == RMX_MODEL_DCN;
+    // Linear blocks of this layer: (column range of x_in, W offset); PNN layer 1 = Linear(x) + Linear(ip)
+    struct Blk { int c0, K; int64_t w; };
+    Blk blks[2] = {{0, L.K, L.w_off}, {0, 0, -1}};
+    int nb = 1;
+    if (L.K1 >= 0) {
+      blks[0] = {0, L.K1, L.w_off};
+      blks[1] = {L.K1, L.K - L.K1, L.w_off2};
+      nb = 2;
+    }
+    for (int q = 0; q < nb; ++q) {
+      const Blk& bk = blks[q];
+      if (o.g_mats)
+        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, bk.K, N, B, &one,
+                               xin + bk.c0, ldin, dpre, L.Npad, &zero, o.g_mats + bk.w, bk.K));
+      if (need_dx)
+        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, bk.K, B, N, &one,
+                               m.mats_dev + bk.w, bk.K, dpre, L.Npad, &zero, dxin + bk.c0, ldin));
+    }
+    if (o.g_mats && L.bias_mode == 1)
+      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, dpre, L.Npad, T.ones, 1, &zero,
+                             o.g_mats + L.b_off, 1));
+    if (o.g_mats && L.bias_mode == 2) {  // one CAdd(1) scalar over all outputs
+      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, dpre, L.Npad, T.ones, 1, &zero, T.tmp, 1));
+      hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(64), 0, s, N, T.tmp, o.g_mats + L.b_off);
+      RMX_HIP(hipGetLastError());
     }
     if (l > 0) {
       const DenseLayer& P = m.layers[l - 1];
-      hipLaunchKernelGGL(relu_back_kernel, dim3(nblk((int64_t)B * P.N)), dim3(256), 0, s, B, P.N, T.h[l - 1], P.Npad,
+      const int PN = eff_n(P);
+      hipLaunchKernelGGL(relu_back_kernel, dim3(nblk((int64_t)B * PN)), dim3(256), 0, s, B, PN, T.h[l - 1], P.Npad,
                          dxin, P.Npad);
       RMX_HIP(hipGetLastError());
     }
     cur ^= 1;
   }
-  // ---- embedding gradients (tower + FM) ----
+  float* dX = T.g[cur];  // dL/d(tower input) [B][ldx]
+
+  // ---- DCN cross stack (closed form), adds into dX ----
+  if (t == RMX_MODEL_DCN) {
+    StageTimer tm(m, s, "cross_back");
+    hipLaunchKernelGGL(cross_back_kernel, dim3(nblk(B)), dim3(256), 0, s, B, Lc, T.xcol, m.cross_scalars, T.dz,
+                       T.coef, T.cst);
+    RMX_HIP(hipGetLastError());
+    // dX += coef [B][L+1] . wc [L+1][D]
+    RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, D, B, Lc + 1, &one, T.wc, D,
+                           T.coef, Lc + 1, &one, dX, T.ldx));
+    if (o.g_mats) {
+      // gwc = coef^T x0 ; + the per-row constants summed over the batch ; beta_l sums
+      RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, D, Lc + 1, B, &one, T.x,
+                             T.ldx, T.coef, Lc + 1, &zero, T.gwc, D));
+      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, 2 * Lc + 1, B, &one, T.cst, 2 * Lc + 1, T.ones, 1,
+                             &zero, T.tmp, 1));
+      hipLaunchKernelGGL(cross_wgrad_kernel, dim3(nblk((int64_t)(Lc + 1) * D)), dim3(256), 0, s, Lc, D, T.gwc, T.tmp,
+                         o.g_mats + m.cross_w_off, o.g_mats + m.wo_x_off);
+      RMX_HIP(hipGetLastError());
+      hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, s, Lc, T.tmp + Lc + 1, o.g_mats + m.cross_b_off);
+      RMX_HIP(hipGetLastError());
+    }
+  }
+
+  // ---- embedding gradients ----
   if (o.g_emb) {
     StageTimer tm(m, s, "emb_grad");
-    hipLaunchKernelGGL(emb_grad_kernel, dim3(nblk((int64_t)B * k)), dim3(256), 0, s, B, F, k, T.x, T.ldx, T.g[cur],
-                       T.ldx, T.dz, t == RMX_MODEL_DEEPFM ? 1 : 0, o.g_emb);
+    if (t == RMX_MODEL_PNN)
+      hipLaunchKernelGGL(pnn_emb_grad_kernel, dim3(nblk((int64_t)B * D)), dim3(256), 0, s, B, F, k, T.x, T.ldx, dX,
+                         T.ldx, o.g_emb);
+    else
+      hipLaunchKernelGGL(emb_grad_kernel, dim3(nblk((int64_t)B * k)), dim3(256), 0, s, B, F, k, T.x, T.ldx, dX,
+                         T.ldx, T.dz, t == RMX_MODEL_DEEPFM ? 1 : 0, o.g_emb);
     RMX_HIP(hipGetLastError());
   }
   return RMX_OK;
