@@ -54,6 +54,16 @@ struct TrainState {
   float* cst = nullptr;         // [B][2L + 1] per-row constants (see cross_back_kernel)
   float* gwc = nullptr;         // [L + 1][D] gradient of wc before the constant parts
   float* tmp = nullptr;         // [max(Npad, 2L + 1)] column sums
+  // xDeepFM CIN (rows r = b*k + j, R = B*k)
+  std::vector<float*> u;        // [R][Npad_l] maps of every CIN layer
+  float* x0 = nullptr;          // [R][F] x0[b*k + j][f] = e[b][f][j]
+  float* gx0 = nullptr;         // [R][F] dL/dx0 (CIN part)
+  float* gu[2] = {nullptr, nullptr};  // [R][maxNpad] dL/du of the layer below (from the layer above)
+  float* gpre = nullptr;        // [R][maxNpad] dL/d(pre-activation) of the current layer
+  float* dzr = nullptr;         // [R] dz[r / k]
+  float* zb = nullptr;          // [rc][max F*Hp] Z = x0 (x) u_prev chunk, then its gradient
+  float* onesR = nullptr;       // [R]
+  int rc = 0;                   // rows per chunk (a multiple of k)
 };
 
 namespace {
@@ -149,7 +159,7 @@ __global__ void relu_back_kernel(int B, int N, const float* __restrict__ h, int 
 // dL/dE[b][f][j] = dx[b][f*k + j] (+ FM: dz[b] * (s_j - e[b][f][j]) / k), thread per (b, j)
 __global__ void emb_grad_kernel(int B, int F, int k, const float* __restrict__ x, int ldx,
                                 const float* __restrict__ dx, int lddx, const float* __restrict__ dz, int fm,
-                                float* __restrict__ gE) {
+                                const float* __restrict__ gx0, float* __restrict__ gE) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)B * k) return;
   const int64_t b = i / k;
@@ -162,6 +172,7 @@ __global__ void emb_grad_kernel(int B, int F, int k, const float* __restrict__ x
   for (int f = 0; f < F; ++f) {
     float v = dx ? dx[b * lddx + f * k + j] : 0.f;
     if (fm) v += gz * (s - xr[f * k + j]) / (float)k;
+    if (gx0) v += gx0[(b * k + j) * F + f];  // xDeepFM: CIN part (x0[b*k + j][f] = e[b][f][j])
     gE[(b * F + f) * k + j] = v;
   }
 }
@@ -257,6 +268,75 @@ __global__ void pnn_emb_grad_kernel(int B, int F, int k, const float* __restrict
   gE[i] = v;
 }
 
+// ---- xDeepFM CIN backward (CINEncoder.scala:60-103; forward semantics in k_gemm.hip) ----
+__global__ void cin_x0_kernel(int B, int F, int k, const float* __restrict__ x, int ldx, float* __restrict__ x0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)B * k * F) return;
+  const int64_t r = i / F;
+  const int f = (int)(i - r * F);
+  const int64_t b = r / k;
+  const int j = (int)(r - b * k);
+  x0[i] = x[b * ldx + f * k + j];
+}
+
+__global__ void expand_dz_kernel(int64_t R, int k, const float* __restrict__ dz, float* __restrict__ dzr) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) dzr[r] = dz[r / k];
+}
+
+// gpre[r][h] = ReLU'(u_l) * (gu[r][h] (from layer l+1) + dz[b] * W_out[slice_l + h] (pooling: Sum over k))
+__global__ void cin_gpre_kernel(int64_t R, int H, int k, const float* __restrict__ u, int ldu,
+                                const float* __restrict__ gu, const float* __restrict__ dz,
+                                const float* __restrict__ wo, float* __restrict__ gpre) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R * H) return;
+  const int64_t r = i / H;
+  const int h = (int)(i - r * H);
+  float g = dz[r / k] * wo[h];
+  if (gu) g += gu[r * ldu + h];
+  gpre[r * ldu + h] = u[r * ldu + h] > 0.f ? g : 0.f;
+}
+
+// z[r][f*Hp + h] = x0[r][f] * up[r][h]  (MM(transB) of (F x 1)(1 x Hp), CINEncoder.scala:152)
+__global__ void cin_z_kernel(int64_t rows, int F, int Hp, const float* __restrict__ x0,
+                             const float* __restrict__ up, int ldu, float* __restrict__ z) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int FH = F * Hp;
+  if (i >= rows * FH) return;
+  const int64_t r = i / FH;
+  const int c = (int)(i - r * FH), f = c / Hp, h = c - f * Hp;
+  z[i] = x0[r * F + f] * up[r * ldu + h];
+}
+
+// gx0[r][f] += sum_h gz[r][f*Hp + h] * up[r][h]
+__global__ void cin_back_x0_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
+                                   const float* __restrict__ up, int ldu, float* __restrict__ gx0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * F) return;
+  const int64_t r = i / F;
+  const int f = (int)(i - r * F);
+  const float* g = gz + r * (int64_t)F * Hp + (int64_t)f * Hp;
+  const float* uu = up + r * ldu;
+  float acc = 0.f;
+  for (int h = 0; h < Hp; ++h) acc += g[h] * uu[h];
+  gx0[i] += acc;
+}
+
+// out[r][h] (=, or += when accum) sum_f gz[r][f*Hp + h] * x0[r][f]
+__global__ void cin_back_u_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
+                                  const float* __restrict__ x0, float* __restrict__ out, int ldo, int accum) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * Hp) return;
+  const int64_t r = i / Hp;
+  const int h = (int)(i - r * Hp);
+  const float* g = gz + r * (int64_t)F * Hp + h;
+  const float* xr = x0 + r * F;
+  float acc = 0.f;
+  for (int f = 0; f < F; ++f) acc += g[(int64_t)f * Hp] * xr[f];
+  if (accum) out[r * ldo + h] += acc;
+  else out[r * ldo + h] = acc;
+}
+
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 // output columns of a tower layer that belong to the layer (DCN fused extra columns excluded)
@@ -285,6 +365,16 @@ int ensure_train(rmx_model& m, int B) {
   tfree(T.coef);
   tfree(T.cst);
   tfree(T.gwc);
+  for (auto& p : T.u) tfree(p);
+  T.u.clear();
+  tfree(T.x0);
+  tfree(T.gx0);
+  tfree(T.gu[0]);
+  tfree(T.gu[1]);
+  tfree(T.gpre);
+  tfree(T.dzr);
+  tfree(T.zb);
+  tfree(T.onesR);
   if (T.part) (void)hipFree(T.part);
   T.part = nullptr;
   int st;
@@ -302,6 +392,27 @@ int ensure_train(rmx_model& m, int B) {
   }
   if ((st = talloc(&T.p, B)) || (st = talloc(&T.dz, B)) || (st = talloc(&T.ones, B))) return st;
   if ((st = talloc(&T.tmp, std::max(maxld, 2 * m.cross_depth + 1)))) return st;
+  if (m.type == RMX_MODEL_XDEEPFM) {
+    const int64_t R = (int64_t)B * m.k;
+    int maxH = 16, maxFH = 16;
+    for (auto& c : m.cin_layers) {
+      maxH = std::max(maxH, c.Npad);
+      maxFH = std::max(maxFH, m.F * c.Hp);
+    }
+    for (auto& c : m.cin_layers) {
+      T.u.push_back(nullptr);
+      if ((st = talloc(&T.u.back(), (size_t)R * c.Npad))) return st;
+    }
+    const int64_t budget = 64ll << 20;  // floats of the Z chunk (256 MB)
+    T.rc = (int)std::min<int64_t>(R, std::max<int64_t>(m.k, budget / maxFH / m.k * m.k));
+    if ((st = talloc(&T.x0, (size_t)R * m.F)) || (st = talloc(&T.gx0, (size_t)R * m.F)) ||
+        (st = talloc(&T.gu[0], (size_t)R * maxH)) || (st = talloc(&T.gu[1], (size_t)R * maxH)) ||
+        (st = talloc(&T.gpre, (size_t)R * maxH)) || (st = talloc(&T.dzr, R)) ||
+        (st = talloc(&T.zb, (size_t)T.rc * maxFH)) || (st = talloc(&T.onesR, R)))
+      return st;
+    hipLaunchKernelGGL(fill_kernel, dim3(nblk(R)), dim3(256), 0, m.ctx->stream, (int)R, 1.0f, T.onesR);
+    RMX_HIP(hipGetLastError());
+  }
   if (m.type == RMX_MODEL_DCN) {
     const int L = m.cross_depth, D = m.F * m.k;
     if ((st = talloc(&T.xcol, (size_t)B * (L + 1))) || (st = talloc(&T.wc, (size_t)(L + 1) * D)) ||
@@ -338,6 +449,15 @@ void train_release(rmx_model& m) {
   tfree(T.coef);
   tfree(T.cst);
   tfree(T.gwc);
+  for (auto& p : T.u) tfree(p);
+  tfree(T.x0);
+  tfree(T.gx0);
+  tfree(T.gu[0]);
+  tfree(T.gu[1]);
+  tfree(T.gpre);
+  tfree(T.dzr);
+  tfree(T.zb);
+  tfree(T.onesR);
   if (T.part) (void)hipFree(T.part);
   if (T.blas) rocblas_destroy_handle(T.blas);
   delete m.train;
@@ -349,10 +469,6 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   const int t = m.type;
   if (m.precision != kF32) {
     set_error("backward: fp32 models only (rmx_model_set_precision(RMX_DTYPE_F32))");
-    return RMX_E_INVALID;
-  }
-  if (t == RMX_MODEL_XDEEPFM) {
-    set_error("backward: not implemented for xDeepFM yet");
     return RMX_E_INVALID;
   }
   if (t == RMX_MODEL_DCN && m.cross_depth > kMaxFusedCross) {
@@ -398,6 +514,17 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       StageTimer tm(m, s, "gather_x");
       if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, in.dtype, T.x, kF32, T.ldx))) return st;
     }
+    if (t == RMX_MODEL_XDEEPFM) {
+      const float* uprev = nullptr;
+      for (size_t l = 0; l < m.cin_layers.size(); ++l) {
+        StageTimer tm(m, s, l == 0 ? "cin_layer1" : (l == 1 ? "cin_layer2" : "cin_layer3+"));
+        // last = false: every layer's maps are stored (the backward needs them)
+        if ((st = launch_cin_layer(s, m.cin_layers[l], l == 0, false, B, F, k, in.ids, (const float*)in.table, uprev,
+                                   T.u[l], m.rowdot)))
+          return st;
+        uprev = T.u[l];
+      }
+    }
     const float* A = T.x;
     int lda = T.ldx;
     static const char* names[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
@@ -423,6 +550,10 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
                                D, T.x, T.ldx, &zero, T.xcol, Lc + 1));
       if ((st = launch_cross_finish(s, B, Lc, T.xcol, m.cross_scalars, m.pre2))) return st;
       oa.pre2 = m.pre2;
+    }
+    if (t == RMX_MODEL_XDEEPFM) {
+      oa.rowsum = m.rowdot;
+      oa.rowsum_k = k;
     }
     oa.wo = m.wo;
     oa.bo = m.bo;
@@ -535,6 +666,59 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     }
   }
 
+  // ---- xDeepFM CIN stack: gradients of C_l, c_l, W_out[pool slices] and dL/dx0 ----
+  if (t == RMX_MODEL_XDEEPFM) {
+    const int64_t R = (int64_t)B * k;
+    StageTimer tm(m, s, "cin_back");
+    hipLaunchKernelGGL(cin_x0_kernel, dim3(nblk(R * F)), dim3(256), 0, s, B, F, k, T.x, T.ldx, T.x0);
+    RMX_HIP(hipGetLastError());
+    hipLaunchKernelGGL(expand_dz_kernel, dim3(nblk(R)), dim3(256), 0, s, R, k, T.dz, T.dzr);
+    RMX_HIP(hipGetLastError());
+    RMX_HIP(hipMemsetAsync(T.gx0, 0, sizeof(float) * R * F, s));
+    const int nc = (int)m.cin_layers.size();
+    int gcur = 0;
+    for (int l = nc - 1; l >= 0; --l) {
+      const CinLayer& c = m.cin_layers[l];
+      const int H = c.H, Hp = c.Hp, FH = F * Hp, ldu = c.Npad;
+      const float* up = l == 0 ? T.x0 : T.u[l - 1];
+      const int ldup = l == 0 ? F : m.cin_layers[l - 1].Npad;
+      hipLaunchKernelGGL(cin_gpre_kernel, dim3(nblk(R * H)), dim3(256), 0, s, R, H, k, T.u[l], ldu,
+                         l == nc - 1 ? nullptr : T.gu[gcur], T.dz, c.wo, T.gpre);
+      RMX_HIP(hipGetLastError());
+      if (o.g_mats) {
+        // pooled slice of W_out: sum_r dz[b] u_l[r][h]; bias c_l: sum_r gpre[r][h]
+        RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, H, (int)R, &one, T.u[l], ldu, T.dzr, 1, &zero,
+                               o.g_mats + c.wo_off, 1));
+        RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, H, (int)R, &one, T.gpre, ldu, T.onesR, 1, &zero,
+                               o.g_mats + c.b_off, 1));
+      }
+      for (int64_t r0 = 0; r0 < R; r0 += T.rc) {
+        const int rows = (int)std::min<int64_t>(T.rc, R - r0);
+        const float* gp = T.gpre + r0 * ldu;
+        if (o.g_mats) {
+          hipLaunchKernelGGL(cin_z_kernel, dim3(nblk((int64_t)rows * FH)), dim3(256), 0, s, (int64_t)rows, F, Hp,
+                             T.x0 + r0 * F, up + r0 * ldup, ldup, T.zb);
+          RMX_HIP(hipGetLastError());
+          const float beta = r0 == 0 ? 0.f : 1.f;
+          RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, FH, H, rows, &one, T.zb,
+                                 FH, gp, ldu, &beta, o.g_mats + c.w_off, FH));
+        }
+        // dL/dz for this chunk: gpre . C_l  [rows][F*Hp]
+        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, FH, rows, H, &one,
+                               m.mats_dev + c.w_off, FH, gp, ldu, &zero, T.zb, FH));
+        hipLaunchKernelGGL(cin_back_x0_kernel, dim3(nblk((int64_t)rows * F)), dim3(256), 0, s, (int64_t)rows, F, Hp,
+                           T.zb, up + r0 * ldup, ldup, T.gx0 + r0 * F);
+        RMX_HIP(hipGetLastError());
+        // through u_{l-1} (layer 0: u_0 = x0, so into gx0 as well)
+        float* gout = l == 0 ? T.gx0 + r0 * F : T.gu[gcur ^ 1] + r0 * m.cin_layers[l - 1].Npad;
+        hipLaunchKernelGGL(cin_back_u_kernel, dim3(nblk((int64_t)rows * Hp)), dim3(256), 0, s, (int64_t)rows, F, Hp,
+                           T.zb, T.x0 + r0 * F, gout, l == 0 ? F : m.cin_layers[l - 1].Npad, l == 0 ? 1 : 0);
+        RMX_HIP(hipGetLastError());
+      }
+      gcur ^= 1;
+    }
+  }
+
   // ---- embedding gradients ----
   if (o.g_emb) {
     StageTimer tm(m, s, "emb_grad");
@@ -543,7 +727,8 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
                          T.ldx, o.g_emb);
     else
       hipLaunchKernelGGL(emb_grad_kernel, dim3(nblk((int64_t)B * k)), dim3(256), 0, s, B, F, k, T.x, T.ldx, dX,
-                         T.ldx, T.dz, t == RMX_MODEL_DEEPFM ? 1 : 0, o.g_emb);
+                         T.ldx, T.dz, t == RMX_MODEL_DEEPFM ? 1 : 0, t == RMX_MODEL_XDEEPFM ? T.gx0 : nullptr,
+                       o.g_emb);
     RMX_HIP(hipGetLastError());
   }
   return RMX_OK;

@@ -93,7 +93,8 @@ def test_oracle_backward_irregular_lr_index():
 
 
 # ------------------------------------------------------------------ GPU ----
-GPU_KINDS = ["lr", "deepfm", "dnn", "dcn", "pnn"]
+GPU_KINDS = ["lr", "deepfm", "dnn", "dcn", "pnn", "xdeepfm"]
+CIN_FOR = {(400, 400, 400): (64, 32), (24, 8): (8, 4), (16,): (16,), (32, 16): (8, 4)}
 SEED_IDS, SEED_TAB, SEED_MATS = 0x5EED2026, 0x7AB1E, 0x3A75
 CROSS = 3
 
@@ -101,11 +102,13 @@ CROSS = 3
 def _gpu_model(rmx, kind, V, F, K, fc):
     return {"lr": lambda: rmx.LR(V, F), "deepfm": lambda: rmx.DeepFM(V, F, K, list(fc)),
             "dnn": lambda: rmx.DNN(V, F, K, list(fc)), "dcn": lambda: rmx.DCN(V, F, K, CROSS, list(fc)),
-            "pnn": lambda: rmx.PNN(V, F, K, list(fc))}[kind]()
+            "pnn": lambda: rmx.PNN(V, F, K, list(fc)),
+            "xdeepfm": lambda: rmx.XDeepFM(V, F, K, list(fc), list(CIN_FOR[tuple(fc)]))}[kind]()
 
 
 def _orc_model(kind, F, K, fc):
-    return oc.make_model(KINDS[kind], F, K, fc=fc if kind != "lr" else (), cross_depth=CROSS if kind == "dcn" else 0)
+    return oc.make_model(KINDS[kind], F, K, fc=fc if kind != "lr" else (), cross_depth=CROSS if kind == "dcn" else 0,
+                         cin=CIN_FOR[tuple(fc)] if kind == "xdeepfm" else ())
 
 
 
@@ -140,6 +143,14 @@ def _hidden_pre(kind, E, mats, fc):
         pre = x @ mats[off:off + K_ * d].reshape(d, K_).T + mats[off + K_ * d:off + K_ * d + d]
         pres.append(pre)
         x, off = np.maximum(pre, 0), off + K_ * d + d
+    if kind == "xdeepfm":  # CIN maps, rows (b, j) regrouped per sample
+        x0 = E.transpose(0, 2, 1).reshape(B * k, F)
+        u, hp = x0, F
+        for h in CIN_FOR[tuple(fc)]:
+            Z = (x0[:, :, None] * u[:, None, :]).reshape(B * k, F * hp)
+            pre = Z @ mats[off:off + F * hp * h].reshape(h, F * hp).T + mats[off + F * hp * h:off + F * hp * h + h]
+            pres.append(pre.reshape(B, k * h))
+            u, off, hp = np.maximum(pre, 0), off + F * hp * h + h, h
     return pres
 
 
@@ -208,6 +219,8 @@ def test_backward_host_arrays_in_place(kind):
     """L-A RecModel.backward: the caller's arrays come back holding the gradients."""
     import rmx
     B, F, K, fc = 64, 6, 8, (32, 16)
+    if kind == "xdeepfm":
+        K = 16  # the CIN kernel's embedding dim
     rng = np.random.default_rng(11)
     m = _gpu_model(rmx, kind, 1000, F, K, fc)
     nnz = B * F
@@ -236,11 +249,19 @@ def test_backward_host_arrays_in_place(kind):
 
 @pytest.mark.gpu
 def test_backward_unsupported_raises():
+    """bf16 models and DCN stacks deeper than the closed form's 8 layers are rejected loudly."""
     import rmx
-    m = rmx.XDeepFM(1000, 4, 16, [8], [4])
+    m = rmx.DeepFM(1000, 4, 16, [8])
+    m.setPrecision(rmx.DTYPE_BF16)
     m.setMats(m.initMats(1))
     m.setBias(0.0)
+    args = (2, (np.repeat(np.arange(2), 4), np.arange(8)), np.zeros(1, np.float32), np.zeros(8, np.float32),
+            np.zeros(8 * 16, np.float32), 16, m.initMats(1), m.getMatsSize(), np.ones(2, np.float32))
     with pytest.raises(rmx.RmxError):
-        m.backward(2, (np.repeat(np.arange(2), 4), np.arange(8)), np.zeros(1, np.float32),
-                   np.zeros(8, np.float32), np.zeros(8 * 16, np.float32), 16, m.initMats(1), m.getMatsSize(),
-                   np.ones(2, np.float32))
+        m.backward(*args)
+    d = rmx.DCN(1000, 4, 16, 9, [8])
+    d.setMats(d.initMats(1))
+    d.setBias(0.0)
+    with pytest.raises(rmx.RmxError):
+        d.backward(2, (np.repeat(np.arange(2), 4), np.arange(8)), np.zeros(1, np.float32), np.zeros(8, np.float32),
+                   np.zeros(8 * 16, np.float32), 16, d.initMats(1), d.getMatsSize(), np.ones(2, np.float32))
