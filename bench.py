@@ -40,7 +40,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded", "dcn_bf16", "pnn_bf16"],
+    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded", "dcn_bf16", "pnn_bf16",
+                                           "deepfm_train", "xdeepfm_train"],
                     default="deepfm")
     ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
@@ -68,6 +69,18 @@ def stage_work(workload, stage, B):
     if stage == "product":  # ids + rows + the [x | ip] row written
         return "byte", B * (F * 4 + F * K * es + (D + P) * es)
     k1 = D + P if workload.startswith("pnn") else D
+    # backward (the *_train workloads): dW and dX GEMMs of every Linear, 2 x 2 B K N
+    if stage == "tower_back1":
+        return "flop", 4.0 * B * k1 * FC[0]
+    if stage == "tower_back2":
+        return "flop", 4.0 * B * FC[0] * FC[1]
+    if stage == "tower_back3":
+        return "flop", 4.0 * B * FC[1] * FC[2]
+    if stage == "cin_back":  # dC_l and dZ_l GEMMs of every CIN layer
+        hps = [F] + CIN[:-1]
+        return "flop", sum(4.0 * B * K * F * hp * h for hp, h in zip(hps, CIN))
+    if stage == "gather_x":
+        return "byte", B * (F * 4 + F * K * es + D * 4)
     if stage == "tower_layer1":
         return "flop", 2.0 * B * k1 * FC[0]
     if stage == "tower_layer2":
@@ -151,14 +164,16 @@ def main():
         dist.init_process_group("gloo")
     import rmx
 
-    B = args.batch or (16384 if args.workload == "xdeepfm" else 65536)
+    train = args.workload.endswith("_train")
+    base = args.workload[:-len("_train")] if train else args.workload
+    B = args.batch or ({"xdeepfm": 16384, "xdeepfm_train": 4096}.get(args.workload, 65536))
     sharded = args.workload == "deepfm_sharded"
     Vw = args.vocab or (100_000_000 if sharded else V)
     rmx.set_device(local)
     ctx = rmx.default_context()
     stream = ctx.stream
     bf16 = args.workload.endswith("bf16")
-    if args.workload == "xdeepfm":
+    if base == "xdeepfm":
         model = rmx.XDeepFM(Vw, F, K, FC, CIN, ctx=ctx)
     elif args.workload == "dcn_bf16":  # configs[4]: DCN depth 3 + fcDims 400^3, bf16 table / weights
         model = rmx.DCN(Vw, F, K, 3, FC, ctx=ctx)
@@ -191,10 +206,23 @@ def main():
     import ctypes
 
     views = [(ids.view(s * B * F, B * F), out.view(s * B, B)) for s in range(nb)]
+    if train:
+        # synthetic labels Bernoulli(0.25), resident before timing; gradient outputs
+        labels = (np.random.default_rng(SEED_IDS).random(nrows) < 0.25).astype(np.float32)
+        tgt = rmx.DeviceArray(ctx, nrows, np.float32)
+        tgt.upload(labels)
+        g_b = rmx.DeviceArray(ctx, 1, np.float32)
+        g_w = rmx.DeviceArray(ctx, B * F, np.float32)
+        g_e = rmx.DeviceArray(ctx, B * F * K, np.float32)
+        g_m = rmx.DeviceArray(ctx, model.matsLength(), np.float32)
+        g_loss = rmx.DeviceArray(ctx, 1, np.float32)
+        tviews = [tgt.view(s * B, B) for s in range(nb)]
 
     def step(i):
         ids_v, out_v = views[i % nb]
-        if sharded:
+        if train:
+            model.backward_ids(table, B, ids_v, tviews[i % nb], g_b, g_w, g_e, g_m, g_loss, stream)
+        elif sharded:
             model.forward_ids_sharded(table, B, ids_v, out_v, stream)
         else:
             model.forward_ids(table, B, ids_v, out_v, stream)
@@ -271,13 +299,15 @@ def main():
     roof["algorithmic_per_launch"] = work
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not train:
         threads = min(16, os.cpu_count() or 1)
         cpu = cpu_baseline_sweep(args.workload, args.cpu_seconds, threads)
 
     if rank == 0:
         line = {
-            "metric": "CTR-forward examples/sec on Criteo-shaped batch, DeepFM & xDeepFM, 1/2/4/8 GPU",
+            "metric": ("CTR-train examples/sec (forward + RecModel.backward gradients; the optimizer lives on "
+                       "the parameter server, out of scope)") if train else
+                      "CTR-forward examples/sec on Criteo-shaped batch, DeepFM & xDeepFM, 1/2/4/8 GPU",
             "value": round(value, 1),
             "unit": "examples/s",
             "n_gpus": world,
@@ -292,7 +322,7 @@ def main():
             "config": {"workload": "%s%s_F39_V%s_k16_fc400x3%s_B%d" % (
                 args.workload, "" if bf16 else "_fp32",
                 ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
-                {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(args.workload, ""), B),
+                {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(base, ""), B),
                 "global_batch": world * B, "rows_per_gpu_set": nrows,
                 "ids": ("zipf%g" % args.zipf) if args.zipf else "uniform",
                 "parallelism": ("hashshard%d_rccl" % world) if sharded else "replicas%d" % world},

@@ -64,6 +64,8 @@ struct TrainState {
   float* zb = nullptr;          // [rc][max F*Hp] Z = x0 (x) u_prev chunk, then its gradient
   float* onesR = nullptr;       // [R]
   int rc = 0;                   // rows per chunk (a multiple of k)
+  float* part2 = nullptr;       // [cap_part] slice partials of wgrad / colsum
+  int64_t cap_part = 0;
 };
 
 namespace {
@@ -308,18 +310,23 @@ __global__ void cin_z_kernel(int64_t rows, int F, int Hp, const float* __restric
   z[i] = x0[r * F + f] * up[r * ldu + h];
 }
 
-// gx0[r][f] += sum_h gz[r][f*Hp + h] * up[r][h]
-__global__ void cin_back_x0_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
-                                   const float* __restrict__ up, int ldu, float* __restrict__ gx0) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows * F) return;
-  const int64_t r = i / F;
-  const int f = (int)(i - r * F);
-  const float* g = gz + r * (int64_t)F * Hp + (int64_t)f * Hp;
+// gx0[r][f] += sum_h gz[r][f*Hp + h] * up[r][h]: one block per row, wave w takes f = w, w + 4, ...,
+// lanes stride h (coalesced 256-B reads of gz), shuffle reduction per f (fixed order).
+__global__ __launch_bounds__(256) void cin_back_x0_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
+                                                          const float* __restrict__ up, int ldu,
+                                                          float* __restrict__ gx0) {
+  const int64_t r = blockIdx.x;
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* uu = up + r * ldu;
-  float acc = 0.f;
-  for (int h = 0; h < Hp; ++h) acc += g[h] * uu[h];
-  gx0[i] += acc;
+  const float* g = gz + r * (int64_t)F * Hp;
+  for (int f = w; f < F; f += 4) {
+    float acc = 0.f;
+    for (int h = lane; h < Hp; h += 64) acc += g[(int64_t)f * Hp + h] * uu[h];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) gx0[r * F + f] += acc;
+  }
 }
 
 // out[r][h] (=, or += when accum) sum_f gz[r][f*Hp + h] * x0[r][f]
@@ -337,7 +344,186 @@ __global__ void cin_back_u_kernel(int64_t rows, int F, int Hp, const float* __re
   else out[r * ldo + h] = acc;
 }
 
+// ---- weight gradients: dW[n][k] = sum_r A[r][n] X[r][k] (reduction over the batch rows) ----
+// The "TN" GEMM of every Linear backward.  Both operands are row-major over the reduction index,
+// so a block stages 16-row chunks of A[:, n0:n0+64] and X[:, k0:k0+64] TRANSPOSED into LDS tile
+// images [col][16 rows] (one 64-B row per column; the row quartets of lane group g are 16-B slots,
+// XOR-swizzled as the forward engine's, k_gemm.hpp) with one ds_write_b128 per thread, and reads
+// MFMA fragments with ds_read_b128: lane (i = l & 15, g = l >> 4) holds rows 4g..4g+3 of column i,
+// feeding 4 k-steps of v_mfma_f32_16x16x4_f32.  4 waves in 2 x 2, 32 x 32 outputs each.  The rows
+// are split into S slices (grid.y) for parallelism; each block writes its partial tile to
+// part[slice][N][K] and wgrad_reduce_kernel sums the slices in fixed order (deterministic).
+constexpr int kWgT = 64;  // block tile (n and k)
+
+__device__ __forceinline__ int wg_slot(int col, int g) { return g ^ ((4 - ((col >> 2) & 3)) & 3); }
+
+__global__ __launch_bounds__(256) void wgrad_kernel(int rows, int N, int K, const float* __restrict__ A, int lda,
+                                                    const float* __restrict__ X, int ldx, int rows_per_slice,
+                                                    int tiles, float* __restrict__ part) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float lds[2][2][kWgT * 16];  // [buf][A|X][col][16]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // XCD-aware order: consecutive block ids go to the 8 XCDs round robin, so XCD x runs slices
+  // x, x + 8, ... and all tiles of a slice share its L2 (the slice's rows are fetched once per XCD)
+  const int bid = blockIdx.x, xcd = bid & 7, idx = bid >> 3;
+  const int slice = (idx / tiles) * 8 + xcd, tile = idx % tiles;
+  const int ntn = (N + kWgT - 1) / kWgT;
+  const int n0 = (tile % ntn) * kWgT, k0 = (tile / ntn) * kWgT;
+  const int r_begin = slice * rows_per_slice;
+  const int r_end = min(rows, r_begin + rows_per_slice);
+  const int nch = r_end > r_begin ? (r_end - r_begin + 15) / 16 : 0;
+  // staging item: column = lane, row quartet h = wid (rows 4h..4h+3 of the chunk)
+  const int col = lane, h = wid;
+  float4 ra, rx;
+  auto gload = [&](int c) {
+    const int r0 = r_begin + c * 16 + 4 * h;
+    float va[4], vx[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + q;
+      const bool ok = r < r_end;
+      va[q] = (ok && n0 + col < N) ? A[(int64_t)r * lda + n0 + col] : 0.f;
+      vx[q] = (ok && k0 + col < K) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
+    }
+    ra = make_float4(va[0], va[1], va[2], va[3]);
+    rx = make_float4(vx[0], vx[1], vx[2], vx[3]);
+  };
+  auto sstore = [&](int buf) {
+    const int off = col * 16 + wg_slot(col, h) * 4;
+    *reinterpret_cast<float4*>(&lds[buf][0][off]) = ra;
+    *reinterpret_cast<float4*>(&lds[buf][1][off]) = rx;
+  };
+  const int wi = wid >> 1, wj = wid & 1, g = lane >> 4, r16 = lane & 15;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nch > 0) {
+    gload(0);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nch) gload(c + 1);
+    f32x4 fa[2], fx[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ca = wi * 32 + t * 16 + r16, cx = wj * 32 + t * 16 + r16;
+      fa[t] = *reinterpret_cast<const f32x4*>(&lds[cur][0][ca * 16 + wg_slot(ca, g) * 4]);
+      fx[t] = *reinterpret_cast<const f32x4*>(&lds[cur][1][cx * 16 + wg_slot(cx, g) * 4]);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a][s4], fx[b][s4], acc[a][b], 0, 0, 0);
+    if (c + 1 < nch) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  float* out = part + (int64_t)slice * N * K;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int k = k0 + wj * 32 + b * 16 + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wi * 32 + a * 16 + 4 * g + r;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][b][r];
+      }
+    }
+}
+
+// out[i] (=, or += when accum) sum_s part[s][i]: a block covers 64 outputs with 4 wave-groups, group
+// q summing slices q, q + 4, ...; the 4 group sums are added in fixed order (deterministic).
+__global__ __launch_bounds__(256) void slice_reduce_kernel(int S, int64_t n, const float* __restrict__ part,
+                                                           float* __restrict__ out, int accum) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + c;
+  float v = 0.f;
+  if (i < n)
+    for (int sl = q; sl < S; sl += 4) v += part[(int64_t)sl * n + i];
+  red[q][c] = v;
+  __syncthreads();
+  if (q == 0 && i < n) {
+    const float t = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    out[i] = accum ? out[i] + t : t;
+  }
+}
+
+// Column sums over row slices: part[slice][n] = sum_{r in slice} w[r] * M[r][n]  (w null: 1).
+// Bias gradients (sum over the batch of dPre) and the output-weight gradients (h^T dz).  A block
+// covers 64 columns x one slice with 4 wave-groups over interleaved rows (coalesced 256-B rows).
+__global__ __launch_bounds__(256) void colsum_kernel(int rows, int N, const float* __restrict__ M, int ldm,
+                                                     const float* __restrict__ w, int rows_per_slice,
+                                                     float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int r0 = blockIdx.y * rows_per_slice, r1 = min(rows, r0 + rows_per_slice);
+  float acc = 0.f;
+  if (n < N) {
+#pragma unroll 8
+    for (int r = r0 + q; r < r1; r += 4) acc += w ? w[r] * M[(int64_t)r * ldm + n] : M[(int64_t)r * ldm + n];
+  }
+  red[q][c] = acc;
+  __syncthreads();
+  if (q == 0 && n < N) part[(int64_t)blockIdx.y * N + n] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
 inline unsigned nblk(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int ensure_part(TrainState& T, int64_t n) {
+  if (n <= T.cap_part) return RMX_OK;
+  RMX_HIP(hipDeviceSynchronize());
+  tfree(T.part2);
+  int st = talloc(&T.part2, (size_t)n);
+  if (st) return st;
+  T.cap_part = n;
+  return RMX_OK;
+}
+
+// out (N x K row-major) (= or +=) A[rows][lda](N columns)^T . X[rows][ldx](K columns)
+int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, int lda, const float* X, int ldx,
+          float* out, bool accum) {
+  if (rows <= 0 || N <= 0 || K <= 0) return RMX_OK;
+  const int tiles = ((N + kWgT - 1) / kWgT) * ((K + kWgT - 1) / kWgT);
+  // slices of ~1024 rows (one slice of both operands, (N + K) * 4 KiB, stays in an XCD's 4 MiB L2),
+  // at least ~1024 blocks in flight, S a multiple of the 8 XCDs
+  int S = std::max((rows + 1023) / 1024, std::min((1024 + tiles - 1) / tiles, std::max(1, rows / 64)));
+  S = round_up(std::min(S, 512), 8);
+  const int rps = round_up((rows + S - 1) / S, 16);
+  int st = ensure_part(T, (int64_t)S * N * K);
+  if (st) return st;
+  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, rows, N, K, A, lda, X, ldx, rps, tiles,
+                     T.part2);
+  RMX_HIP(hipGetLastError());
+  hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)N * K + 63) / 64)), dim3(256), 0, s, S,
+                     (int64_t)N * K, T.part2, out, accum ? 1 : 0);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// out[n] (= or +=) sum_r w[r] M[r][n]  (w null: plain column sums)
+int colsum(TrainState& T, hipStream_t s, int rows, int N, const float* M, int ldm, const float* w, float* out,
+           bool accum) {
+  if (rows <= 0 || N <= 0) return RMX_OK;
+  int S = std::max(1, std::min(128, rows / 512));
+  const int rps = (rows + S - 1) / S;
+  S = (rows + rps - 1) / rps;
+  int st = ensure_part(T, (int64_t)S * N);
+  if (st) return st;
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, S), dim3(256), 0, s, rows, N, M, ldm, w, rps, T.part2);
+  RMX_HIP(hipGetLastError());
+  hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, S, (int64_t)N, T.part2,
+                     out, accum ? 1 : 0);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
 
 // output columns of a tower layer that belong to the layer (DCN fused extra columns excluded)
 inline int eff_n(const DenseLayer& L) { return L.N1 >= 0 ? L.N1 : L.N; }
@@ -375,6 +561,8 @@ int ensure_train(rmx_model& m, int B) {
   tfree(T.dzr);
   tfree(T.zb);
   tfree(T.onesR);
+  tfree(T.part2);
+  T.cap_part = 0;
   if (T.part) (void)hipFree(T.part);
   T.part = nullptr;
   int st;
@@ -458,6 +646,7 @@ void train_release(rmx_model& m) {
   tfree(T.dzr);
   tfree(T.zb);
   tfree(T.onesR);
+  tfree(T.part2);
   if (T.part) (void)hipFree(T.part);
   if (T.blas) rocblas_destroy_handle(T.blas);
   delete m.train;
@@ -479,6 +668,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   int st = model_ensure_ws(m, B);  // y12 (first order + FM) lives in the inference workspace
   if (st) return st;
   if ((st = ensure_train(m, B))) return st;
+  if (m.timing) ++m.timed_calls;
   TrainState& T = *m.train;
   RMX_BLAS(rocblas_set_stream(T.blas, s));
   const int F = m.F, k = m.k, D = F * k, Lc = m.cross_depth;
@@ -588,9 +778,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     const DenseLayer& last = m.layers.back();
     const int N = eff_n(last);
     StageTimer tm(m, s, "head_back");
-    if (o.g_mats)
-      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, T.h[nl - 1], last.Npad, T.dz, 1, &zero,
-                             o.g_mats + m.wo_off, 1));
+    if (o.g_mats && (st = colsum(T, s, B, N, T.h[nl - 1], last.Npad, T.dz, o.g_mats + m.wo_off, false))) return st;
     hipLaunchKernelGGL(head_back_kernel, dim3(nblk((int64_t)B * N)), dim3(256), 0, s, B, N, T.h[nl - 1], last.Npad,
                        T.dz, m.wo, T.g[0], last.Npad);
     RMX_HIP(hipGetLastError());
@@ -617,18 +805,16 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     }
     for (int q = 0; q < nb; ++q) {
       const Blk& bk = blks[q];
-      if (o.g_mats)
-        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, bk.K, N, B, &one,
-                               xin + bk.c0, ldin, dpre, L.Npad, &zero, o.g_mats + bk.w, bk.K));
+      if (o.g_mats && (st = wgrad(T, s, B, N, bk.K, dpre, L.Npad, xin + bk.c0, ldin, o.g_mats + bk.w, false)))
+        return st;
       if (need_dx)
         RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, bk.K, B, N, &one,
                                m.mats_dev + bk.w, bk.K, dpre, L.Npad, &zero, dxin + bk.c0, ldin));
     }
-    if (o.g_mats && L.bias_mode == 1)
-      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, dpre, L.Npad, T.ones, 1, &zero,
-                             o.g_mats + L.b_off, 1));
+    if (o.g_mats && L.bias_mode == 1 && (st = colsum(T, s, B, N, dpre, L.Npad, nullptr, o.g_mats + L.b_off, false)))
+      return st;
     if (o.g_mats && L.bias_mode == 2) {  // one CAdd(1) scalar over all outputs
-      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, N, B, &one, dpre, L.Npad, T.ones, 1, &zero, T.tmp, 1));
+      if ((st = colsum(T, s, B, N, dpre, L.Npad, nullptr, T.tmp, false))) return st;
       hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(64), 0, s, N, T.tmp, o.g_mats + L.b_off);
       RMX_HIP(hipGetLastError());
     }
@@ -654,10 +840,8 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
                            T.coef, Lc + 1, &one, dX, T.ldx));
     if (o.g_mats) {
       // gwc = coef^T x0 ; + the per-row constants summed over the batch ; beta_l sums
-      RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, D, Lc + 1, B, &one, T.x,
-                             T.ldx, T.coef, Lc + 1, &zero, T.gwc, D));
-      RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, 2 * Lc + 1, B, &one, T.cst, 2 * Lc + 1, T.ones, 1,
-                             &zero, T.tmp, 1));
+      if ((st = wgrad(T, s, B, Lc + 1, D, T.coef, Lc + 1, T.x, T.ldx, T.gwc, false))) return st;
+      if ((st = colsum(T, s, B, 2 * Lc + 1, T.cst, 2 * Lc + 1, nullptr, T.tmp, false))) return st;
       hipLaunchKernelGGL(cross_wgrad_kernel, dim3(nblk((int64_t)(Lc + 1) * D)), dim3(256), 0, s, Lc, D, T.gwc, T.tmp,
                          o.g_mats + m.cross_w_off, o.g_mats + m.wo_x_off);
       RMX_HIP(hipGetLastError());
@@ -687,10 +871,8 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       RMX_HIP(hipGetLastError());
       if (o.g_mats) {
         // pooled slice of W_out: sum_r dz[b] u_l[r][h]; bias c_l: sum_r gpre[r][h]
-        RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, H, (int)R, &one, T.u[l], ldu, T.dzr, 1, &zero,
-                               o.g_mats + c.wo_off, 1));
-        RMX_BLAS(rocblas_sgemv(T.blas, rocblas_operation_none, H, (int)R, &one, T.gpre, ldu, T.onesR, 1, &zero,
-                               o.g_mats + c.b_off, 1));
+        if ((st = colsum(T, s, (int)R, H, T.u[l], ldu, T.dzr, o.g_mats + c.wo_off, false))) return st;
+        if ((st = colsum(T, s, (int)R, H, T.gpre, ldu, nullptr, o.g_mats + c.b_off, false))) return st;
       }
       for (int64_t r0 = 0; r0 < R; r0 += T.rc) {
         const int rows = (int)std::min<int64_t>(T.rc, R - r0);
@@ -699,15 +881,13 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
           hipLaunchKernelGGL(cin_z_kernel, dim3(nblk((int64_t)rows * FH)), dim3(256), 0, s, (int64_t)rows, F, Hp,
                              T.x0 + r0 * F, up + r0 * ldup, ldup, T.zb);
           RMX_HIP(hipGetLastError());
-          const float beta = r0 == 0 ? 0.f : 1.f;
-          RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_transpose, FH, H, rows, &one, T.zb,
-                                 FH, gp, ldu, &beta, o.g_mats + c.w_off, FH));
+          if ((st = wgrad(T, s, rows, H, FH, gp, ldu, T.zb, FH, o.g_mats + c.w_off, r0 > 0))) return st;
         }
         // dL/dz for this chunk: gpre . C_l  [rows][F*Hp]
         RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, FH, rows, H, &one,
                                m.mats_dev + c.w_off, FH, gp, ldu, &zero, T.zb, FH));
-        hipLaunchKernelGGL(cin_back_x0_kernel, dim3(nblk((int64_t)rows * F)), dim3(256), 0, s, (int64_t)rows, F, Hp,
-                           T.zb, up + r0 * ldup, ldup, T.gx0 + r0 * F);
+        hipLaunchKernelGGL(cin_back_x0_kernel, dim3(rows), dim3(256), 0, s, (int64_t)rows, F, Hp, T.zb,
+                           up + r0 * ldup, ldup, T.gx0 + r0 * F);
         RMX_HIP(hipGetLastError());
         // through u_{l-1} (layer 0: u_0 = x0, so into gx0 as well)
         float* gout = l == 0 ? T.gx0 + r0 * F : T.gu[gcur ^ 1] + r0 * m.cin_layers[l - 1].Npad;
