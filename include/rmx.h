@@ -64,10 +64,14 @@ extern "C" {
 #define RMX_LAYOUT_K_MAJOR 0   /* reference Angel PS layout: k rows x V columns (ParRecModel.scala:95-101) */
 #define RMX_LAYOUT_ROW_MAJOR 1 /* V rows x k columns                                                      */
 
+#define RMX_FORMAT_LIBSVM 0    /* "label id:value ..."          SampleParser.parseLIBSVM (SampleParser.scala:23-51) */
+#define RMX_FORMAT_LIBFFM 1    /* "label field:id:value ..."    SampleParser.parseLIBFFM (SampleParser.scala:53-85) */
+
 typedef struct rmx_ctx rmx_ctx;
 typedef struct rmx_model rmx_model;
 typedef struct rmx_table rmx_table;
 typedef struct rmx_shard rmx_shard;
+typedef struct rmx_samples rmx_samples;
 
 /* ------------------------------------------------------------------ misc -- */
 const char* rmx_last_error(void);
@@ -238,6 +242,25 @@ int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w,
 /* Collective: L-B forward of this rank's batch (d_ids [batch * nFields]) over the sharded table. */
 int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t batch, const int32_t* d_ids,
                             float* d_out, void* stream);
+
+/* ---- samples: native LIBSVM / LIBFFM parser (host, multi-threaded) ----
+ * Replaces SampleParser.parse (yr/data/SampleParser.scala:14-85) for text in memory (one sample per
+ * '\n'-terminated line): rows[nnz] = line index, cols[nnz] = id - 1, values[nnz], targets[lines] =
+ * labels, fields[nnz] (LIBFFM only).  Malformed lines fail with RMX_E_INVALID naming the line, where
+ * the reference throws NumberFormatException / ArrayIndexOutOfBoundsException.  nthreads <= 0:
+ * all hardware threads.  The arrays stay valid until rmx_samples_free. */
+int rmx_samples_parse(const char* text, size_t len, int format, int nthreads, rmx_samples** out);
+int rmx_samples_free(rmx_samples* s);
+int64_t rmx_samples_lines(const rmx_samples* s);
+int64_t rmx_samples_nnz(const rmx_samples* s);
+const int64_t* rmx_samples_rows(const rmx_samples* s);
+const int64_t* rmx_samples_cols(const rmx_samples* s);
+const float* rmx_samples_values(const rmx_samples* s);
+const float* rmx_samples_targets(const rmx_samples* s);
+const int64_t* rmx_samples_fields(const rmx_samples* s);  /* NULL for LIBSVM */
+/* ids [lines][n_fields] (int32, ParRecModel.scala:342 .toInt) of a regular batch (every line has
+ * exactly n_fields pairs: the models' Reshape(B, F, k)); RMX_E_SHAPE otherwise. */
+int rmx_samples_ids(const rmx_samples* s, int32_t n_fields, int32_t* ids, int64_t cap);
 
 #ifdef __cplusplus
 }

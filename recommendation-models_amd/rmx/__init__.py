@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT_K_MAJOR,  # noqa: F401
-                   LAYOUT_ROW_MAJOR, DTYPE_F32, DTYPE_BF16, check, ptr)
+                   LAYOUT_ROW_MAJOR, DTYPE_F32, DTYPE_BF16, FORMAT_LIBSVM, FORMAT_LIBFFM, check, ptr)
 
 import ctypes
 
@@ -524,8 +524,64 @@ class PNN(RecModel):
 
 
 # ------------------------------------------------------------------ parser ---
+class Samples:
+    """Parsed LIBSVM / LIBFFM text (native parser, csrc/parse.cpp): numpy copies of the COO arrays."""
+
+    def __init__(self, text, fmt=_lib.FORMAT_LIBSVM, nthreads=0):
+        if isinstance(text, str):
+            text = text.encode()
+        buf = ctypes.c_char_p(text)  # points into the bytes object: no copy
+        h = ctypes.c_void_p()
+        check(_lib.lib.rmx_samples_parse(buf, len(text), int(fmt), int(nthreads), ctypes.byref(h)))
+        try:
+            L = _lib.lib.rmx_samples_lines(h)
+            n = _lib.lib.rmx_samples_nnz(h)
+
+            def arr(fn, ct, dt, cnt):
+                p = fn(h)
+                if not cnt or not p:
+                    return np.zeros(0, dt)
+                return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ct)), shape=(cnt,)).copy()
+            self.rows = arr(_lib.lib.rmx_samples_rows, ctypes.c_int64, np.int64, n)
+            self.cols = arr(_lib.lib.rmx_samples_cols, ctypes.c_int64, np.int64, n)
+            self.values = arr(_lib.lib.rmx_samples_values, ctypes.c_float, np.float32, n)
+            self.targets = arr(_lib.lib.rmx_samples_targets, ctypes.c_float, np.float32, L)
+            self.fields = (arr(_lib.lib.rmx_samples_fields, ctypes.c_int64, np.int64, n)
+                           if fmt == _lib.FORMAT_LIBFFM else None)
+            self._h = h
+        except Exception:
+            _lib.lib.rmx_samples_free(h)
+            raise
+
+    def ids(self, n_fields):
+        """int32 ids [lines * n_fields] of a regular batch (rmx_samples_ids)."""
+        out = np.zeros(len(self.targets) * int(n_fields), np.int32)
+        check(_lib.lib.rmx_samples_ids(self._h, int(n_fields), out.ctypes.data_as(ctypes.c_void_p), out.size))
+        return out
+
+    def coo(self):
+        return CooLongFloatMatrix(self.rows, self.cols, self.values)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None:
+            try:
+                _lib.lib.rmx_samples_free(h)
+            except Exception:
+                pass
+            self._h = None
+
+
 class SampleParser:
-    """yr/data/SampleParser.scala:14-85 (LIBSVM / LIBFFM text -> COO, 1-based ids -> id - 1)."""
+    """yr/data/SampleParser.scala:14-85 (LIBSVM / LIBFFM text -> COO, 1-based ids -> id - 1), on the
+    native multi-threaded parser (csrc/parse.cpp).  lines: a list of strings (one sample each) or
+    one bytes / str blob of '\n'-terminated lines."""
+
+    @staticmethod
+    def _text(lines):
+        if isinstance(lines, (bytes, str)):
+            return lines
+        return "\n".join(lines)
 
     @staticmethod
     def parse(lines, type_):
@@ -535,30 +591,11 @@ class SampleParser:
         return coo, None, targets
 
     @staticmethod
-    def parseLIBSVM(lines):
-        rows, cols, vals = [], [], []
-        targets = np.zeros(len(lines), np.float32)
-        for i, line in enumerate(lines):
-            parts = line.split(" ")
-            targets[i] = float(parts[0])
-            for kv in parts[1:]:
-                k, v = kv.split(":")
-                rows.append(i)
-                cols.append(int(k) - 1)
-                vals.append(float(v))
-        return CooLongFloatMatrix(rows, cols, vals), targets
+    def parseLIBSVM(lines, nthreads=0):
+        s = Samples(SampleParser._text(lines), _lib.FORMAT_LIBSVM, nthreads)
+        return s.coo(), s.targets
 
     @staticmethod
-    def parseLIBFFM(lines):
-        rows, cols, fields, vals = [], [], [], []
-        targets = np.zeros(len(lines), np.float32)
-        for i, line in enumerate(lines):
-            parts = line.split(" ")
-            targets[i] = float(parts[0])
-            for fkv in parts[1:]:
-                f, k, v = fkv.split(":")
-                rows.append(i)
-                fields.append(int(f))
-                cols.append(int(k) - 1)
-                vals.append(float(v))
-        return CooLongFloatMatrix(rows, cols, vals), np.asarray(fields, np.int64), targets
+    def parseLIBFFM(lines, nthreads=0):
+        s = Samples(SampleParser._text(lines), _lib.FORMAT_LIBFFM, nthreads)
+        return s.coo(), s.fields, s.targets

@@ -18,6 +18,7 @@ RMX_E_HIP = -5
 RMX_E_NOMEM = -6
 RMX_E_MATS = -7
 RMX_E_COMM = -8
+FORMAT_LIBSVM, FORMAT_LIBFFM = 0, 1
 UNIQUE_ID_BYTES = 128
 
 DTYPE_F32 = 0
@@ -93,6 +94,16 @@ SIGNATURES = [
     ("rmx_shard_local_rows", c_i64, [c_vp]),
     ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),
     ("rmx_shard_last_sent", c_i64, [c_vp]),
+    ("rmx_samples_parse", c_int, [c_vp, c_sz, c_int, c_int, c_vp]),
+    ("rmx_samples_free", c_int, [c_vp]),
+    ("rmx_samples_lines", c_i64, [c_vp]),
+    ("rmx_samples_nnz", c_i64, [c_vp]),
+    ("rmx_samples_rows", c_vp, [c_vp]),
+    ("rmx_samples_cols", c_vp, [c_vp]),
+    ("rmx_samples_values", c_vp, [c_vp]),
+    ("rmx_samples_targets", c_vp, [c_vp]),
+    ("rmx_samples_fields", c_vp, [c_vp]),
+    ("rmx_samples_ids", c_int, [c_vp, c_i32, c_vp, c_i64]),
     ("rmx_shard_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_forward_ids_sharded", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
 ]
