@@ -187,6 +187,16 @@ int rmx_backward_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int3
                      const float* d_targets, float* d_g_bias, float* d_g_weights, float* d_g_embedding,
                      float* d_g_mats, float* d_loss, void* stream);
 
+/* Predict loop over a device-resident row set (ParRecModel.predict*, ParRecModel.scala:519-581):
+ * scores[r] for rows r < n_rows of ids [n_rows][F], forwards of `batch` rows. */
+int rmx_predict_ids(rmx_model* m, const rmx_table* t, int64_t n_rows, const int32_t* d_ids,
+                    int32_t batch, float* d_scores, void* stream);
+/* AUC of (label > 0, score) pairs on the device (the examples' per-epoch metric,
+ * example/DeepFMLocalExample.scala:44-52): Mann-Whitney statistic, tied scores count 1/2.
+ * *auc = NaN when one class is empty.  Synchronises the stream. */
+int rmx_auc(rmx_ctx* ctx, int64_t n, const float* d_labels, const float* d_scores, double* auc,
+            void* stream);
+
 /* Zipf-like ids (SURVEY.md §8d secondary): rank r of field f drawn with P(r) ~ (r+1)^-exponent
  * (continuous power-law inversion, double precision), id = f * (num_rows / n_fields) + r. */
 int rmx_gen_ids_zipf(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,

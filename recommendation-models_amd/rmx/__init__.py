@@ -274,6 +274,14 @@ class ShardedTable:
             pass
 
 
+def auc(ctx, labels_dev, scores_dev, n=None, stream=None):
+    """Device AUC of (label > 0, score) pairs (rmx_auc; ties count 1/2)."""
+    n = labels_dev.n if n is None else int(n)
+    out = ctypes.c_double()
+    check(_lib.lib.rmx_auc(ctx.handle, n, labels_dev.ptr, scores_dev.ptr, ctypes.byref(out), stream))
+    return out.value
+
+
 def gen_ids(ctx, seed, row0, batch, n_fields, num_rows, ids_dev, stream=None, zipf=0.0):
     """Synthetic field-partitioned ids straight into HBM (SURVEY.md §8d generator): uniform within
     the field (bit-identical to oracle orc_gen_ids), or Zipf-like with exponent `zipf` > 0."""
@@ -442,6 +450,11 @@ class RecModel:
     def forward_ids(self, table, batch, ids_dev, out_dev, stream=None):
         """L-B forward: ids [batch * nFields] int32 and out [batch] float32 are DeviceArrays."""
         check(_lib.lib.rmx_forward_ids(self._device(), table.handle, int(batch), ids_dev.ptr, out_dev.ptr, stream))
+
+    def predict_ids(self, table, n_rows, ids_dev, scores_dev, batch=65536, stream=None):
+        """ParRecModel.predict over a device-resident row set: scores for n_rows rows of ids."""
+        check(_lib.lib.rmx_predict_ids(self._device(), table.handle, int(n_rows), ids_dev.ptr, int(batch),
+                                       scores_dev.ptr, stream))
 
     def forward_ids_sharded(self, shard, batch, ids_dev, out_dev, stream=None):
         """Collective L-B forward over a ShardedTable (every rank calls it with its own batch)."""
