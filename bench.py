@@ -298,6 +298,22 @@ def main():
     roof["kernel"] = dom
     roof["algorithmic_per_launch"] = work
 
+    # predict loop over the whole resident row set + AUC (ParRecModel.predict, the examples' metric)
+    pa = None
+    if not train and not sharded:
+        labels = (np.random.default_rng(SEED_IDS).random(nrows) < 0.25).astype(np.float32)
+        dl = rmx.DeviceArray(ctx, nrows, np.float32)
+        dl.upload(labels)
+        ctx.sync()
+        t0 = time.perf_counter()
+        model.predict_ids(table, nrows, ids, out, batch=B, stream=stream)
+        ctx.sync()
+        t1 = time.perf_counter()
+        a = rmx.auc(ctx, dl, out, stream=stream)
+        t2 = time.perf_counter()
+        pa = {"rows": nrows, "predict_ms": round((t1 - t0) * 1e3, 3), "auc_ms": round((t2 - t1) * 1e3, 3),
+              "auc": round(a, 6), "labels": "Bernoulli(0.25), independent of the scores (AUC ~ 0.5)"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not train:
         threads = min(16, os.cpu_count() or 1)
@@ -330,6 +346,7 @@ def main():
                              "nnz_per_step": B * F}} if sharded else {}),
             "roofline": roof,
             "cpu_baseline": cpu,
+            **({"predict_auc": pa} if pa else {}),
             "stages": per_stage,
         }
         print(json.dumps(line), flush=True)
