@@ -554,15 +554,26 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   //   1: LDS-DMA ring (4 chunks), same tiling;
   //   2: LDS-DMA ring (3 chunks), 4 x 2 waves of 32 rows x NT/2 tiles;
   //   3: LDS-DMA ring (3 chunks), 8 x 2 waves of 16 rows x NT/2 tiles, 4 waves / SIMD in one
-  //      16-wave block -- the default for even NT >= 8 (the model pads N = 400 to 26 tiles):
-  //      N = 400, M = 65536, fp32: 0.289 ms/layer vs 0.315 (variant 0); bf16 0.063 vs 0.092.
+  //      16-wave block (default for even NT >= 8 other than 26): N = 400, M = 65536, fp32
+  //      0.289 ms/layer vs 0.315 (variant 0); bf16 0.063 vs 0.092;
+  //   4: LDS-DMA ring (2 chunks), 4 x 2 waves of 16 rows, 2 blocks / CU (NT = 26);
+  //   5: LDS-DMA ring (2 chunks), 4 x 2 waves of 32 rows, 2 blocks / CU (NT = 26).
   // Variants 2 / 3 need an even NT.  Small batches: 4-wave blocks, register-staged.
   constexpr bool kEven = NT % 2 == 0 && NT >= 8;
-  int var = tuning_get("tower_variant", kEven ? 3 : 0);
+  // defaults (A/B'd with tools/tune.py, N = 400 padded to 26 tiles): 8-wave blocks with a 2-deep
+  // LDS-DMA ring fit 2 blocks per CU (one block's epilogue overlaps the other's MFMAs): fp32
+  // 0.280 / 0.183 ms for layers 1 / 2 vs 0.288 / 0.189 (variant 3), bf16 DCN 457 vs 431 M ex/s; the
+  // fp32 output layer prefers 32 rows per wave (variant 5: 0.171 vs 0.177 ms)
+  const int def = NT == 26 ? ((epi == Epi::kOutput && !BF) ? 5 : 4) : (kEven ? 3 : 0);
+  int var = tuning_get("tower_variant", def);
   if (p.M >= 65536) {
     if constexpr (kEven) {
       if (var == 2) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 1, 3>, BF>(s, p, amode, epi);
       if (var == 3) return launch_epi<Tile<1, NT / 2, 8, 2, 1, 4, 3>, BF>(s, p, amode, epi);
+      if constexpr (NT == 26) {
+        if (var == 4) return launch_epi<Tile<1, NT / 2, 4, 2, 1, 4, 2>, BF>(s, p, amode, epi);
+        if (var == 5) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 2, 2>, BF>(s, p, amode, epi);
+      }
     }
     if (var == 1) return launch_epi<Tile<1, NT, 8, 1, 1, 1, 4>, BF>(s, p, amode, epi);
     if (amode == kDenseA) return launch_epi<Tile<1, NT, 8, 1, 2, 1>, BF>(s, p, amode, epi);
