@@ -160,9 +160,17 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
   }
   const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
   if (L.W16) return launch_tower_bf16(s, p, nt, amode, epi);
+  if (L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0 && (epi != Epi::kOutput || L.Npad == kS3BN || oa->part)) {
+    // fp32 layer on the bf16 matrix cores through the exact 3-way split (k_gemm_s3.hip)
+    p.Wp = reinterpret_cast<const float*>(L.W3);
+    p.Kpad = (L.Kpad / 16 + 1) / 2 * 32;
+    int st = launch_tower_s3(s, p, amode, epi);
+    if (st == RMX_OK && epi == Epi::kOutput && L.Npad > kS3BN) st = launch_out_finish(s, M, L.Npad / kS3BN, *oa);
+    return st;
+  }
   switch (nt) {
 #define RMX_NT(n) \
-  case n: return launch_tower_nt<n, false>(s, p, amode, epi);
+  case n: return launch_tower_nt<n, kPrecF32>(s, p, amode, epi);
     RMX_NT(1) RMX_NT(2) RMX_NT(3) RMX_NT(4) RMX_NT(5) RMX_NT(6) RMX_NT(7)
     RMX_NT(8) RMX_NT(10) RMX_NT(13) RMX_NT(16) RMX_NT(20) RMX_NT(25) RMX_NT(26)
 #undef RMX_NT
@@ -196,6 +204,11 @@ int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, in
   if (first && L.Hp_pad > p.XS - 4) {
     set_error("cin: first layer Hp_pad mismatch");
     return RMX_E_INVALID;
+  }
+  if (L.W3 && f32_split_enabled() && L.Npad == kS3BN) {
+    p.Wp = reinterpret_cast<const float*>(L.W3);
+    p.Kpad = round_up(p.K, 32);
+    return launch_cin_s3(s, p);
   }
   switch (L.Npad / 16) {
 #define RMX_NT(n) \

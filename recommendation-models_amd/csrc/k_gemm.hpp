@@ -91,10 +91,24 @@ struct Tile {
   static constexpr int BM = WM * MT * 16, BN = NT * 16;
 };
 
-template <class T, int AMODE>
+// Operand precision of a GEMM instantiation:
+//   kPrecF32   fp32 operands on v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain);
+//   kPrecBF16  bf16 operands on v_mfma_f32_16x16x32_bf16 (the bf16 configuration, configs[4]);
+//   kPrecS3    fp32 operands computed on v_mfma_f32_16x16x32_bf16 through an exact 3-way bf16 split:
+//              x = hi + mid + lo (each bf16, exact for every normal fp32), x*y summed over the six
+//              products hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid.  |mid| <= 2^-8 |x| and
+//              |lo| <= 2^-17 |x|, so the dropped terms are <= (2^-24 + 2^-34) |x y| (the size of
+//              one fp32 rounding) and every kept product is exact in the fp32 accumulator: the
+//              result is fp32-accurate at 6 x 16 / (8 x 32) = 3/8 of the fp32 MFMA cycles.  The weights are pre-split into three bf16 planes (W3); the A operand
+//              is split in registers.
+enum Prec : int { kPrecF32 = 0, kPrecBF16 = 1, kPrecS3 = 2 };
+
+template <class T, int AMODE, int PREC = kPrecF32>
 struct StageGeom {
-  static constexpr int AROWS = AMODE != kCinOuter ? T::BM * T::BKC : 0;
-  static constexpr int ROWS = AROWS + T::BN * T::BKC;  // 64-B rows per stage
+  // kPrecS3: one stage = one 32-wide K step: A as two fp32 16-wide chunks [2][BM], B as the three
+  // bf16 planes [3][BN] (each a 64-B row of 32 values)
+  static constexpr int AROWS = AMODE != kCinOuter ? T::BM * (PREC == kPrecS3 ? 2 : T::BKC) : 0;
+  static constexpr int ROWS = AROWS + T::BN * (PREC == kPrecS3 ? 3 : T::BKC);  // 64-B rows per stage
   static constexpr int FLOATS = ROWS * 16;
 };
 
@@ -110,16 +124,35 @@ struct EpiGeom {
   static constexpr int FLOATS = RW * LD * T::NW;
 };
 
-template <class T, int AMODE, int EPI, bool BF>
+// x (8 fp32 as two float4) = hi + mid + lo exactly, each a bf16x8 (kPrecS3)
+__device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, bf16x8& hi, bf16x8& mi, bf16x8& lo) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float v = q < 4 ? x0[q & 3] : x1[q & 3];
+    const __bf16 h = (__bf16)v;
+    const float r = v - (float)h;
+    const __bf16 m = (__bf16)r;
+    hi[q] = h;
+    mi[q] = m;
+    lo[q] = (__bf16)(r - (float)m);
+  }
+}
+
+template <class T, int AMODE, int EPI, int PREC>
 __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
-  // BF: bf16 operands (v_mfma_f32_16x16x32_bf16, K chunk of 32 per 64-B row), fp32 accumulate,
-  // bf16 stored activations; otherwise fp32 throughout (v_mfma_f32_16x16x4_f32, K chunk 16).
-  constexpr int KC = BF ? 32 : 16, KS = KC / 4;  // elements per chunk row / per 16-B slot
-  static_assert(!BF || AMODE != kCinOuter, "CIN is fp32 only");
+  // kPrecBF16: bf16 operands (v_mfma_f32_16x16x32_bf16, K chunk of 32 per 64-B row), fp32
+  // accumulate, bf16 stored activations; kPrecF32: fp32 throughout (v_mfma_f32_16x16x4_f32, K
+  // chunk 16); kPrecS3: fp32 A chunks of 16 (two per stage), three bf16 B planes of 32, fp32
+  // stored activations.  A "chunk" c below is a K step of KC elements (32 for kPrecS3).
+  constexpr bool BF = PREC == kPrecBF16, S3 = PREC == kPrecS3;
+  constexpr int KC = (BF || S3) ? 32 : 16;       // K elements per step
+  constexpr int KCA = BF ? 32 : 16, KSA = KCA / 4;  // A elements per 64-B row / per 16-B slot
+  static_assert(!BF || AMODE != kCinOuter, "CIN has no bf16 configuration");
+  static_assert(!S3 || T::BKC == 1, "kPrecS3 stages one K step at a time");
   constexpr int MT = T::MT, NTW = T::NTW, WN = T::WN, BKC = T::BKC;
   constexpr int BM = T::BM, BN = T::BN, NTHR = T::NTHR;
   constexpr bool A_LDS = AMODE != kCinOuter;
-  using SG = StageGeom<T, AMODE>;
+  using SG = StageGeom<T, AMODE, PREC>;
   constexpr int AROWS = SG::AROWS, ROWS = SG::ROWS, STAGE = SG::FLOATS;
   constexpr int ITEMS = ROWS * 4;  // float4 items per stage
   constexpr int PER = (ITEMS + NTHR - 1) / NTHR;
@@ -179,46 +212,52 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Global source of logical 16-B slot g of stage row `row` (A rows first: [BKC or 2][BM], then
+  // B rows [BKC or 3][BN]) for stage st; nullptr = zeros (out-of-range rows, K padding).
+  auto src_of = [&](int row, int g, int st) -> const void* {
+    if (row < AROWS) {
+      const int cc = row / BM, r = row - cc * BM;
+      const int c = S3 ? 2 * st + cc : st * BKC + cc;  // A chunk of KCA elements
+      const int m = m0 + r;
+      const int kk = c * KCA + g * KSA;
+      if (m >= M || kk >= p.K) return nullptr;
+      if constexpr (AMODE == kGatherK16) {
+        // fp32: chunk c = field c; bf16: chunk c = fields 2c, 2c+1 (two 32-B rows)
+        const int f = BF ? 2 * c + (g >> 1) : c;
+        const int id = sids[r * F + f];
+        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * 16 + (g & 1) * 8)
+                  : (const void*)(p.ga.table + (int64_t)id * 16 + g * 4);
+      } else if constexpr (AMODE == kGatherAny) {
+        const int f = kk / p.ga.k, j = kk - f * p.ga.k;
+        const int id = sids[r * F + f];
+        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * p.ga.k + j)
+                  : (const void*)(p.ga.table + (int64_t)id * p.ga.k + j);
+      } else {
+        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + (int64_t)m * p.lda + kk)
+                  : (const void*)(p.A + (int64_t)m * p.lda + kk);
+      }
+    }
+    const int rb = row - AROWS;
+    const int cc = rb / BN, n = rb - cc * BN;
+    if constexpr (S3)  // plane cc of step st: W3 [steps][3][Npad][32] bf16
+      return reinterpret_cast<const bf16_t*>(p.Wp) + ((int64_t)(st * 3 + cc) * p.Npad + n0 + n) * 32 + g * 8;
+    const int c = st * BKC + cc;
+    if (c >= nchunks) return nullptr;
+    return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.Wp) + ((int64_t)c * p.Npad + n0 + n) * 32 + g * 8)
+              : (const void*)(p.Wp + ((int64_t)c * p.Npad + n0 + n) * 16 + g * 4);
+  };
+
   float4 stage[PER];
-  // item i of a stage: row = i >> 2 (A rows first: [BKC][BM], then B rows [BKC][BN]), slot g = i & 3
+  // item i of a stage: row = i >> 2, slot g = i & 3
   auto gload = [&](int st) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int i = tid + q * NTHR;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       const int row = i >> 2, g = i & 3;
-      if (row < AROWS) {
-        const int cc = row / BM, r = row - cc * BM;
-        const int c = st * BKC + cc;
-        const int m = m0 + r;
-        const int kk = c * KC + g * KS;
-        if (m < M && kk < p.K) {
-          if constexpr (AMODE == kGatherK16) {
-            // fp32: chunk c = field c; bf16: chunk c = fields 2c, 2c+1 (two 32-B rows)
-            const int f = BF ? 2 * c + (g >> 1) : c;
-            const int id = sids[r * F + f];
-            v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * 16 +
-                                                       (g & 1) * 8)
-                   : *reinterpret_cast<const float4*>(p.ga.table + (int64_t)id * 16 + g * 4);
-          } else if constexpr (AMODE == kGatherAny) {
-            const int f = kk / p.ga.k, j = kk - f * p.ga.k;
-            const int id = sids[r * F + f];
-            v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.ga.table) +
-                                                       (int64_t)id * p.ga.k + j)
-                   : *reinterpret_cast<const float4*>(p.ga.table + (int64_t)id * p.ga.k + j);
-          } else {
-            v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.A) + (int64_t)m * p.lda + kk)
-                   : *reinterpret_cast<const float4*>(p.A + (int64_t)m * p.lda + kk);
-          }
-        }
-      } else if (row < ROWS) {
-        const int rb = row - AROWS;
-        const int cc = rb / BN, n = rb - cc * BN;
-        const int c = st * BKC + cc;
-        if (c < nchunks)
-          v = BF ? *reinterpret_cast<const float4*>(reinterpret_cast<const bf16_t*>(p.Wp) +
-                                                     ((int64_t)c * p.Npad + n0 + n) * 32 + g * 8)
-                 : *reinterpret_cast<const float4*>(p.Wp + ((int64_t)c * p.Npad + n0 + n) * 16 + g * 4);
+      if (row < ROWS) {
+        const void* src = src_of(row, g, st);
+        if (src) v = *reinterpret_cast<const float4*>(src);
       }
       stage[q] = v;
     }
@@ -241,25 +280,96 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   for (int i = 0; i < MT; ++i) arow[i] = wm * MT * 16 + i * 16 + r16;
   const int bt0 = wn * NTW;  // first column tile of this wave
 
-  // kCinOuter: the row's u[h-chunk] for the current hc, reloaded when hc changes
-  float4 uf[MT];
-  int cur_hc = -1;
-  auto load_u = [&](int hc) {
+  // kCinOuter: the row's u[h-chunk] for the current hc, reloaded when hc changes (kPrecS3: one
+  // cache per half of the 32-wide step, whose two 16-wide chunks may sit in different h-chunks)
+  constexpr int NU = S3 ? 2 : 1;
+  float4 uf[NU][MT];
+  int cur_hc[NU];
+#pragma unroll
+  for (int h = 0; h < NU; ++h) cur_hc[h] = -1;
+  auto load_u = [&](int h, int hc) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       if (p.cin_first) {
-        uf[i] = *reinterpret_cast<const float4*>(extra + arow[i] * p.XS + hc * 16 + g * 4);
+        uf[h][i] = *reinterpret_cast<const float4*>(extra + arow[i] * p.XS + hc * 16 + g * 4);
       } else {
         const int m = m0 + arow[i];
-        uf[i] = m < M ? *reinterpret_cast<const float4*>(p.u_prev + (int64_t)m * p.ldu + hc * 16 + g * 4)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        uf[h][i] = m < M ? *reinterpret_cast<const float4*>(p.u_prev + (int64_t)m * p.ldu + hc * 16 + g * 4)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    cur_hc = hc;
+    cur_hc[h] = hc;
+  };
+  // CIN A fragment of 16-wide chunk c16 (= hc * F + f): a = x0[row][f] * u[row][16 hc + 4 g ..]
+  auto cin_a = [&](int h, int c16, f32x4* a) {
+    if (c16 * 16 >= p.K) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      return;
+    }
+    const int hc = c16 / F, f = c16 - hc * F;
+    if (hc != cur_hc[h]) load_u(h, hc);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const float xv = extra[arow[i] * p.XS + f];
+      a[i] = f32x4{xv * uf[h][i].x, xv * uf[h][i].y, xv * uf[h][i].z, xv * uf[h][i].w};
+    }
+  };
+
+  // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
+  // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
+  auto compute_step_s3 = [&](const float* cur, int c) {
+    f32x4 a0[MT], a1[MT];
+    if constexpr (A_LDS) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int o = arow[i] * 16 + swz_slot(arow[i], g) * 4;
+        a0[i] = *reinterpret_cast<const f32x4*>(cur + o);
+        a1[i] = *reinterpret_cast<const f32x4*>(cur + BM * 16 + o);
+      }
+    } else {
+      cin_a(0, 2 * c, a0);
+      cin_a(1, 2 * c + 1, a1);
+    }
+    bf16x8 ah[MT], am[MT], al[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
+    const float* Bt = cur + AROWS * 16;  // planes [3][BN] of 64-B rows
+    constexpr int GS = 4;                // column tiles whose B fragments are in flight together
+#pragma unroll
+    for (int j0 = 0; j0 < NTW; j0 += GS) {
+      f32x4 bh[GS], bm[GS], bl[GS];
+#pragma unroll
+      for (int t = 0; t < GS; ++t)
+        if (j0 + t < NTW) {
+          const int row = (bt0 + j0 + t) * 16 + r16;
+          const int o = row * 16 + swz_slot(row, g) * 4;
+          bh[t] = *reinterpret_cast<const f32x4*>(Bt + o);
+          bm[t] = *reinterpret_cast<const f32x4*>(Bt + BN * 16 + o);
+          bl[t] = *reinterpret_cast<const f32x4*>(Bt + 2 * BN * 16 + o);
+        }
+#pragma unroll
+      for (int t = 0; t < GS; ++t)
+        if (j0 + t < NTW)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            f32x4 d = acc[i][j0 + t];
+            // smallest terms first
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], __builtin_bit_cast(bf16x8, bm[t]), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], __builtin_bit_cast(bf16x8, bh[t]), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(bf16x8, bl[t]), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], __builtin_bit_cast(bf16x8, bh[t]), d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(bf16x8, bm[t]), d, 0, 0, 0);
+            acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(bf16x8, bh[t]), d, 0, 0, 0);
+          }
+    }
   };
 
   // one K chunk c of the stage image at `cur` (chunk slot cc inside the stage)
   auto compute_chunk = [&](const float* cur, int cc, int c) {
+    if constexpr (S3) {
+      compute_step_s3(cur, c);
+    } else {
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
       f32x4 a[MT];
       if constexpr (A_LDS) {
@@ -268,13 +378,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         for (int i = 0; i < MT; ++i)
           a[i] = *reinterpret_cast<const f32x4*>(At + arow[i] * 16 + swz_slot(arow[i], g) * 4);
       } else {
-        const int hc = c / F, f = c - hc * F;
-        if (hc != cur_hc) load_u(hc);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          const float xv = extra[arow[i] * p.XS + f];
-          a[i] = f32x4{xv * uf[i].x, xv * uf[i].y, xv * uf[i].z, xv * uf[i].w};
-        }
+        cin_a(0, c, a);
       }
       // groups of >= 4 independent accumulator tiles: consecutive MFMAs of one tile are a group
       // apart (>= 128 cycles), past the 40-cycle dependent latency of v_mfma_f32_16x16x4_f32
@@ -308,6 +412,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                   acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s4], b[t][s4], acc[i][j0 + t], 0, 0, 0);
         }
       }
+    }
   };
 
   if constexpr (RING == 0) {
@@ -343,30 +448,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         const int ins = wid + q * NW;
         if (ins < NINS) {
           const int row = ins * 16 + (lane >> 2), ps = lane & 3;
-          const void* src = g_rmx_zero16;
-          if (row < AROWS) {
-            const int r = row, g = swz_slot(r, ps), m = m0 + r, kk = c * KC + g * KS;
-            if (m < M && kk < p.K) {
-              if constexpr (AMODE == kGatherK16) {
-                const int f = BF ? 2 * c + (g >> 1) : c;
-                const int id = sids[r * F + f];
-                src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * 16 + (g & 1) * 8)
-                         : (const void*)(p.ga.table + (int64_t)id * 16 + g * 4);
-              } else if constexpr (AMODE == kGatherAny) {
-                const int f = kk / p.ga.k, j = kk - f * p.ga.k;
-                const int id = sids[r * F + f];
-                src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * p.ga.k + j)
-                         : (const void*)(p.ga.table + (int64_t)id * p.ga.k + j);
-              } else {
-                src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + (int64_t)m * p.lda + kk)
-                         : (const void*)(p.A + (int64_t)m * p.lda + kk);
-              }
-            }
-          } else {
-            const int n = row - AROWS, g = swz_slot(n, ps);
-            src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.Wp) + ((int64_t)c * p.Npad + n0 + n) * 32 + g * 8)
-                     : (const void*)(p.Wp + ((int64_t)c * p.Npad + n0 + n) * 16 + g * 4);
-          }
+          const int lrow = row < AROWS ? row % BM : (row - AROWS) % BN;
+          const void* src = src_of(row, swz_slot(lrow, ps), c);
+          if (!src) src = g_rmx_zero16;
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
         }
       }
@@ -448,7 +532,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
-        const int n = (bt0 + j) * 16 + r16;
+        const int n = n0 + (bt0 + j) * 16 + r16;
         const float bn = p.bias[n];
         const float wv = EPI == kEpiOutput ? p.oa.wo[n] : p.wo[n];
 #pragma unroll
@@ -483,6 +567,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         p.rowdot[m] = p.cin_first ? y : p.rowdot[m] + y;
       } else {
         const OutArgs& oa = p.oa;
+        if (gridDim.y > 1) {  // a column slice of the layer: partial logit, out_finish_kernel combines
+          oa.part[(int64_t)blockIdx.y * M + m] = y;
+          continue;
+        }
         if (oa.has_bo) y = y + oa.bo;
         if (oa.rowsum) {
           float rs = 0.f;
@@ -511,9 +599,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 constexpr int kNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16, 20, 25, 26};
 constexpr int kCinNTs[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 13, 16};
 
-template <class T, int AMODE, int EPI, bool BF = false>
+template <class T, int AMODE, int EPI, int PREC = kPrecF32>
 int launch_cfg(hipStream_t s, GemmArgs& p) {
-  using SG = StageGeom<T, AMODE>;
+  using SG = StageGeom<T, AMODE, PREC>;
   size_t lds = sizeof(float) * T::NBUF * SG::FLOATS;
   if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * T::BM * p.ga.F;
   if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
@@ -527,8 +615,16 @@ int launch_cfg(hipStream_t s, GemmArgs& p) {
     set_error("gemm: Npad " + std::to_string(p.Npad) + " is not a multiple of the block width");
     return RMX_E_INVALID;
   }
+  if (EPI == kEpiCin && p.Npad != T::BN) {
+    set_error("gemm: a CIN layer must fit one block");
+    return RMX_E_INVALID;
+  }
+  if (EPI == kEpiOutput && p.Npad != T::BN && !p.oa.part) {
+    set_error("gemm: a sliced output layer needs the partial-logit buffer");
+    return RMX_E_INVALID;
+  }
   dim3 grid((p.M + T::BM - 1) / T::BM, p.Npad / T::BN);
-  auto kern = gemm_kernel<T, AMODE, EPI, BF>;
+  auto kern = gemm_kernel<T, AMODE, EPI, PREC>;
   if (lds > 64 * 1024)
     RMX_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(kern, grid, dim3(T::NTHR), lds, s, p);
@@ -536,18 +632,18 @@ int launch_cfg(hipStream_t s, GemmArgs& p) {
   return RMX_OK;
 }
 
-template <class T, bool BF>
+template <class T, int PREC>
 int launch_epi(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
-#define RMX_EPI(AM)                                                          \
-  if (epi == Epi::kReluStore) return launch_cfg<T, AM, kEpiRelu, BF>(s, p); \
-  return launch_cfg<T, AM, kEpiOutput, BF>(s, p);
+#define RMX_EPI(AM)                                                            \
+  if (epi == Epi::kReluStore) return launch_cfg<T, AM, kEpiRelu, PREC>(s, p); \
+  return launch_cfg<T, AM, kEpiOutput, PREC>(s, p);
   if (amode == kDenseA) { RMX_EPI(kDenseA) }
   if (amode == kGatherK16) { RMX_EPI(kGatherK16) }
   RMX_EPI(kGatherAny)
 #undef RMX_EPI
 }
 
-template <int NT, bool BF>
+template <int NT, int PREC>
 int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // Large batches (M >= 65536, >= 2 blocks of 128 rows per CU).  Knob "tower_variant":
   //   0: register-staged double buffer, 8 waves on M x all NT tiles per wave (2 waves / SIMD);
@@ -564,22 +660,22 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // LDS-DMA ring fit 2 blocks per CU (one block's epilogue overlaps the other's MFMAs): fp32
   // 0.280 / 0.183 ms for layers 1 / 2 vs 0.288 / 0.189 (variant 3), bf16 DCN 457 vs 431 M ex/s; the
   // fp32 output layer prefers 32 rows per wave (variant 5: 0.171 vs 0.177 ms)
-  const int def = NT == 26 ? ((epi == Epi::kOutput && !BF) ? 5 : 4) : (kEven ? 3 : 0);
+  const int def = NT == 26 ? ((epi == Epi::kOutput && PREC == kPrecF32) ? 5 : 4) : (kEven ? 3 : 0);
   int var = tuning_get("tower_variant", def);
   if (p.M >= 65536) {
     if constexpr (kEven) {
-      if (var == 2) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 1, 3>, BF>(s, p, amode, epi);
-      if (var == 3) return launch_epi<Tile<1, NT / 2, 8, 2, 1, 4, 3>, BF>(s, p, amode, epi);
+      if (var == 2) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 1, 3>, PREC>(s, p, amode, epi);
+      if (var == 3) return launch_epi<Tile<1, NT / 2, 8, 2, 1, 4, 3>, PREC>(s, p, amode, epi);
       if constexpr (NT == 26) {
-        if (var == 4) return launch_epi<Tile<1, NT / 2, 4, 2, 1, 4, 2>, BF>(s, p, amode, epi);
-        if (var == 5) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 2, 2>, BF>(s, p, amode, epi);
+        if (var == 4) return launch_epi<Tile<1, NT / 2, 4, 2, 1, 4, 2>, PREC>(s, p, amode, epi);
+        if (var == 5) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 2, 2>, PREC>(s, p, amode, epi);
       }
     }
-    if (var == 1) return launch_epi<Tile<1, NT, 8, 1, 1, 1, 4>, BF>(s, p, amode, epi);
-    if (amode == kDenseA) return launch_epi<Tile<1, NT, 8, 1, 2, 1>, BF>(s, p, amode, epi);
-    return launch_epi<Tile<1, NT, 8, 1, 1, 1>, BF>(s, p, amode, epi);
+    if (var == 1) return launch_epi<Tile<1, NT, 8, 1, 1, 1, 4>, PREC>(s, p, amode, epi);
+    if (amode == kDenseA) return launch_epi<Tile<1, NT, 8, 1, 2, 1>, PREC>(s, p, amode, epi);
+    return launch_epi<Tile<1, NT, 8, 1, 1, 1>, PREC>(s, p, amode, epi);
   }
-  return launch_epi<Tile<1, NT, 4, 1, 1, 1>, BF>(s, p, amode, epi);
+  return launch_epi<Tile<1, NT, 4, 1, 1, 1>, PREC>(s, p, amode, epi);
 }
 
 template <int NT>
@@ -596,5 +692,9 @@ int launch_cin_nt(hipStream_t s, GemmArgs& p) {
 
 
 int launch_tower_bf16(hipStream_t s, GemmArgs& p, int nt, int amode, Epi epi);
+// kPrecS3 (k_gemm_s3.hip): tower layers with Npad % 208 == 0, CIN layers with Npad == 208
+constexpr int kS3BN = 208;
+int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi);
+int launch_cin_s3(hipStream_t s, GemmArgs& p);
 
 }  // namespace rmx

@@ -9,7 +9,7 @@ namespace rmx {
 int launch_tower_bf16(hipStream_t s, GemmArgs& p, int nt, int amode, Epi epi) {
   switch (nt) {
 #define RMX_NT(n) \
-  case n: return launch_tower_nt<n, true>(s, p, amode, epi);
+  case n: return launch_tower_nt<n, kPrecBF16>(s, p, amode, epi);
     RMX_NT(1) RMX_NT(2) RMX_NT(3) RMX_NT(4) RMX_NT(5) RMX_NT(6) RMX_NT(7)
     RMX_NT(8) RMX_NT(10) RMX_NT(13) RMX_NT(16) RMX_NT(20) RMX_NT(25) RMX_NT(26)
 #undef RMX_NT

@@ -1,0 +1,116 @@
+// k_gemm_s3.hip -- fp32 tower / CIN GEMMs on the bf16 matrix cores through an exact 3-way split
+// (k_gemm.hpp kPrecS3), gfx950.
+//
+// Why: on gfx950 v_mfma_f32_16x16x4_f32 runs at 64 FLOP/clk/SIMD (157 TF), 1/16 of
+// v_mfma_f32_16x16x32_bf16.  Every normal fp32 x is exactly hi + mid + lo with three bf16 parts
+// (8 significand bits each), so x*y = sum of 9 exact bf16 products; the six kept ones
+// (hi*hi, hi*mid, mid*hi, hi*lo, lo*hi, mid*mid) leave out mid*lo + lo*mid + lo*lo <=
+// (2^-24 + 2^-34) |x y| (|mid| <= 2^-8 |x|, |lo| <= 2^-17 |x|): the size of one rounding of the
+// fp32 FMA chain the reference's MKL sgemm (and our f32 MFMA path) performs per product.
+// Six bf16 MFMAs cost 96 cycles per 16x16x32 tile step against 256 for eight f32 MFMAs.
+// Parity is checked against the fp64 oracle at the same 1e-5 bar as the f32 path
+// (tests/test_gpu_parity.py, test_split_gemm.py); rmx_set_tuning("f32_split", 0) selects the
+// f32 MFMA engine.
+//
+// The semantics are those of k_gemm.hip (HigherOrderEncoder.scala:34-59 tower layers,
+// CINEncoder.scala:36-58 / 105-176 CIN layers); only the arithmetic of the K reduction differs.
+#include "k_gemm.hpp"
+
+namespace rmx {
+
+bool f32_split_enabled() { return tuning_get("f32_split", 1) != 0; }
+
+int64_t split3_elems(int n16, int Npad) { return (int64_t)((n16 + 1) / 2) * 3 * Npad * 32; }
+
+// fp32 packed [n16][Npad][16] -> [steps][3][Npad][32] bf16 (steps = ceil(n16 / 2)).  Position
+// 8g + 4h + q of a 32-wide step holds element 4g + q of fp32 chunk 2s + h: the K order in which
+// lane group g of the split A fragment holds its values (k_gemm.hpp compute_step_s3).
+__global__ void pack_split3_kernel(const float* __restrict__ Wp, int n16, int Npad, int64_t tot,
+                                   bf16_t* __restrict__ W3) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int pos = (int)(i & 31);
+  const int64_t rest = i >> 5;
+  const int n = (int)(rest % Npad);
+  const int64_t s = rest / Npad;
+  const int g = pos >> 3, h = (pos >> 2) & 1, q = pos & 3;
+  const int64_t c = 2 * s + h;
+  const float v = c < n16 ? Wp[(c * Npad + n) * 16 + 4 * g + q] : 0.f;
+  const bf16_t hi = (bf16_t)v;
+  const float r = v - (float)hi;
+  const bf16_t mid = (bf16_t)r;
+  const bf16_t lo = (bf16_t)(r - (float)mid);
+  const int64_t plane = (int64_t)Npad * 32;
+  const int64_t o = s * 3 * plane + (int64_t)n * 32 + pos;
+  W3[o] = hi;
+  W3[o + plane] = mid;
+  W3[o + 2 * plane] = lo;
+}
+
+int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3) {
+  const int64_t tot = (int64_t)((n16 + 1) / 2) * Npad * 32;
+  if (tot <= 0) return RMX_OK;
+  hipLaunchKernelGGL(pack_split3_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, Wp, n16, Npad, tot,
+                     W3);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// Output head of a layer computed in ny column slices: logit = sum of the slices' partial dots
+// (slice order), then the same combination as the fused epilogue (k_gemm.hpp kEpiOutput).
+__global__ __launch_bounds__(256) void out_finish_kernel(int M, int ny, OutArgs oa) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float y = oa.part[m];
+  for (int j = 1; j < ny; ++j) y += oa.part[(int64_t)j * M + m];
+  if (oa.has_bo) y = y + oa.bo;
+  if (oa.rowsum) {
+    float rs = 0.f;
+    for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
+    y = rs + y;
+  }
+  if (oa.pre2) y = oa.pre2[m] + y;
+  float t = oa.pre ? oa.pre[m] + y : y;
+  t = t + oa.beta;
+  oa.out[m] = 1.0f / (1.0f + expf(-t));
+}
+
+int launch_out_finish(hipStream_t s, int M, int ny, const OutArgs& oa) {
+  if (M <= 0) return RMX_OK;
+  hipLaunchKernelGGL(out_finish_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, ny, oa);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// Tower layer, kPrecS3.  Blocks of 8 waves x 16 (or 32) rows span 208 columns (13 tiles), so a
+// 400-wide layer (Npad 416) runs as 2 column slices; one K step = 32 (A: two fp32 chunks, B: the
+// three bf16 planes) through a 2-deep LDS-DMA ring.  Knob "s3_tower":
+//   0  MT = 1: 56 KiB per stage (128 A rows x 2 + 208 x 3 B rows), 1 block / CU;
+//   1  MT = 2 on dense A (BM = 256, 71 KiB per stage; halves the B fragment reads per MFMA);
+//      gather layers keep MT = 1 (their id tile would not fit) -- the default: DeepFM 400^3 at
+//      B = 65,536, layers 2 / 3: 0.125 / 0.117 ms vs 0.136 / 0.128 (MT = 1) and 0.194 / 0.174
+//      on the f32 MFMA engine;
+//   2  MT = 1, register-staged double buffer.
+constexpr int kS3NT = 13;
+
+int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
+  const int var = tuning_get("s3_tower", 1);
+  if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
+  if (var == 1 && amode == kDenseA) return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
+  return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
+}
+
+// CIN layer, kPrecS3 (H <= 208): only the B planes go through LDS (39 KiB per K step); the A
+// operand x0[f] * u[h] is formed in fp32 registers and split there.  Knob "s3_cin":
+//   0  MT = 1, 2-deep LDS-DMA ring;  1  MT = 1, 3-deep ring;  2  MT = 2, 2-deep ring (default:
+//   CIN 200^3 at B = 16,384, layer 2: 3.73 ms vs 4.60 (MT = 1) and 6.69 on the f32 MFMA engine);
+//   3  MT = 1, register-staged double buffer.
+int launch_cin_s3(hipStream_t s, GemmArgs& p) {
+  const int var = tuning_get("s3_cin", 2);
+  if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+  if (var == 2) return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+  if (var == 3) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+  return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+}
+
+}  // namespace rmx

@@ -130,6 +130,14 @@ int dev_alloc(float** p, size_t n) {
   return RMX_OK;
 }
 
+int dev_alloc_bf16(bf16_t** p, int64_t n) {
+  if (hipMalloc(p, sizeof(bf16_t) * (n > 0 ? n : 1)) != hipSuccess) {
+    set_error("out of device memory (" + std::to_string(n * 2) + " bytes)");
+    return RMX_E_NOMEM;
+  }
+  return RMX_OK;
+}
+
 template <class T>
 void dev_free(T*& p) {
   if (p) (void)hipFree(p);
@@ -303,6 +311,7 @@ int model_build(rmx_model& m) {
   if (m.mats_len > 0 && (st = dev_alloc(&m.mats_dev, m.mats_len))) return st;
   for (auto& L : m.layers) {
     if ((st = dev_alloc(&L.W, (size_t)L.Kpad * L.Npad))) return st;
+    if ((st = dev_alloc_bf16(&L.W3, split3_elems(L.Kpad / kChunk, L.Npad)))) return st;
     if ((st = dev_alloc(&L.b, L.Npad))) return st;
   }
   if (!m.layers.empty()) {
@@ -310,6 +319,7 @@ int model_build(rmx_model& m) {
   }
   for (auto& c : m.cin_layers) {
     if ((st = dev_alloc(&c.W, (size_t)c.Hp_pad * m.F * c.Npad))) return st;
+    if ((st = dev_alloc_bf16(&c.W3, split3_elems(c.Hp_pad / kChunk * m.F, c.Npad)))) return st;
     if ((st = dev_alloc(&c.b, c.Npad))) return st;
     if ((st = dev_alloc(&c.wo, c.Npad))) return st;
   }
@@ -387,11 +397,13 @@ void model_release(rmx_model& m) {
   for (auto& L : m.layers) {
     dev_free(L.W);
     dev_free(L.W16);
+    dev_free(L.W3);
     dev_free(L.b);
   }
   dev_free(m.wo);
   for (auto& c : m.cin_layers) {
     dev_free(c.W);
+    dev_free(c.W3);
     dev_free(c.b);
     dev_free(c.wo);
   }
@@ -408,6 +420,7 @@ void model_release(rmx_model& m) {
   dev_free(m.ubuf[0]);
   dev_free(m.ubuf[1]);
   dev_free(m.rowdot);
+  dev_free(m.opart);
   dev_free(m.la_E);
   dev_free(m.la_w);
   dev_free(m.la_E16);
@@ -440,6 +453,7 @@ int model_set_precision(rmx_model& m, int dtype) {
   for (auto& L : m.layers) {
     dev_free(L.W);
     dev_free(L.W16);
+    dev_free(L.W3);
     L.Kpad = round_up(L.K, dtype == kBF16 ? 32 : kChunk);
     if (dtype == kBF16) {
       if (hipMalloc(&L.W16, sizeof(bf16_t) * (size_t)L.Kpad * L.Npad) != hipSuccess) {
@@ -448,6 +462,7 @@ int model_set_precision(rmx_model& m, int dtype) {
       }
     } else {
       int st = dev_alloc(&L.W, (size_t)L.Kpad * L.Npad);
+      if (!st) st = dev_alloc_bf16(&L.W3, split3_elems(L.Kpad / kChunk, L.Npad));
       if (st) return st;
     }
   }
@@ -468,8 +483,10 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   if (m.mats_len > 0)
     RMX_HIP(hipMemcpyAsync(m.mats_dev, host_mats, sizeof(float) * m.mats_len, hipMemcpyHostToDevice, s));
   int st;
-  for (auto& L : m.layers)
+  for (auto& L : m.layers) {
     if ((st = launch_pack_linear(s, m.mats_dev, L))) return st;
+    if (L.W3 && (st = launch_pack_split3(s, L.W, L.Kpad / kChunk, L.Npad, L.W3))) return st;
+  }
   if (!m.layers.empty()) {
     const auto& last = m.layers.back();
     if ((st = copy_slice(s, m.mats_dev + m.wo_off, last.N, last.Npad, m.wo))) return st;
@@ -477,6 +494,7 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   }
   for (auto& c : m.cin_layers) {
     if ((st = launch_pack_cin(s, m.mats_dev, m.F, c))) return st;
+    if (c.W3 && (st = launch_pack_split3(s, c.W, c.Hp_pad / kChunk * m.F, c.Npad, c.W3))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.b_off, c.H, c.Npad, c.b))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.wo_off, c.H, c.Npad, c.wo))) return st;
   }
@@ -521,12 +539,15 @@ int ensure_ws(rmx_model& m, int B) {
   dev_free(m.ubuf[0]);
   dev_free(m.ubuf[1]);
   dev_free(m.rowdot);
+  dev_free(m.opart);
   int st;
   int maxN = 16;
   for (auto& L : m.layers) maxN = std::max(maxN, L.Npad);
   if (!m.layers.empty()) {
     if ((st = dev_alloc(&m.h[0], (size_t)B * maxN))) return st;
     if ((st = dev_alloc(&m.h[1], (size_t)B * maxN))) return st;
+    // partial logits of an output layer run in column slices (k_gemm_s3.hip)
+    if ((st = dev_alloc(&m.opart, (size_t)B * (m.layers.back().Npad / 208 + 1)))) return st;
   }
   if ((st = dev_alloc(&m.y12, B))) return st;
   if ((st = dev_alloc(&m.pre2, B))) return st;
@@ -634,6 +655,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   oa.pre = pre;
   oa.beta = in.beta;
   oa.out = in.out;
+  oa.part = m.opart;
   const float* A = nullptr;
   int lda = 0;
   AGatherArgs ga{in.ids, (const float*)in.table, F, k};

@@ -59,6 +59,7 @@ struct DenseLayer {
   int64_t w_off_x = -1, w_off_o = -1;
   float* W = nullptr;   // device, packed fp32 [Kpad/16][Npad][16]
   bf16_t* W16 = nullptr;  // device, packed bf16 [Kpad/32][Npad][32] (bf16 models; W unused then)
+  bf16_t* W3 = nullptr;   // device, fp32 W split into 3 bf16 planes [ceil(Kpad/32)][3][Npad][32] (kPrecS3)
   float* b = nullptr;   // device [Npad]
 };
 
@@ -89,6 +90,7 @@ struct OutArgs {
   int rowsum_k;
   float beta;            // global bias
   float* out;            // [M] probabilities
+  float* part;           // [Npad / BN][M] partial logits when the layer spans several column blocks
 };
 
 // Raw extra columns of a layer (DenseLayer::N1): written unrounded in fp32 to ptr[m * ld + (n - n_main)].
@@ -116,6 +118,12 @@ int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const void* wtab
 int launch_convert_bf16(hipStream_t s, const float* src, int64_t n, bf16_t* dst);
 int launch_widen_bf16(hipStream_t s, const bf16_t* src, int64_t n, float* dst);
 int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L);
+// fp32 packed [n16][Npad][16] -> the three bf16 planes of the split GEMM (k_gemm_s3.hip)
+int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3);
+int64_t split3_elems(int n16, int Npad);  // bf16 elements of W3
+bool f32_split_enabled();                 // rmx_set_tuning("f32_split") (default on)
+// partial logits [ny][M] -> head combination + sigmoid
+int launch_out_finish(hipStream_t s, int M, int ny, const OutArgs& oa);
 int launch_transpose_kmajor(hipStream_t s, const float* src_kv, int64_t V, int k, void* dst_vk, int dt);
 
 }  // namespace rmx

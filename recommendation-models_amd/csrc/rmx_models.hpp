@@ -53,6 +53,7 @@ struct CinLayer {
   float* W = nullptr;
   float* b = nullptr;
   float* wo = nullptr;  // [Npad] slice of the output Linear for this layer's pooled maps
+  bf16_t* W3 = nullptr;  // kPrecS3 planes of W (k_gemm_s3.hip)
 };
 
 }  // namespace rmx
@@ -97,6 +98,7 @@ struct rmx_model {
   float* xbuf = nullptr;              // [B][Kpad0] materialised A (PNN [x | ip], generic k)
   float* ubuf[2] = {nullptr, nullptr};  // [B*k][Npad] CIN maps
   float* rowdot = nullptr;            // [B*k] CIN per-row output partials
+  float* opart = nullptr;             // [slices][B] partial logits of a column-sliced output layer
   // L-A staging
   int64_t la_nnz = 0;
   int la_B = 0;
