@@ -335,33 +335,39 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
     const float* Bt = cur + AROWS * 16;  // planes [3][BN] of 64-B rows
-    constexpr int GS = 4;                // column tiles whose B fragments are in flight together
+    // the three plane fragments of column tile t
+    auto ldb = [&](int t, f32x4* b) {
+      const int row = (bt0 + t) * 16 + r16;
+      const int o = row * 16 + swz_slot(row, g) * 4;
+      b[0] = *reinterpret_cast<const f32x4*>(Bt + o);
+      b[1] = *reinterpret_cast<const f32x4*>(Bt + BN * 16 + o);
+      b[2] = *reinterpret_cast<const f32x4*>(Bt + 2 * BN * 16 + o);
+    };
+    // software pipeline: the fragments of tile t + PF are read while tile t's MFMAs run, so each
+    // MFMA group waits only for its own reads (counted lgkmcnt), not for a drained LDS queue
+    constexpr int PF = 2;
+    f32x4 bq[PF + 1][3];
 #pragma unroll
-    for (int j0 = 0; j0 < NTW; j0 += GS) {
-      f32x4 bh[GS], bm[GS], bl[GS];
+    for (int t = 0; t < PF && t < NTW; ++t) ldb(t, bq[t]);
 #pragma unroll
-      for (int t = 0; t < GS; ++t)
-        if (j0 + t < NTW) {
-          const int row = (bt0 + j0 + t) * 16 + r16;
-          const int o = row * 16 + swz_slot(row, g) * 4;
-          bh[t] = *reinterpret_cast<const f32x4*>(Bt + o);
-          bm[t] = *reinterpret_cast<const f32x4*>(Bt + BN * 16 + o);
-          bl[t] = *reinterpret_cast<const f32x4*>(Bt + 2 * BN * 16 + o);
-        }
+    for (int t = 0; t < NTW; ++t) {
+      if (t + PF < NTW) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tile's MFMAs
+      const f32x4* b = bq[t % (PF + 1)];
+      const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
+      const bf16x8 bm = __builtin_bit_cast(bf16x8, b[1]);
+      const bf16x8 bl = __builtin_bit_cast(bf16x8, b[2]);
 #pragma unroll
-      for (int t = 0; t < GS; ++t)
-        if (j0 + t < NTW)
-#pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            f32x4 d = acc[i][j0 + t];
-            // smallest terms first
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], __builtin_bit_cast(bf16x8, bm[t]), d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], __builtin_bit_cast(bf16x8, bh[t]), d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(bf16x8, bl[t]), d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], __builtin_bit_cast(bf16x8, bh[t]), d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(bf16x8, bm[t]), d, 0, 0, 0);
-            acc[i][j0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], __builtin_bit_cast(bf16x8, bh[t]), d, 0, 0, 0);
-          }
+      for (int i = 0; i < MT; ++i) {
+        f32x4 d = acc[i][t];
+        // smallest terms first
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, d, 0, 0, 0);
+        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, d, 0, 0, 0);
+      }
     }
   };
 

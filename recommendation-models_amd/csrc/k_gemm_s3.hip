@@ -96,7 +96,11 @@ constexpr int kS3NT = 13;
 int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   const int var = tuning_get("s3_tower", 1);
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
-  if (var == 1 && amode == kDenseA) return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
+  // MT = 2 only while its blocks still cover every CU (M = 16,384 x 400: 128 blocks of 256 rows
+  // ran 0.055 ms vs 0.038 with 256 blocks of 128 rows)
+  const int64_t blocks2 = (int64_t)(p.M + 255) / 256 * (p.Npad / (kS3NT * 16));
+  if (var == 1 && amode == kDenseA && blocks2 >= 256)
+    return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
   return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
 }
 
