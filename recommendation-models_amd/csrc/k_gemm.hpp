@@ -56,6 +56,12 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
+// Diagnostic builds only (tools/diag_build.sh; never set in librmx.so): 1 = no A split,
+// 2 = no per-step barrier, 4 = no MFMAs in the split GEMM.  Results are wrong; timings isolate costs.
+#ifndef RMX_GEMM_DIAG
+#define RMX_GEMM_DIAG 0
+#endif
+
 enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
 enum EpiMode : int { kEpiRelu = 0, kEpiOutput = 1, kEpiCin = 2 };
 
@@ -76,6 +82,7 @@ struct GemmArgs {
   float* rowdot;       // kEpiCin: [M]
   float* xcol;         // kEpiRelu: raw extra columns n >= xn_main -> xcol[m * xld + n - xn_main] (DCN cross)
   int xn_main, xld;
+  int prio;            // 1: the first half of the block's waves issue at raised priority (s_setprio)
 };
 
 // Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
@@ -206,6 +213,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     __syncthreads();
   }
 
+  // Staggered issue (knob "gemm_prio"): waves w and w + NW/2 share a SIMD; giving the first half
+  // priority lets it finish its post-barrier VALU work (A split, addressing) and start its MFMAs
+  // while the partner's VALU runs in the MFMA shadow.
+  if (p.prio && wid < T::NW / 2) __builtin_amdgcn_s_setprio(2);
   f32x4 acc[MT][NTW];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -333,7 +344,15 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     }
     bf16x8 ah[MT], am[MT], al[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
+    for (int i = 0; i < MT; ++i) {
+      if constexpr (RMX_GEMM_DIAG & 1) {
+        ah[i] = __builtin_bit_cast(bf16x8, a0[i]);
+        am[i] = __builtin_bit_cast(bf16x8, a1[i]);
+        al[i] = ah[i];
+      } else {
+        split3(a0[i], a1[i], ah[i], am[i], al[i]);
+      }
+    }
     const float* Bt = cur + AROWS * 16;  // planes [3][BN] of 64-B rows
     // the three plane fragments of column tile t
     auto ldb = [&](int t, f32x4* b) {
@@ -357,6 +376,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
       const bf16x8 bm = __builtin_bit_cast(bf16x8, b[1]);
       const bf16x8 bl = __builtin_bit_cast(bf16x8, b[2]);
+      if constexpr (RMX_GEMM_DIAG & 4) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][t] += b[0] + b[1] + b[2] + __builtin_bit_cast(f32x4, ah[i]);
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         f32x4 d = acc[i][t];
@@ -466,7 +490,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
       vm_wait(younger * my_n);                             // this wave's DMAs of chunk c have landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // and its reads of chunk c - 1 are done
-      __builtin_amdgcn_s_barrier();                        // ... for every wave
+      if constexpr (!(RMX_GEMM_DIAG & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave
       if (c + RING - 1 < nchunks) issue(c + RING - 1);     // refills the buffer of chunk c - 1
       compute_chunk(smem + (c % RING) * STAGE, 0, c);
     }

@@ -95,6 +95,7 @@ constexpr int kS3NT = 13;
 
 int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   const int var = tuning_get("s3_tower", 1);
+  p.prio = tuning_get("gemm_prio", 0);
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
   // MT = 2 only while its blocks still cover every CU (M = 16,384 x 400: 128 blocks of 256 rows
   // ran 0.055 ms vs 0.038 with 256 blocks of 128 rows)
@@ -111,6 +112,7 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 //   3  MT = 1, register-staged double buffer.
 int launch_cin_s3(hipStream_t s, GemmArgs& p) {
   const int var = tuning_get("s3_cin", 2);
+  p.prio = tuning_get("gemm_prio", 0);
   if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   if (var == 2) return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   if (var == 3) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kCinOuter, kEpiCin, kPrecS3>(s, p);
