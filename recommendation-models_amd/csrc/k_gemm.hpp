@@ -172,11 +172,23 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   float* extra = smem + T::NBUF * STAGE;  // gather: int ids [BM][F]; CIN: x0 [BM][XS]
   int* sids = reinterpret_cast<int*>(extra);
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wid through readfirstlane: the compiler then treats everything derived from it as scalar
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int M = p.M;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // XCD-aware block order for a layer in two column slices (kPrecS3, N = 400): blocks are dealt to
+  // the 8 XCDs round-robin in linear order, so linear ids L and L + 8 land on the same XCD back to
+  // back; map them to the two slices of one M block so the second slice's A rows (gathered table
+  // rows or the previous activations) come from that XCD's L2 instead of HBM.
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (gridDim.y == 2 && (gridDim.x & 7) == 0) {
+    const int L = blockIdx.x + blockIdx.y * gridDim.x;
+    const int j = L >> 3;
+    by = j & 1;
+    bx = (j >> 1) * 8 + (L & 7);
+  }
+  const int m0 = bx * BM;
+  const int n0 = by * BN;
   const int nchunks = p.Kpad / KC;
   const int nstages = (nchunks + BKC - 1) / BKC;
   const int F = p.ga.F;
@@ -471,6 +483,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     constexpr int NINS = ROWS / 16;
     constexpr int IPW = (NINS + NW - 1) / NW;
     const int my_n = wid < NINS ? (NINS - 1 - wid) / NW + 1 : 0;  // DMAs this wave issues per chunk
+    // A wave's instructions are the same every step (ins is wave-uniform), so the A / B region
+    // and the chunk / plane of an instruction are scalar; dense A and B sources are a 32-bit
+    // per-lane element offset plus a per-step stride (launch_cfg checks M * lda < 2^32).
     auto issue = [&](int c) {
       float* buf = smem + (c % RING) * STAGE;
 #pragma unroll
@@ -478,9 +493,32 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         const int ins = wid + q * NW;
         if (ins < NINS) {
           const int row = ins * 16 + (lane >> 2), ps = lane & 3;
-          const int lrow = row < AROWS ? row % BM : (row - AROWS) % BN;
-          const void* src = src_of(row, swz_slot(lrow, ps), c);
-          if (!src) src = g_rmx_zero16;
+          const void* src;
+          if (ins * 16 < AROWS) {
+            const int cc = ins * 16 / BM;
+            const int r = row - cc * BM, g = swz_slot(r, ps);
+            if constexpr (AMODE == kDenseA) {
+              const int m = m0 + r, kk = c * KC + cc * KCA + g * KSA;
+              const uint32_t o = (uint32_t)m * (uint32_t)p.lda + (uint32_t)kk;
+              src = (m < M && kk < p.K) ? (BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + o)
+                                             : (const void*)(p.A + o))
+                                        : (const void*)g_rmx_zero16;
+            } else {
+              src = src_of(row, g, c);
+              if (!src) src = g_rmx_zero16;
+            }
+          } else {
+            const int cc = (ins * 16 - AROWS) / BN;
+            const int n = row - AROWS - cc * BN, g = swz_slot(n, ps);
+            if constexpr (S3) {
+              src = reinterpret_cast<const bf16_t*>(p.Wp) +
+                    ((uint32_t)((c * 3 + cc) * p.Npad + n0 + n) * 32u + (uint32_t)(g * 8));
+            } else {
+              src = BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.Wp) +
+                                       ((uint32_t)(c * p.Npad + n0 + n) * 32u + (uint32_t)(g * 8)))
+                       : (const void*)(p.Wp + ((uint32_t)(c * p.Npad + n0 + n) * 16u + (uint32_t)(g * 4)));
+            }
+          }
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
         }
       }
@@ -598,7 +636,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       } else {
         const OutArgs& oa = p.oa;
         if (gridDim.y > 1) {  // a column slice of the layer: partial logit, out_finish_kernel combines
-          oa.part[(int64_t)blockIdx.y * M + m] = y;
+          oa.part[(int64_t)by * M + m] = y;
           continue;
         }
         if (oa.has_bo) y = y + oa.bo;
@@ -643,6 +681,10 @@ int launch_cfg(hipStream_t s, GemmArgs& p) {
   }
   if (p.Npad % T::BN) {
     set_error("gemm: Npad " + std::to_string(p.Npad) + " is not a multiple of the block width");
+    return RMX_E_INVALID;
+  }
+  if (T::RING > 0 && AMODE == kDenseA && (int64_t)p.M * p.lda >= (int64_t)1 << 32) {
+    set_error("gemm: batch too large for one launch (M * lda >= 2^32 elements)");
     return RMX_E_INVALID;
   }
   if (EPI == kEpiCin && p.Npad != T::BN) {

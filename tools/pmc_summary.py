@@ -53,7 +53,7 @@ def load(d):
 
 def stage_of(kernel):
     """bench.py stage name of a kernel (template signature -> stage)."""
-    m = re.search(r"gemm_kernel<Tile<[^>]*>, (\d+), (\d+), (true|false)>", kernel)
+    m = re.search(r"gemm_kernel<Tile<[^>]*>, (\d+), (\d+), (true|false|\d+)>", kernel)
     if m:
         amode, epi = int(m.group(1)), int(m.group(2))
         if amode == 3:
