@@ -120,9 +120,20 @@ static int tower_nt_for(int Npad) {
   return best;
 }
 
+static bool use_s3(const DenseLayer& L) { return L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0; }
+
+bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* ga) {
+  return ga && ga->k == 16 && ga->F <= kFmMaxF && !L.W16 && use_s3(L) && tuning_get("fm_fuse", 1) != 0;
+}
+
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
-                       const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa, const XColArgs* xc) {
+                       const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa, const XColArgs* xc,
+                       const FmArgs* fm) {
   if (M <= 0) return RMX_OK;
+  if (fm && (epi != Epi::kReluStore || !tower_fm_fusable(L, ga))) {
+    set_error("gemm: the fused first order + FM needs a gathered split-GEMM layer 1");
+    return RMX_E_INVALID;
+  }
   const int nt = tower_nt_for(L.Npad);
   if (epi == Epi::kOutput && nt * 16 != L.Npad) {
     // too wide for one block: store the ReLU activations, then a separate head pass
@@ -160,7 +171,11 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
   }
   const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
   if (L.W16) return launch_tower_bf16(s, p, nt, amode, epi);
-  if (L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0 && (epi != Epi::kOutput || L.Npad == kS3BN || oa->part)) {
+  if (fm) {
+    p.fm_w = fm->w;
+    p.fm_y = fm->y;
+  }
+  if (use_s3(L) && (epi != Epi::kOutput || L.Npad == kS3BN || oa->part)) {
     // fp32 layer on the bf16 matrix cores through the exact 3-way split (k_gemm_s3.hip)
     p.Wp = reinterpret_cast<const float*>(L.W3);
     p.Kpad = (L.Kpad / 16 + 1) / 2 * 32;

@@ -83,7 +83,30 @@ struct GemmArgs {
   float* xcol;         // kEpiRelu: raw extra columns n >= xn_main -> xcol[m * xld + n - xn_main] (DCN cross)
   int xn_main, xld;
   int prio;            // 1: the first half of the block's waves issue at raised priority (s_setprio)
+  // DeepFM first order + FM fused into tower layer 1 (kGatherK16 + kPrecS3, column slice 0): the A
+  // tiles that stream through LDS are the gathered field rows, so the FM sums ride along and
+  // fm_y[m] = y1 + y2 (bit-identical to encoder_k16_kernel<1>: same fp32 order, no contraction).
+  const float* fm_w;   // first-order weights [V]
+  float* fm_y;         // [M], nullptr = off
 };
+
+constexpr int kFmMaxF = 40;  // fused FM: fields per sample it handles (F = 39 at the headline config)
+
+// FM sums of one A fragment pair (fields 2c, 2c + 1; j = 4g .. 4g + 3): s += e, q += e * e in field
+// order, without FMA contraction (SecondOrderEncoder.scala:19-34, the oracle's order)
+__device__ __forceinline__ void fm_accum(const f32x4& a0, const f32x4& a1, f32x4& fs, f32x4& fq) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    fs[t] = fs[t] + a0[t];
+    fq[t] = fq[t] + a0[t] * a0[t];
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    fs[t] = fs[t] + a1[t];
+    fq[t] = fq[t] + a1[t] * a1[t];
+  }
+}
 
 // Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
 // tiles); the block spans BM = WM*MT*16 rows and BN = WN*NTW*16 columns.  BKC 16-wide K chunks per
@@ -229,6 +252,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // priority lets it finish its post-barrier VALU work (A split, addressing) and start its MFMAs
   // while the partner's VALU runs in the MFMA shadow.
   if (p.prio && wid < T::NW / 2) __builtin_amdgcn_s_setprio(2);
+  constexpr bool FM = AMODE == kGatherK16 && S3 && EPI == kEpiRelu;
+  const bool fm_on = FM && p.fm_y != nullptr && by == 0;
+  f32x4 fm_s[FM ? MT : 1], fm_q[FM ? MT : 1];
+#pragma unroll
+  for (int i = 0; i < (FM ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc[MT][NTW];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -350,6 +378,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         a0[i] = *reinterpret_cast<const f32x4*>(cur + o);
         a1[i] = *reinterpret_cast<const f32x4*>(cur + BM * 16 + o);
       }
+      if constexpr (FM)
+        if (fm_on)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
     } else {
       cin_a(0, 2 * c, a0);
       cin_a(1, 2 * c + 1, a1);
@@ -574,6 +606,38 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       __syncthreads();
     }
   };
+  if constexpr (FM) {
+    if (fm_on) {
+      // y2 = 0.5 * (sum_j (s_j^2 - q_j) / k), j sequential over the four lane groups; y1 = sum_f w in
+      // field order (encoder_k16_kernel<1> arithmetic); one lane per row writes y1 + y2
+#pragma clang fp contract(off)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        float d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) d[t] = fm_s[i][t] * fm_s[i][t] - fm_q[i][t];
+        float a = 0.f;
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) a += __shfl(d[t], gg * 16 + r16);
+        // y1: lane group g loads the weights of fields g, g + 4, ...; they are summed in field order
+        // (loading them before the main loop measured slower: it holds 10 more registers through it)
+        float wv[kFmMaxF / 4];
+#pragma unroll
+        for (int u = 0; u < kFmMaxF / 4; ++u) {
+          const int f = u * 4 + g;
+          wv[u] = f < F ? p.fm_w[sids[arow[i] * F + f]] : 0.f;
+        }
+        float y1 = 0.f;
+#pragma unroll
+        for (int f = 0; f < kFmMaxF; ++f)
+          if (f < F) y1 += __shfl(wv[f >> 2], (f & 3) * 16 + r16);
+        const int m = m0 + arow[i];
+        if (g == 0 && m < M) p.fm_y[m] = y1 + 0.5f * (a / 16.0f);
+      }
+    }
+  }
   if constexpr (EPI == kEpiRelu) {
     if (p.xcol) {  // DCN: the cross dot products ride along as extra raw columns
 #pragma unroll

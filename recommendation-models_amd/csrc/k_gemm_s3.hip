@@ -87,7 +87,8 @@ int launch_out_finish(hipStream_t s, int M, int ny, const OutArgs& oa) {
 // three bf16 planes) through a 2-deep LDS-DMA ring.  Knob "s3_tower":
 //   0  MT = 1: 56 KiB per stage (128 A rows x 2 + 208 x 3 B rows), 1 block / CU;
 //   1  MT = 2 on dense A (BM = 256, 71 KiB per stage; halves the B fragment reads per MFMA);
-//      gather layers keep MT = 1 (their id tile would not fit) -- the default: DeepFM 400^3 at
+//      gather layers keep MT = 1 (their id tile would not fit beside the ring; streaming the ids
+//      through registers instead measured slower, and spilled at MT = 2) -- the default: DeepFM 400^3 at
 //      B = 65,536, layers 2 / 3: 0.125 / 0.117 ms vs 0.136 / 0.128 (MT = 1) and 0.194 / 0.174
 //      on the f32 MFMA engine;
 //   2  MT = 1, register-staged double buffer.

@@ -632,9 +632,15 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out);
   }
 
-  // 1. first order (+ FM for DeepFM)
+  // 1. first order (+ FM for DeepFM; fused into tower layer 1 when it gathers through the split GEMM)
   const float* pre = nullptr;
-  if (m.type == RMX_MODEL_DEEPFM) {
+  AGatherArgs ga{in.ids, (const float*)in.table, F, k};
+  bool gather_first = !needs_gather_x(m);
+  const bool fm_fused = m.type == RMX_MODEL_DEEPFM && !in.y1 && in.dtype == kF32 && gather_first &&
+                        m.layers.size() > 1 && tower_fm_fusable(m.layers[0], &ga);
+  if (fm_fused) {
+    pre = m.y12;
+  } else if (m.type == RMX_MODEL_DEEPFM) {
     StageTimer t(m, s, "encoder_fm");
     st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr);
     pre = m.y12;
@@ -658,8 +664,6 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   oa.part = m.opart;
   const float* A = nullptr;
   int lda = 0;
-  AGatherArgs ga{in.ids, (const float*)in.table, F, k};
-  bool gather_first = !needs_gather_x(m);
 
   if (m.type == RMX_MODEL_XDEEPFM) {
     const float* uprev = nullptr;
@@ -707,9 +711,10 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
     XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
+    FmArgs fm{(const float*)in.wtab, m.y12};
     st = launch_tower_layer(s, L, B, A, lda, (i == 0 && gather_first) ? &ga : nullptr, C, L.Npad,
                             last ? Epi::kOutput : Epi::kReluStore, last ? &oa : nullptr,
-                            (i == 0 && m.dcn_fused) ? &xc : nullptr);
+                            (i == 0 && m.dcn_fused) ? &xc : nullptr, (i == 0 && fm_fused) ? &fm : nullptr);
     if (st) return st;
     if (i == 0 && m.dcn_fused && (st = launch_cross_finish(s, B, m.cross_depth, m.xcol, m.cross_scalars, m.pre2)))
       return st;

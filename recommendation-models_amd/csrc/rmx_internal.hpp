@@ -99,9 +99,17 @@ struct XColArgs {
   int n_main, ld;
 };
 
+// DeepFM first order + FM computed by tower layer 1 while its A rows stream through LDS
+struct FmArgs {
+  const float* w;  // first-order weights [V] (fp32 table)
+  float* y;        // [M] y1 + y2
+};
+
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa,
-                       const XColArgs* xc = nullptr);
+                       const XColArgs* xc = nullptr, const FmArgs* fm = nullptr);
+// true when launch_tower_layer(L, gather, kReluStore) can compute the FmArgs outputs
+bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* gather);
 
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);

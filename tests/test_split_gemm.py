@@ -35,8 +35,8 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k in ("f32_split", "s3_tower", "s3_cin"):
-        rmx.set_tuning(k, {"f32_split": 1, "s3_tower": 1, "s3_cin": 2}[k])
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1}.items():
+        rmx.set_tuning(k, v)
 
 
 def _model(kind, V):
@@ -148,3 +148,16 @@ def test_split_host_arrays_path(ctx):
     got = m.forward(B, rmx.CooLongFloatMatrix(index, ids), bias, w, e, K, mats, m.getMatsSize())
     ref = oc.forward(oc.make_model(oc.DEEPFM, F, K, fc=(400, 400, 400)), B, index, bias, w, e, mats, 1)
     assert np.abs(np.asarray(got) - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("B", [1, 300, 4099])
+def test_fused_fm_bitwise_equals_encoder(ctx, B):
+    """DeepFM's first order + FM computed inside tower layer 1 (fm_fuse, the default) gives the same
+    bits as the standalone encoder kernel (itself bit-exact to the oracle's y1 + y2)."""
+    run, ref64 = _case(ctx, "deepfm", B)
+    rmx.set_tuning("fm_fuse", 0)
+    p_enc = run()
+    rmx.set_tuning("fm_fuse", 1)
+    p_fused = run()
+    assert np.array_equal(p_fused, p_enc)
+    assert np.abs(p_fused - ref64).max() <= TOL
