@@ -62,6 +62,21 @@ __device__ __forceinline__ void vm_wait(int n) {
 #define RMX_GEMM_DIAG 0
 #endif
 
+#if RMX_GEMM_DIAG & 8
+// per-phase cycle sums of one wave (block 0, wave 0) of the last split-GEMM launch (tools/diag_phases.py)
+__device__ unsigned long long g_rmx_diag_t[8];
+#define RMX_TMARK(k)                                                             \
+  do {                                                                           \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
+    if (dmark) dsum[k] += _t - dlast;                                            \
+    dlast = _t;                                                                  \
+  } while (0)
+#else
+#define RMX_TMARK(k) \
+  do {               \
+  } while (0)
+#endif
+
 enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
 enum EpiMode : int { kEpiRelu = 0, kEpiOutput = 1, kEpiCin = 2 };
 
@@ -258,6 +273,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < (FM ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc[MT][NTW];
+#if RMX_GEMM_DIAG & 8
+  const bool dmark = blockIdx.x == 0 && blockIdx.y == 0 && wid == 0;
+  unsigned long long dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dlast = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -369,7 +388,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 
   // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
   // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
-  auto compute_step_s3 = [&](const float* cur, int c) {
+  // DMA instructions per wave per stage (ring kernels); kPrecS3 spreads them over the MFMA tiles
+  constexpr int kIPW = (ROWS / 16 + T::NW - 1) / T::NW;
+  auto compute_step_s3 = [&](const float* cur, int c, auto&& dma) {
     f32x4 a0[MT], a1[MT];
     if constexpr (A_LDS) {
 #pragma unroll
@@ -386,6 +407,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       cin_a(0, 2 * c, a0);
       cin_a(1, 2 * c + 1, a1);
     }
+    RMX_TMARK(3);  // 3: A fragments (LDS reads / CIN generation)
     bf16x8 ah[MT], am[MT], al[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -397,6 +419,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         split3(a0[i], a1[i], ah[i], am[i], al[i]);
       }
     }
+    RMX_TMARK(4);  // 4: split
     const float* Bt = cur + AROWS * 16;  // planes [3][BN] of 64-B rows
     // the three plane fragments of column tile t
     auto ldb = [&](int t, f32x4* b) {
@@ -415,6 +438,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
       if (t + PF < NTW) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
+      // one of the next stage's DMA instructions per tile: a DMA issue can stall the wave for ~200
+      // cycles (vector-memory queue), which here overlaps the partner wave's MFMAs instead of
+      // idling the SIMD in a separate post-barrier phase
+      if (t < kIPW) dma(t);
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tile's MFMAs
       const f32x4* b = bq[t % (PF + 1)];
       const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
@@ -437,12 +464,15 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, d, 0, 0, 0);
       }
     }
+#pragma unroll
+    for (int q = NTW; q < kIPW; ++q) dma(q);
+    RMX_TMARK(5);  // 5: MFMA section (issue)
   };
 
   // one K chunk c of the stage image at `cur` (chunk slot cc inside the stage)
   auto compute_chunk = [&](const float* cur, int cc, int c) {
     if constexpr (S3) {
-      compute_step_s3(cur, c);
+      compute_step_s3(cur, c, [](int) {});
     } else {
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
       f32x4 a[MT];
@@ -518,12 +548,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     // A wave's instructions are the same every step (ins is wave-uniform), so the A / B region
     // and the chunk / plane of an instruction are scalar; dense A and B sources are a 32-bit
     // per-lane element offset plus a per-step stride (launch_cfg checks M * lda < 2^32).
-    auto issue = [&](int c) {
+    auto issue_one = [&](int c, int q) {
       float* buf = smem + (c % RING) * STAGE;
-#pragma unroll
-      for (int q = 0; q < IPW; ++q) {
+      {
         const int ins = wid + q * NW;
-        if (ins < NINS) {
+        if (q < IPW && ins < NINS) {
           const int row = ins * 16 + (lane >> 2), ps = lane & 3;
           const void* src;
           if (ins * 16 < AROWS) {
@@ -555,15 +584,38 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         }
       }
     };
+    auto issue = [&](int c) {
+#pragma unroll
+      for (int q = 0; q < IPW; ++q) issue_one(c, q);
+    };
     for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
     for (int c = 0; c < nchunks; ++c) {
       const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
+      RMX_TMARK(6);  // 6: MFMA issue tail of the previous step (+ prologue)
       vm_wait(younger * my_n);                             // this wave's DMAs of chunk c have landed
+      RMX_TMARK(0);  // 0: DMA wait
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // and its reads of chunk c - 1 are done
       if constexpr (!(RMX_GEMM_DIAG & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave
-      if (c + RING - 1 < nchunks) issue(c + RING - 1);     // refills the buffer of chunk c - 1
-      compute_chunk(smem + (c % RING) * STAGE, 0, c);
+      RMX_TMARK(1);  // 1: barrier
+      const int cn = c + RING - 1;  // the stage refilled into the buffer of chunk c - 1
+      if constexpr (S3) {
+        RMX_TMARK(2);
+        compute_step_s3(smem + (c % RING) * STAGE, c, [&](int q) {
+          if (cn < nchunks) issue_one(cn, q);
+        });
+      } else {
+        if (cn < nchunks) issue(cn);
+        RMX_TMARK(2);  // 2: DMA issue
+        compute_chunk(smem + (c % RING) * STAGE, 0, c);
+      }
     }
+    RMX_TMARK(6);
+#if RMX_GEMM_DIAG & 8
+    if (dmark && lane == 0) {
+      for (int k = 0; k < 7; ++k) g_rmx_diag_t[k] = dsum[k];
+      g_rmx_diag_t[7] = nchunks;
+    }
+#endif
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }

@@ -121,3 +121,12 @@ int launch_cin_s3(hipStream_t s, GemmArgs& p) {
 }
 
 }  // namespace rmx
+
+#if RMX_GEMM_DIAG & 8
+// diagnostic builds only: the per-phase cycle sums of the last split-GEMM launch
+extern "C" int rmx_diag_phases(unsigned long long* out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 8) == hipSuccess
+             ? 0
+             : -5;
+}
+#endif

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Per-phase cycles of one wave of the split GEMM (diagnostic build: tools/diag_build.sh 8, then
+RMX_LIB=build/diag8/librmx.so python tools/diag_phases.py --workload xdeepfm|deepfm).  Runs one
+forward, then after each stage reads g_rmx_diag_t (block 0, wave 0 of that launch)."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "recommendation-models_amd"))
+import rmx  # noqa: E402
+
+NAMES = ["dma_wait", "barrier", "dma_issue", "a_frag", "split", "mfma_section", "mfma_tail+prologue"]
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="xdeepfm")
+ap.add_argument("--batch", type=int, default=0)
+a = ap.parse_args()
+F, K, V = 39, 16, 1_000_000
+ctx = rmx.default_context()
+if a.workload == "xdeepfm":
+    m, B = rmx.XDeepFM(V, F, K, [400, 400, 400], [200, 200, 200]), a.batch or 16384
+else:
+    m, B = rmx.DeepFM(V, F, K, [400, 400, 400]), a.batch or 65536
+m.setMats(m.initMats(0x3A75))
+m.setBias(0.01)
+t = rmx.EmbeddingTable(ctx, V, K)
+t.fill_synthetic(0x7AB1E)
+ids = rmx.DeviceArray(ctx, B * F, np.int32)
+rmx.gen_ids(ctx, 0x5EED2026, 0, B, F, V, ids)
+out = rmx.DeviceArray(ctx, B, np.float32)
+for _ in range(3):
+    m.forward_ids(t, B, ids, out)
+ctx.sync()
+buf = (ctypes.c_ulonglong * 8)()
+assert rmx._lib.lib.rmx_diag_phases(buf) == 0
+v = list(buf)
+steps = v[7]
+tot = sum(v[:7])
+print("last split-GEMM launch (%s): %d K steps, block 0 wave 0" % (a.workload, steps))
+for n, x in zip(NAMES, v[:7]):
+    print("  %-20s %12d cycles  %6.0f /step  %5.1f %%" % (n, x, x / max(steps, 1), 100.0 * x / max(tot, 1)))
