@@ -470,9 +470,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   };
 
   // one K chunk c of the stage image at `cur` (chunk slot cc inside the stage)
-  auto compute_chunk = [&](const float* cur, int cc, int c) {
+  // dma(q): issue this wave's q-th DMA instruction of the next stage (ring kernels), spread over the
+  // MFMA groups so its issue stall overlaps MFMAs (a no-op for the register-staged pipeline)
+  auto compute_chunk = [&](const float* cur, int cc, int c, auto&& dma) {
     if constexpr (S3) {
-      compute_step_s3(cur, c, [](int) {});
+      compute_step_s3(cur, c, dma);
     } else {
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
       f32x4 a[MT];
@@ -490,6 +492,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
         const int j0 = gi * NTW / NG, j1 = (gi + 1) * NTW / NG;
+#pragma unroll
+        for (int q = gi * kIPW / NG; q < (gi + 1) * kIPW / NG; ++q) dma(q);
         f32x4 b[8];
 #pragma unroll
         for (int t = 0; t < 8; ++t)
@@ -532,7 +536,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       for (int cc = 0; cc < BKC; ++cc) {
         const int c = st * BKC + cc;
         if (BKC > 1 && c >= nchunks) break;
-        compute_chunk(cur, cc, c);
+        compute_chunk(cur, cc, c, [](int) {});
       }
       if (more) sstore(nxt);
       __syncthreads();
@@ -598,16 +602,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       if constexpr (!(RMX_GEMM_DIAG & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave
       RMX_TMARK(1);  // 1: barrier
       const int cn = c + RING - 1;  // the stage refilled into the buffer of chunk c - 1
-      if constexpr (S3) {
-        RMX_TMARK(2);
-        compute_step_s3(smem + (c % RING) * STAGE, c, [&](int q) {
-          if (cn < nchunks) issue_one(cn, q);
-        });
-      } else {
-        if (cn < nchunks) issue(cn);
-        RMX_TMARK(2);  // 2: DMA issue
-        compute_chunk(smem + (c % RING) * STAGE, 0, c);
-      }
+      RMX_TMARK(2);
+      compute_chunk(smem + (c % RING) * STAGE, 0, c, [&](int q) {
+        if (cn < nchunks) issue_one(cn, q);
+      });
     }
     RMX_TMARK(6);
 #if RMX_GEMM_DIAG & 8
