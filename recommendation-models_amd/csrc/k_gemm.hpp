@@ -846,7 +846,10 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // LDS-DMA ring fit 2 blocks per CU (one block's epilogue overlaps the other's MFMAs): fp32
   // 0.280 / 0.183 ms for layers 1 / 2 vs 0.288 / 0.189 (variant 3), bf16 DCN 457 vs 431 M ex/s; the
   // fp32 output layer prefers 32 rows per wave (variant 5: 0.171 vs 0.177 ms)
-  const int def = NT == 26 ? ((epi == Epi::kOutput && PREC == kPrecF32) ? 5 : 4) : (kEven ? 3 : 0);
+  // bf16 layers with a long K (PNN layer 1: K = 624 + 741) prefer the 16-wave 3-deep ring
+  // (0.098 vs 0.119 ms at B = 65,536)
+  const int def = NT == 26 ? ((epi == Epi::kOutput && PREC == kPrecF32) ? 5 : (PREC == kPrecBF16 && p.K >= 1024 ? 3 : 4))
+                           : (kEven ? 3 : 0);
   int var = tuning_get("tower_variant", def);
   if (p.M >= 65536) {
     if constexpr (kEven) {
