@@ -43,6 +43,9 @@ __device__ __forceinline__ int swz_slot(int row, int g) { return g ^ ((4 - ((row
 
 // 16 zero bytes: the LDS-DMA source of out-of-range rows / K padding (a DMA always writes its slot)
 static __device__ __attribute__((aligned(16))) float g_rmx_zero16[4];
+// id -1 (a zero row): the LDS-DMA source of out-of-range entries of the id ring
+static __device__ __attribute__((aligned(16))) int g_rmx_neg1[4] = {-1, -1, -1, -1};
+
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
 __device__ __forceinline__ void vm_wait(int n) {
@@ -148,6 +151,11 @@ struct Tile {
 //              is split in registers.
 enum Prec : int { kPrecF32 = 0, kPrecBF16 = 1, kPrecS3 = 2 };
 
+// kPrecS3 layer-1 gathers with an explicit id array: the ids of the next stages stream into a small
+// LDS ring by DMA (2 slots x 2 fields x BM) instead of a [BM][F] id tile, so a BM = 256 ring fits
+template <class T, int AMODE, int PREC>
+constexpr bool kIdRing = AMODE == kGatherK16 && PREC == kPrecS3 && T::RING == 2 && T::MT == 2;
+
 template <class T, int AMODE, int PREC = kPrecF32>
 struct StageGeom {
   // kPrecS3: one stage = one 32-wide K step: A as two fp32 16-wide chunks [2][BM], B as the three
@@ -231,7 +239,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   const int nstages = (nchunks + BKC - 1) / BKC;
   const int F = p.ga.F;
 
-  if constexpr (AMODE == kGatherK16 || AMODE == kGatherAny) {
+  constexpr bool IDRING = kIdRing<T, AMODE, PREC>;
+  int* idring = reinterpret_cast<int*>(extra);  // IDRING: [2 slots][2 fields][BM] ids
+  if constexpr ((AMODE == kGatherK16 || AMODE == kGatherAny) && !IDRING) {
     for (int i = tid; i < BM * F; i += NTHR) {
       const int r = i / F, f = i - r * F;
       const int m = m0 + r;
@@ -389,7 +399,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
   // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
   // DMA instructions per wave per stage (ring kernels); kPrecS3 spreads them over the MFMA tiles
-  constexpr int kIPW = (ROWS / 16 + T::NW - 1) / T::NW;
+  constexpr int kQID = IDRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;  // id-ring DMAs per wave
+  constexpr int kIPW = kQID + (ROWS / 16 + T::NW - 1) / T::NW;
   auto compute_step_s3 = [&](const float* cur, int c, auto&& dma) {
     f32x4 a0[MT], a1[MT];
     if constexpr (A_LDS) {
@@ -568,6 +579,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
               src = (m < M && kk < p.K) ? (BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + o)
                                              : (const void*)(p.A + o))
                                         : (const void*)g_rmx_zero16;
+            } else if constexpr (IDRING) {
+              const int id = idring[((c & 1) * 2 + cc) * BM + r];
+              src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)g_rmx_zero16;
             } else {
               src = src_of(row, g, c);
               if (!src) src = g_rmx_zero16;
@@ -592,6 +606,25 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int q = 0; q < IPW; ++q) issue_one(c, q);
     };
+    // IDRING: the ids of fields 2c, 2c + 1 for the block's rows -> slot c & 1 (one dword per lane)
+    auto issue_id = [&](int c, int q) {
+      const int ins = wid + q * NW;
+      if (ins < 2 * BM / 64) {
+        const int v = ins * 64 + lane, part = v / BM, r = v - part * BM, m = m0 + r, f = 2 * c + part;
+        const void* src = (m < M && f < F) ? (const void*)(p.ga.ids + (int64_t)m * F + f) : (const void*)g_rmx_neg1;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(idring + (c & 1) * 2 * BM + ins * 64),
+                                         4, 0, 0);
+      }
+    };
+    if constexpr (IDRING) {
+#pragma unroll
+      for (int q = 0; q < kQID; ++q) {
+        issue_id(0, q);
+        if (nchunks > 1) issue_id(1, q);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
     for (int c = 0; c < nchunks; ++c) {
       const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
@@ -604,7 +637,14 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       const int cn = c + RING - 1;  // the stage refilled into the buffer of chunk c - 1
       RMX_TMARK(2);
       compute_chunk(smem + (c % RING) * STAGE, 0, c, [&](int q) {
-        if (cn < nchunks) issue_one(cn, q);
+        if (q < kQID) {
+          // ids of step c + 2 into the slot of step c (its last reader, the issue of stage c,
+          // ran before this step's barrier)
+          if constexpr (IDRING)
+            if (c + 2 < nchunks) issue_id(c + 2, q);
+        } else if (cn < nchunks) {
+          issue_one(cn, q - kQID);
+        }
       });
     }
     RMX_TMARK(6);
@@ -677,7 +717,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int u = 0; u < kFmMaxF / 4; ++u) {
           const int f = u * 4 + g;
-          wv[u] = f < F ? p.fm_w[sids[arow[i] * F + f]] : 0.f;
+          int id = 0;
+          if (f < F) {
+            if constexpr (IDRING) id = p.ga.ids[(int64_t)(m0 + arow[i] < M ? m0 + arow[i] : m0) * F + f];
+            else id = sids[arow[i] * F + f];
+          }
+          wv[u] = f < F ? p.fm_w[id] : 0.f;
         }
         float y1 = 0.f;
 #pragma unroll
@@ -785,7 +830,15 @@ template <class T, int AMODE, int EPI, int PREC = kPrecF32>
 int launch_cfg(hipStream_t s, GemmArgs& p) {
   using SG = StageGeom<T, AMODE, PREC>;
   size_t lds = sizeof(float) * T::NBUF * SG::FLOATS;
-  if (AMODE == kGatherK16 || AMODE == kGatherAny) lds += sizeof(int) * T::BM * p.ga.F;
+  if (kIdRing<T, AMODE, PREC>) {
+    if (!p.ga.ids) {
+      set_error("gemm: the id-ring gather needs an explicit id array");
+      return RMX_E_INVALID;
+    }
+    lds += sizeof(int) * 4 * T::BM;
+  } else if (AMODE == kGatherK16 || AMODE == kGatherAny) {
+    lds += sizeof(int) * T::BM * p.ga.F;
+  }
   if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
   if (EPI != kEpiOutput) lds = std::max(lds, sizeof(float) * EpiGeom<T, SG::FLOATS>::FLOATS);
   lds = std::max(lds, sizeof(float) * T::WN * T::BM);  // row-reduction partials

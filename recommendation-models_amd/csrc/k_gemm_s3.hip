@@ -86,9 +86,9 @@ int launch_out_finish(hipStream_t s, int M, int ny, const OutArgs& oa) {
 // 400-wide layer (Npad 416) runs as 2 column slices; one K step = 32 (A: two fp32 chunks, B: the
 // three bf16 planes) through a 2-deep LDS-DMA ring.  Knob "s3_tower":
 //   0  MT = 1: 56 KiB per stage (128 A rows x 2 + 208 x 3 B rows), 1 block / CU;
-//   1  MT = 2 on dense A (BM = 256, 71 KiB per stage; halves the B fragment reads per MFMA);
-//      gather layers keep MT = 1 (their id tile would not fit beside the ring; streaming the ids
-//      through registers instead measured slower, and spilled at MT = 2) -- the default: DeepFM 400^3 at
+//   1  MT = 2 (BM = 256, 71 KiB per stage; halves the B fragment reads per MFMA) on dense A and on
+//      k = 16 gathers with an id array (ids by DMA into a 4 KiB LDS ring: a [BM][F] id tile would
+//      not fit; streaming them through registers measured slower and spilled) -- the default: DeepFM 400^3 at
 //      B = 65,536, layers 2 / 3: 0.125 / 0.117 ms vs 0.136 / 0.128 (MT = 1) and 0.194 / 0.174
 //      on the f32 MFMA engine;
 //   2  MT = 1, register-staged double buffer.
@@ -101,7 +101,8 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // MT = 2 only while its blocks still cover every CU (M = 16,384 x 400: 128 blocks of 256 rows
   // ran 0.055 ms vs 0.038 with 256 blocks of 128 rows)
   const int64_t blocks2 = (int64_t)(p.M + 255) / 256 * (p.Npad / (kS3NT * 16));
-  if (var == 1 && amode == kDenseA && blocks2 >= 256)
+  // k = 16 gathers with an id array take MT = 2 too (their ids stream through an LDS ring)
+  if (var == 1 && (amode == kDenseA || (amode == kGatherK16 && p.ga.ids)) && blocks2 >= 256)
     return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
   return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
 }

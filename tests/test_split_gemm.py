@@ -150,7 +150,7 @@ def test_split_host_arrays_path(ctx):
     assert np.abs(np.asarray(got) - ref).max() <= TOL
 
 
-@pytest.mark.parametrize("B", [1, 300, 4099])
+@pytest.mark.parametrize("B", [1, 300, 4099, 40000])  # 40000: BM = 256 tiles (id ring), ragged tail
 def test_fused_fm_bitwise_equals_encoder(ctx, B):
     """DeepFM's first order + FM computed inside tower layer 1 (fm_fuse, the default) gives the same
     bits as the standalone encoder kernel (itself bit-exact to the oracle's y1 + y2)."""
