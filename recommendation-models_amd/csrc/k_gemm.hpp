@@ -284,7 +284,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   for (int i = 0; i < (FM ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc[MT][NTW];
 #if RMX_GEMM_DIAG & 8
-  const bool dmark = blockIdx.x == 0 && blockIdx.y == 0 && wid == 0;
+  // DIAG & 16: only CIN launches record (xDeepFM's last split-GEMM launch is a tower layer)
+  const bool dmark = blockIdx.x == 0 && blockIdx.y == 0 && wid == 0 && (!(RMX_GEMM_DIAG & 16) || AMODE == kCinOuter);
   unsigned long long dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dlast = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll
@@ -381,20 +382,30 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     cur_hc[h] = hc;
   };
   // CIN A fragment of 16-wide chunk c16 (= hc * F + f): a = x0[row][f] * u[row][16 hc + 4 g ..]
-  auto cin_a = [&](int h, int c16, f32x4* a) {
+  auto cin_x0 = [&](int c16, float* xv) {  // the x0 scalars of chunk c16 (LDS)
+    const int f = c16 - (c16 / F) * F;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) xv[i] = c16 * 16 < p.K ? extra[arow[i] * p.XS + f] : 0.f;
+  };
+  auto cin_a_x = [&](int h, int c16, const float* xv, f32x4* a) {
     if (c16 * 16 >= p.K) {
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       return;
     }
-    const int hc = c16 / F, f = c16 - hc * F;
+    const int hc = c16 / F;
     if (hc != cur_hc[h]) load_u(h, hc);
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const float xv = extra[arow[i] * p.XS + f];
-      a[i] = f32x4{xv * uf[h][i].x, xv * uf[h][i].y, xv * uf[h][i].z, xv * uf[h][i].w};
-    }
+    for (int i = 0; i < MT; ++i)
+      a[i] = f32x4{xv[i] * uf[h][i].x, xv[i] * uf[h][i].y, xv[i] * uf[h][i].z, xv[i] * uf[h][i].w};
   };
+  auto cin_a = [&](int h, int c16, f32x4* a) {
+    float xv[MT];
+    cin_x0(c16, xv);
+    cin_a_x(h, c16, xv, a);
+  };
+  // kPrecS3: the x0 scalars of the next K step, read during this step's MFMAs (x0 is static in LDS)
+  float x0q[2][MT];
 
   // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
   // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
@@ -415,8 +426,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
           for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
     } else {
-      cin_a(0, 2 * c, a0);
-      cin_a(1, 2 * c + 1, a1);
+      if (c == 0) {
+        cin_x0(0, x0q[0]);
+        cin_x0(1, x0q[1]);
+      }
+      cin_a_x(0, 2 * c, x0q[0], a0);
+      cin_a_x(1, 2 * c + 1, x0q[1], a1);
     }
     RMX_TMARK(3);  // 3: A fragments (LDS reads / CIN generation)
     bf16x8 ah[MT], am[MT], al[MT];
@@ -453,6 +468,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       // cycles (vector-memory queue), which here overlaps the partner wave's MFMAs instead of
       // idling the SIMD in a separate post-barrier phase
       if (t < kIPW) dma(t);
+      if constexpr (!A_LDS)
+        if (t == 0) {
+          cin_x0(2 * c + 2, x0q[0]);
+          cin_x0(2 * c + 3, x0q[1]);
+        }
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tile's MFMAs
       const f32x4* b = bq[t % (PF + 1)];
       const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
@@ -649,7 +669,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     }
     RMX_TMARK(6);
 #if RMX_GEMM_DIAG & 8
-    if (dmark && lane == 0) {
+    if (dmark && lane == 0 && nchunks > 100) {  // (DIAG & 16: CIN layers 2+, K = F * 208)
       for (int k = 0; k < 7; ++k) g_rmx_diag_t[k] = dsum[k];
       g_rmx_diag_t[7] = nchunks;
     }
