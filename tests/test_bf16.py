@@ -125,3 +125,32 @@ def test_bf16_rejects_mismatched_table_and_xdeepfm():
     x = rmx.XDeepFM(1000, F, K, [8], [8])
     with pytest.raises(rmx.RmxError):
         x.setPrecision(rmx.DTYPE_BF16)
+
+
+@pytest.mark.parametrize("kind", ["dcn", "pnn"])
+def test_bf16_bench_batch_matches_bf16_oracle(kind):
+    """B = 65,536 (the bench batch): the large-batch tower variants (8/16-wave LDS-DMA rings, the
+    long-K PNN layer 1) against the bf16 oracle on a head and a tail slice of the batch."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 50_003, 65536
+    m, om = _model(kind, V)
+    t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16)
+    t.fill_synthetic(SEED_TAB)
+    mats = oc.round_bf16(m.initMats(SEED_MATS))
+    m.setPrecision(rmx.DTYPE_BF16)
+    m.setMats(mats)
+    m.setBias(0.01)
+    ids_d = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_d)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(t, B, ids_d, out)
+    ctx.sync()
+    got = out.numpy()
+    wt, et = _rounded_table(V)
+    for r0, n in ((0, 512), (B - 300, 300)):
+        ids = oc.gen_ids(SEED_IDS, r0, n, F, V).astype(np.int64)
+        w, e = oc.gather(wt, et, 1, ids)
+        index = np.repeat(np.arange(n, dtype=np.int64), F)
+        ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 2)
+        assert np.abs(got[r0:r0 + n] - ref).max() <= TOL_BF16
