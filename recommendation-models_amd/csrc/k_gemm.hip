@@ -122,15 +122,17 @@ static int tower_nt_for(int Npad) {
 
 static bool use_s3(const DenseLayer& L) { return L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0; }
 
-bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* ga) {
-  return ga && ga->k == 16 && ga->F <= kFmMaxF && !L.W16 && use_s3(L) && tuning_get("fm_fuse", 1) != 0;
+bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* ga, bool sums) {
+  // every k = 16 gather kernel has the first-order epilogue; the FM sums need fp32 A fragments
+  // (the split GEMM)
+  return ga && ga->k == 16 && ga->F <= kFmMaxF && tuning_get("fm_fuse", 1) != 0 && (!sums || (!L.W16 && use_s3(L)));
 }
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa, const XColArgs* xc,
                        const FmArgs* fm) {
   if (M <= 0) return RMX_OK;
-  if (fm && (epi != Epi::kReluStore || !tower_fm_fusable(L, ga))) {
+  if (fm && (epi != Epi::kReluStore || !tower_fm_fusable(L, ga, fm->sums != 0))) {
     set_error("gemm: the fused first order + FM needs a gathered split-GEMM layer 1");
     return RMX_E_INVALID;
   }
@@ -169,12 +171,14 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
     p.xn_main = xc->n_main;
     p.xld = xc->ld;
   }
-  const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
-  if (L.W16) return launch_tower_bf16(s, p, nt, amode, epi);
   if (fm) {
     p.fm_w = fm->w;
+    p.fm_w_bf16 = fm->w_bf16;
+    p.fm_sums = fm->sums;
     p.fm_y = fm->y;
   }
+  const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
+  if (L.W16) return launch_tower_bf16(s, p, nt, amode, epi);
   if (use_s3(L) && (epi != Epi::kOutput || L.Npad == kS3BN || oa->part)) {
     // fp32 layer on the bf16 matrix cores through the exact 3-way split (k_gemm_s3.hip)
     p.Wp = reinterpret_cast<const float*>(L.W3);

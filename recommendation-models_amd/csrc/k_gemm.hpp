@@ -104,7 +104,10 @@ struct GemmArgs {
   // DeepFM first order + FM fused into tower layer 1 (kGatherK16 + kPrecS3, column slice 0): the A
   // tiles that stream through LDS are the gathered field rows, so the FM sums ride along and
   // fm_y[m] = y1 + y2 (bit-identical to encoder_k16_kernel<1>: same fp32 order, no contraction).
-  const float* fm_w;   // first-order weights [V]
+  // Without the FM sums (fm_sums = 0) the same epilogue gives the first order alone (y1, the other
+  // models' Scatter term, bit-identical to encoder_k16_kernel<0>) for any k = 16 gather layer 1.
+  const void* fm_w;    // first-order weights [V] (bf16 when fm_w_bf16)
+  int fm_w_bf16, fm_sums;
   float* fm_y;         // [M], nullptr = off
 };
 
@@ -277,11 +280,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // priority lets it finish its post-barrier VALU work (A split, addressing) and start its MFMAs
   // while the partner's VALU runs in the MFMA shadow.
   if (p.prio && wid < T::NW / 2) __builtin_amdgcn_s_setprio(2);
-  constexpr bool FM = AMODE == kGatherK16 && S3 && EPI == kEpiRelu;
+  constexpr bool FM = AMODE == kGatherK16 && EPI == kEpiRelu;  // first order (+ FM sums on kPrecS3)
+  constexpr bool FMS = FM && S3;
   const bool fm_on = FM && p.fm_y != nullptr && by == 0;
-  f32x4 fm_s[FM ? MT : 1], fm_q[FM ? MT : 1];
+  const bool fm_sums = FMS && fm_on && p.fm_sums;
+  f32x4 fm_s[FMS ? MT : 1], fm_q[FMS ? MT : 1];
 #pragma unroll
-  for (int i = 0; i < (FM ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < (FMS ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc[MT][NTW];
 #if RMX_GEMM_DIAG & 8
   // DIAG & 16: only CIN launches record (xDeepFM's last split-GEMM launch is a tower layer)
@@ -421,8 +426,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         a0[i] = *reinterpret_cast<const f32x4*>(cur + o);
         a1[i] = *reinterpret_cast<const f32x4*>(cur + BM * 16 + o);
       }
-      if constexpr (FM)
-        if (fm_on)
+      if constexpr (FMS)
+        if (fm_sums)
 #pragma unroll
           for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
     } else {
@@ -723,14 +728,18 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma clang fp contract(off)
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
-        float d[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) d[t] = fm_s[i][t] * fm_s[i][t] - fm_q[i][t];
         float a = 0.f;
+        if constexpr (FMS) {
+          if (fm_sums) {
+            float d[4];
 #pragma unroll
-        for (int gg = 0; gg < 4; ++gg)
+            for (int t = 0; t < 4; ++t) d[t] = fm_s[i][t] * fm_s[i][t] - fm_q[i][t];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) a += __shfl(d[t], gg * 16 + r16);
+            for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+              for (int t = 0; t < 4; ++t) a += __shfl(d[t], gg * 16 + r16);
+          }
+        }
         // y1: lane group g loads the weights of fields g, g + 4, ...; they are summed in field order
         // (loading them before the main loop measured slower: it holds 10 more registers through it)
         float wv[kFmMaxF / 4];
@@ -742,14 +751,16 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
             if constexpr (IDRING) id = p.ga.ids[(int64_t)(m0 + arow[i] < M ? m0 + arow[i] : m0) * F + f];
             else id = sids[arow[i] * F + f];
           }
-          wv[u] = f < F ? p.fm_w[id] : 0.f;
+          wv[u] = f < F ? (p.fm_w_bf16 ? (float)reinterpret_cast<const bf16_t*>(p.fm_w)[id]
+                                       : reinterpret_cast<const float*>(p.fm_w)[id])
+                        : 0.f;
         }
         float y1 = 0.f;
 #pragma unroll
         for (int f = 0; f < kFmMaxF; ++f)
           if (f < F) y1 += __shfl(wv[f >> 2], (f & 3) * 16 + r16);
         const int m = m0 + arow[i];
-        if (g == 0 && m < M) p.fm_y[m] = y1 + 0.5f * (a / 16.0f);
+        if (g == 0 && wn == 0 && m < M) p.fm_y[m] = fm_sums ? y1 + 0.5f * (a / 16.0f) : y1;
       }
     }
   }

@@ -636,8 +636,12 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   const float* pre = nullptr;
   AGatherArgs ga{in.ids, (const float*)in.table, F, k};
   bool gather_first = !needs_gather_x(m);
-  const bool fm_fused = m.type == RMX_MODEL_DEEPFM && !in.y1 && in.dtype == kF32 && gather_first &&
-                        m.layers.size() > 1 && tower_fm_fusable(m.layers[0], &ga);
+  // DeepFM on the split GEMM: first order + FM inside tower layer 1; the other models with a
+  // gathered layer 1 (xDeepFM, DCN): the first order there
+  const bool deepfm = m.type == RMX_MODEL_DEEPFM;
+  const bool fm_fused = (deepfm || m.type == RMX_MODEL_XDEEPFM || m.type == RMX_MODEL_DCN) && !in.y1 &&
+                        (!deepfm || in.dtype == kF32) && gather_first && m.layers.size() > 1 &&
+                        tower_fm_fusable(m.layers[0], &ga, deepfm);
   if (fm_fused) {
     pre = m.y12;
   } else if (m.type == RMX_MODEL_DEEPFM) {
@@ -711,7 +715,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
     XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
-    FmArgs fm{(const float*)in.wtab, m.y12};
+    FmArgs fm{in.wtab, in.dtype == kBF16 ? 1 : 0, deepfm ? 1 : 0, m.y12};
     st = launch_tower_layer(s, L, B, A, lda, (i == 0 && gather_first) ? &ga : nullptr, C, L.Npad,
                             last ? Epi::kOutput : Epi::kReluStore, last ? &oa : nullptr,
                             (i == 0 && m.dcn_fused) ? &xc : nullptr, (i == 0 && fm_fused) ? &fm : nullptr);

@@ -99,17 +99,19 @@ struct XColArgs {
   int n_main, ld;
 };
 
-// DeepFM first order + FM computed by tower layer 1 while its A rows stream through LDS
+// First order (+ DeepFM's FM) computed by tower layer 1 while its A rows stream through LDS
 struct FmArgs {
-  const float* w;  // first-order weights [V] (fp32 table)
-  float* y;        // [M] y1 + y2
+  const void* w;   // first-order weights [V] (table element type)
+  int w_bf16;      // 1: bf16 weights
+  int sums;        // 1: y = y1 + y2 (DeepFM, split-GEMM layer 1); 0: y = y1
+  float* y;        // [M]
 };
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa,
                        const XColArgs* xc = nullptr, const FmArgs* fm = nullptr);
-// true when launch_tower_layer(L, gather, kReluStore) can compute the FmArgs outputs
-bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* gather);
+// true when launch_tower_layer(L, gather, kReluStore) can compute the FmArgs outputs (sums: + FM)
+bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* gather, bool sums);
 
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);

@@ -161,3 +161,28 @@ def test_fused_fm_bitwise_equals_encoder(ctx, B):
     p_fused = run()
     assert np.array_equal(p_fused, p_enc)
     assert np.abs(p_fused - ref64).max() <= TOL
+
+
+@pytest.mark.parametrize("kind,bf16", [("xdeepfm", False), ("dcn", False), ("dcn", True)])
+@pytest.mark.parametrize("B", [300, 65536])
+def test_fused_first_order_bitwise(ctx, kind, bf16, B):
+    """xDeepFM / DCN: the first order (Scatter) computed in tower layer 1's epilogue (fm_fuse) gives
+    the same bits as the standalone first-order kernel, fp32 and bf16 tables."""
+    V = 50000
+    m = _model(kind, V)
+    if bf16:
+        m.setPrecision(rmx.DTYPE_BF16)
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    table = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
+    table.fill_synthetic(SEED_TAB)
+    ids_dev = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_dev)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    res = []
+    for fuse in (0, 1):
+        rmx.set_tuning("fm_fuse", fuse)
+        m.forward_ids(table, B, ids_dev, out)
+        ctx.sync()
+        res.append(out.numpy().copy())
+    assert np.array_equal(res[0], res[1])
