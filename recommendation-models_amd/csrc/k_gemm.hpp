@@ -157,7 +157,7 @@ enum Prec : int { kPrecF32 = 0, kPrecBF16 = 1, kPrecS3 = 2 };
 // kPrecS3 layer-1 gathers with an explicit id array: the ids of the next stages stream into a small
 // LDS ring by DMA (2 slots x 2 fields x BM) instead of a [BM][F] id tile, so a BM = 256 ring fits
 template <class T, int AMODE, int PREC>
-constexpr bool kIdRing = AMODE == kGatherK16 && PREC == kPrecS3 && T::RING == 2 && T::MT == 2;
+constexpr bool kIdRing = AMODE == kGatherK16 && PREC == kPrecS3 && T::RING == 2 && T::MT >= 2;
 
 template <class T, int AMODE, int PREC = kPrecF32>
 struct StageGeom {
