@@ -400,6 +400,15 @@ def main():
             **({"predict_auc": pa} if pa else {}),
             "stages": per_stage,
         }
+        if not train:
+            # BASELINE.json asks for the HBM-roofline fraction too: the whole forward's algorithmic
+            # bytes per example (ids + first-order weights + embedding rows + output)
+            es = 2 if bf16 else 4
+            bpe = F * 4 + F * es + F * K * es + 4
+            line["forward_hbm"] = {"algorithmic_bytes_per_example": bpe,
+                                   "gbs": round(value * bpe / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                   "frac": round(value * bpe / 1e9 / PEAK_HBM_GBS, 4),
+                                   "note": "compute-bound: the dense tower / CIN, not the gather, sets the rate"}
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
