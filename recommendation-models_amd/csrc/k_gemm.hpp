@@ -109,6 +109,12 @@ struct GemmArgs {
   const void* fm_w;    // first-order weights [V] (bf16 when fm_w_bf16)
   int fm_w_bf16, fm_sums;
   float* fm_y;         // [M], nullptr = off
+  // kEpiRelu variants for the backward's dX = dPre W (train.hip): raw = store acc (+ bias when
+  // bias != nullptr) without the ReLU; mask [M][ldmask]: zero the entries whose mask is <= 0 (the
+  // ReLU backward of the layer below, fused)
+  int raw;
+  const float* mask;
+  int ldmask;
 };
 
 constexpr int kFmMaxF = 40;  // fused FM: fields per sample it handles (F = 39 at the headline config)
@@ -695,13 +701,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int t = 0; t < NTH; ++t) {
         if (j0 + t >= NTW) break;
-        const float bn = p.bias[n0 + (bt0 + j0 + t) * 16 + r16];
+        const float bn = p.bias ? p.bias[n0 + (bt0 + j0 + t) * 16 + r16] : 0.f;
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = acc[i][j0 + t][r] + bn;
-            wbuf[(i * 16 + g * 4 + r) * LD + t * 16 + r16] = v > 0.f ? v : 0.f;
+            wbuf[(i * 16 + g * 4 + r) * LD + t * 16 + r16] = (p.raw || v > 0.f) ? v : 0.f;
           }
       }
       __syncthreads();
@@ -710,8 +716,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         const int rr = q / nf4, c4 = q - rr * nf4;
         const int m = m0 + wm * RW + rr;
         if (m < M) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(wbuf + rr * LD + c4 * 4);
+          f32x4 v = *reinterpret_cast<const f32x4*>(wbuf + rr * LD + c4 * 4);
           const int64_t o = (int64_t)m * ldd + n0 + (bt0 + j0) * 16 + c4 * 4;
+          if (p.mask) {
+            const f32x4 h = *reinterpret_cast<const f32x4*>(p.mask + (int64_t)m * p.ldmask + n0 + (bt0 + j0) * 16 + c4 * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = h[e] > 0.f ? v[e] : 0.f;
+          }
           if constexpr (BF)
             *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(dst) + o) = __builtin_convertvector(v, bf16x4);
           else

@@ -56,6 +56,56 @@ int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t
   return RMX_OK;
 }
 
+// W^T of a Linear(in = K, out = N) at L.w_off (single block, no extra rows): element (col j, k n) =
+// W[n][j], packed [KTpad/16][NTpad][16] fp32
+__global__ void pack_linear_t_kernel(const float* __restrict__ mats, int64_t w_off, int N, int K, int KTpad,
+                                     int NTpad, float* __restrict__ Wp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)KTpad * NTpad) return;
+  const int kk = (int)(i & 15);
+  const int64_t rest = i >> 4;
+  const int j = (int)(rest % NTpad);
+  const int n = (int)(rest / NTpad) * 16 + kk;
+  Wp[i] = (n < N && j < K) ? mats[w_off + (int64_t)n * K + j] : 0.f;
+}
+
+int launch_pack_linear_t(hipStream_t s, const float* mats_dev, DenseLayer& L) {
+  if (!L.WT) return RMX_OK;
+  const int64_t tot = (int64_t)L.KTpad * L.NTpad;
+  hipLaunchKernelGGL(pack_linear_t_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats_dev, L.w_off,
+                     L.N, L.K, L.KTpad, L.NTpad, L.WT);
+  RMX_HIP(hipGetLastError());
+  return launch_pack_split3(s, L.WT, L.KTpad / 16, L.NTpad, L.WT3);
+}
+
+bool dx_s3_usable(const DenseLayer& L, int ldx) {
+  return L.WT3 && f32_split_enabled() && L.NTpad % kS3BN == 0 && L.NTpad <= ldx;
+}
+
+int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, int lda, float* dx, int ldx,
+                 const float* mask, int ldmask) {
+  if (!dx_s3_usable(L, ldx) || (mask && L.NTpad > ldmask)) {
+    set_error("dx: no split-GEMM W^T for this layer");
+    return RMX_E_INVALID;
+  }
+  if (B <= 0) return RMX_OK;
+  GemmArgs p{};
+  p.M = B;
+  p.K = L.N;
+  p.Kpad = (L.KTpad / 16 + 1) / 2 * 32;
+  p.Npad = L.NTpad;
+  p.A = dpre;
+  p.lda = lda;
+  p.Wp = reinterpret_cast<const float*>(L.WT3);
+  p.bias = nullptr;
+  p.C = dx;
+  p.ldc = ldx;
+  p.raw = 1;
+  p.mask = mask;
+  p.ldmask = ldmask;
+  return launch_tower_s3(s, p, kDenseA, Epi::kReluStore);
+}
+
 // Output head of a layer computed in ny column slices: logit = sum of the slices' partial dots
 // (slice order), then the same combination as the fused epilogue (k_gemm.hpp kEpiOutput).
 __global__ __launch_bounds__(256) void out_finish_kernel(int M, int ny, OutArgs oa) {

@@ -144,6 +144,21 @@ void dev_free(T*& p) {
   p = nullptr;
 }
 
+// W^T planes for the backward's dX on the split GEMM (single-block fp32 layers whose input width
+// pads to a multiple of 208 with at most one extra 16-wide tile, e.g. 400 -> 416, 624; the dX buffer's
+// row stride must also hold NTpad, checked at launch: dx_s3_usable)
+int alloc_wt(DenseLayer& L) {
+  dev_free(L.WT);
+  dev_free(L.WT3);
+  L.KTpad = L.NTpad = 0;
+  if (L.K1 >= 0 || L.N1 >= 0 || round_up(L.K, 208) - round_up(L.K, kChunk) > kChunk) return RMX_OK;
+  L.KTpad = round_up(L.N, kChunk);
+  L.NTpad = round_up(L.K, 208);
+  int st = dev_alloc(&L.WT, (size_t)L.KTpad * L.NTpad);
+  if (!st) st = dev_alloc_bf16(&L.WT3, split3_elems(L.KTpad / kChunk, L.NTpad));
+  return st;
+}
+
 // the GEMM gathers 16-B slots straight from table rows: k must be a multiple of 4 fp32 / 8 bf16
 bool needs_gather_x(const rmx_model& m) { return m.k % (m.precision == kBF16 ? 8 : 4) != 0; }
 
@@ -313,6 +328,7 @@ int model_build(rmx_model& m) {
     if ((st = dev_alloc(&L.W, (size_t)L.Kpad * L.Npad))) return st;
     if ((st = dev_alloc_bf16(&L.W3, split3_elems(L.Kpad / kChunk, L.Npad)))) return st;
     if ((st = dev_alloc(&L.b, L.Npad))) return st;
+    if ((st = alloc_wt(L))) return st;
   }
   if (!m.layers.empty()) {
     if ((st = dev_alloc(&m.wo, m.layers.back().Npad))) return st;
@@ -398,6 +414,8 @@ void model_release(rmx_model& m) {
     dev_free(L.W);
     dev_free(L.W16);
     dev_free(L.W3);
+    dev_free(L.WT);
+    dev_free(L.WT3);
     dev_free(L.b);
   }
   dev_free(m.wo);
@@ -454,6 +472,8 @@ int model_set_precision(rmx_model& m, int dtype) {
     dev_free(L.W);
     dev_free(L.W16);
     dev_free(L.W3);
+    dev_free(L.WT);
+    dev_free(L.WT3);
     L.Kpad = round_up(L.K, dtype == kBF16 ? 32 : kChunk);
     if (dtype == kBF16) {
       if (hipMalloc(&L.W16, sizeof(bf16_t) * (size_t)L.Kpad * L.Npad) != hipSuccess) {
@@ -463,6 +483,7 @@ int model_set_precision(rmx_model& m, int dtype) {
     } else {
       int st = dev_alloc(&L.W, (size_t)L.Kpad * L.Npad);
       if (!st) st = dev_alloc_bf16(&L.W3, split3_elems(L.Kpad / kChunk, L.Npad));
+      if (!st) st = alloc_wt(L);
       if (st) return st;
     }
   }
@@ -486,6 +507,7 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   for (auto& L : m.layers) {
     if ((st = launch_pack_linear(s, m.mats_dev, L))) return st;
     if (L.W3 && (st = launch_pack_split3(s, L.W, L.Kpad / kChunk, L.Npad, L.W3))) return st;
+    if (L.WT && (st = launch_pack_linear_t(s, m.mats_dev, L))) return st;
   }
   if (!m.layers.empty()) {
     const auto& last = m.layers.back();

@@ -60,6 +60,11 @@ struct DenseLayer {
   float* W = nullptr;   // device, packed fp32 [Kpad/16][Npad][16]
   bf16_t* W16 = nullptr;  // device, packed bf16 [Kpad/32][Npad][32] (bf16 models; W unused then)
   bf16_t* W3 = nullptr;   // device, fp32 W split into 3 bf16 planes [ceil(Kpad/32)][3][Npad][32] (kPrecS3)
+  // W^T for the backward's dX = dPre W on the split GEMM (fp32 single-block layers, train.hip):
+  // a Linear(in = N, out = K) packed like W (fp32 [KTpad/16][NTpad][16]) and split into WT3
+  int KTpad = 0, NTpad = 0;
+  float* WT = nullptr;
+  bf16_t* WT3 = nullptr;
   float* b = nullptr;   // device [Npad]
 };
 
@@ -128,6 +133,13 @@ int launch_gather(hipStream_t s, int64_t n, const int32_t* ids, const void* wtab
 int launch_convert_bf16(hipStream_t s, const float* src, int64_t n, bf16_t* dst);
 int launch_widen_bf16(hipStream_t s, const bf16_t* src, int64_t n, float* dst);
 int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L);
+// W^T of a single-block layer into L.WT / L.WT3 (k_gemm_s3.hip)
+int launch_pack_linear_t(hipStream_t s, const float* mats_dev, DenseLayer& L);
+// dX[B][ldx] = dPre[B][lda] W (+ mask: dX *= (mask > 0)), on the split GEMM; RMX_E_INVALID when the
+// layer has no W^T planes (the caller then uses its library GEMM)
+int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, int lda, float* dx, int ldx,
+                 const float* mask, int ldmask);
+bool dx_s3_usable(const DenseLayer& L, int ldx);
 // fp32 packed [n16][Npad][16] -> the three bf16 planes of the split GEMM (k_gemm_s3.hip)
 int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3);
 int64_t split3_elems(int n16, int Npad);  // bf16 elements of W3

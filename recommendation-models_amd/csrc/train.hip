@@ -803,13 +803,23 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       blks[1] = {L.K1, L.K - L.K1, L.w_off2};
       nb = 2;
     }
+    // dX on the split GEMM (W^T planes) when the layer has them, with the ReLU backward of the layer
+    // below fused as a mask; otherwise the library GEMM + relu_back_kernel
+    const float* mask = l > 0 ? T.h[l - 1] : nullptr;
+    const int ldmask = l > 0 ? m.layers[l - 1].Npad : 0;
+    bool masked = false;
     for (int q = 0; q < nb; ++q) {
       const Blk& bk = blks[q];
       if (o.g_mats && (st = wgrad(T, s, B, N, bk.K, dpre, L.Npad, xin + bk.c0, ldin, o.g_mats + bk.w, false)))
         return st;
-      if (need_dx)
+      if (!need_dx) continue;
+      if (nb == 1 && m.precision == kF32 && dx_s3_usable(L, ldin) && (!mask || L.NTpad <= ldmask)) {
+        if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, dxin + bk.c0, ldin, mask, ldmask))) return st;
+        masked = mask != nullptr;
+      } else {
         RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, bk.K, B, N, &one,
                                m.mats_dev + bk.w, bk.K, dpre, L.Npad, &zero, dxin + bk.c0, ldin));
+      }
     }
     if (o.g_mats && L.bias_mode == 1 && (st = colsum(T, s, B, N, dpre, L.Npad, nullptr, o.g_mats + L.b_off, false)))
       return st;
@@ -818,7 +828,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(64), 0, s, N, T.tmp, o.g_mats + L.b_off);
       RMX_HIP(hipGetLastError());
     }
-    if (l > 0) {
+    if (l > 0 && !masked) {
       const DenseLayer& P = m.layers[l - 1];
       const int PN = eff_n(P);
       hipLaunchKernelGGL(relu_back_kernel, dim3(nblk((int64_t)B * PN)), dim3(256), 0, s, B, PN, T.h[l - 1], P.Npad,
