@@ -216,11 +216,29 @@ __global__ __launch_bounds__(256) void product_kernel(int B, int F, int k, const
 // and no LDS.  Each lane writes its x fragment (16 B) and, for row i of its G tile, the pair slots
 // p(i, j) = i(2F-i-1)/2 + j-i-1 of 16 consecutive j (one contiguous segment per 16 lanes).
 // One wave per sample, grid-strided.
+// 16-byte stores of the [x | ip] row: 8 bf16 or 4 fp32 per lane-store
+template <class X>
+struct Vec16;
+template <>
+struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+};
+template <>
+struct Vec16<float> {
+  static constexpr int N = 4;
+};
+
 template <class T, class X, int NTILE>
 __global__ __launch_bounds__(256) void product16_kernel(int B, int F, const int32_t* __restrict__ ids,
                                                         const T* __restrict__ table, X* __restrict__ xbuf, int ldx) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
+  typedef X xvec4 __attribute__((ext_vector_type(4)));
+  // the wave's [ip | zero pad] segment of the row, assembled in LDS and written with 16-B stores
+  // (the pair slots of one G tile row are 2-B scattered writes otherwise)
+  constexpr int kSeg = 64 * 63 / 2 + 32;
+  __shared__ __attribute__((aligned(16))) X seg[4][kSeg];
   const int lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
+  X* sw = seg[threadIdx.x >> 6];
   const int D = F * 16;
   const int P = F * (F - 1) / 2;
   const int nw = gridDim.x * 4;
@@ -233,13 +251,16 @@ __global__ __launch_bounds__(256) void product16_kernel(int B, int F, const int3
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (row < F) {
         v = load4(table + (int64_t)ids[(int64_t)b * F + row] * 16 + g * 4);
-        st1(xr + row * 16 + g * 4 + 0, v.x);
-        st1(xr + row * 16 + g * 4 + 1, v.y);
-        st1(xr + row * 16 + g * 4 + 2, v.z);
-        st1(xr + row * 16 + g * 4 + 3, v.w);
+        xvec4 xv;
+        xv[0] = (X)v.x;
+        xv[1] = (X)v.y;
+        xv[2] = (X)v.z;
+        xv[3] = (X)v.w;
+        *reinterpret_cast<xvec4*>(xr + row * 16 + g * 4) = xv;
       }
       fr[t] = f32x4{v.x, v.y, v.z, v.w};
     }
+    for (int c = P + lane; c < ldx - D; c += 64) sw[c] = (X)0.f;
 #pragma unroll
     for (int I = 0; I < NTILE; ++I)
 #pragma unroll
@@ -251,17 +272,21 @@ __global__ __launch_bounds__(256) void product16_kernel(int B, int F, const int3
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = I * 16 + g * 4 + r;
-          if (i < j && j < F) st1(xr + D + i * (2 * F - i - 1) / 2 + (j - i - 1), acc[r]);
+          if (i < j && j < F) sw[i * (2 * F - i - 1) / 2 + (j - i - 1)] = (X)acc[r];
         }
       }
-    for (int c = D + P + lane; c < ldx; c += 64) st1(xr + c, 0.f);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's LDS writes, before its lanes read them
+    constexpr int VN = Vec16<X>::N;
+    for (int c = lane * VN; c < ldx - D; c += 64 * VN)
+      *reinterpret_cast<float4*>(xr + D + c) = *reinterpret_cast<const float4*>(sw + c);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next sample's writes
   }
 }
 
 int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt,
                    const int32_t* pairs, int P, void* xbuf, int xdt, int ldx) {
   if (B <= 0) return RMX_OK;
-  if (k == 16 && F <= 64 && ids) {
+  if (k == 16 && F <= 64 && ids && ldx - F * 16 <= 64 * 63 / 2 + 32) {
     const int nblk = std::min((B + 3) / 4, 256 * 16);
     const dim3 grid(nblk), blk(256);
 #define RMX_PROD(NTL)                                                                                              \
