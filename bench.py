@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--set", default="", help="kernel knobs before building the model, k=v,k=v (rmx_set_tuning)")
     return ap.parse_args()
 
 
@@ -199,6 +200,9 @@ def main():
         import torch.distributed as dist  # CPU (gloo) barrier / max only: the GPU work is librmx
         dist.init_process_group("gloo")
     import rmx
+    for kv in filter(None, args.set.split(",")):
+        k_, v_ = kv.split("=")
+        rmx.set_tuning(k_, int(v_))
 
     train = args.workload.endswith("_train")
     base = args.workload[:-len("_train")] if train else args.workload

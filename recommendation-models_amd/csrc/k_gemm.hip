@@ -125,7 +125,11 @@ static bool use_s3(const DenseLayer& L) { return L.W3 && f32_split_enabled() && 
 bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* ga, bool sums) {
   // every k = 16 gather kernel has the first-order epilogue; the FM sums need fp32 A fragments
   // (the split GEMM)
-  return ga && ga->k == 16 && ga->F <= kFmMaxF && tuning_get("fm_fuse", 1) != 0 && (!sums || (!L.W16 && use_s3(L)));
+  // knobs: fm_fuse (DeepFM first order + FM, default on: +4 % at the bench), fo_fuse (first order
+  // alone for xDeepFM / DCN, default off: neutral for xDeepFM, -1 % for DCN bf16 at the bench, where
+  // the epilogue's weight gathers miss the caches)
+  if (tuning_get(sums ? "fm_fuse" : "fo_fuse", sums ? 1 : 0) == 0) return false;
+  return ga && ga->k == 16 && ga->F <= kFmMaxF && (!sums || (!L.W16 && use_s3(L)));
 }
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,

@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 0}.items():
         rmx.set_tuning(k, v)
 
 
@@ -166,7 +166,7 @@ def test_fused_fm_bitwise_equals_encoder(ctx, B):
 @pytest.mark.parametrize("kind,bf16", [("xdeepfm", False), ("dcn", False), ("dcn", True)])
 @pytest.mark.parametrize("B", [300, 65536])
 def test_fused_first_order_bitwise(ctx, kind, bf16, B):
-    """xDeepFM / DCN: the first order (Scatter) computed in tower layer 1's epilogue (fm_fuse) gives
+    """xDeepFM / DCN: the first order (Scatter) computed in tower layer 1's epilogue (fo_fuse) gives
     the same bits as the standalone first-order kernel, fp32 and bf16 tables."""
     V = 50000
     m = _model(kind, V)
@@ -181,7 +181,7 @@ def test_fused_first_order_bitwise(ctx, kind, bf16, B):
     out = rmx.DeviceArray(ctx, B, np.float32)
     res = []
     for fuse in (0, 1):
-        rmx.set_tuning("fm_fuse", fuse)
+        rmx.set_tuning("fo_fuse", fuse)
         m.forward_ids(table, B, ids_dev, out)
         ctx.sync()
         res.append(out.numpy().copy())
