@@ -179,6 +179,7 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
     p.fm_w = fm->w;
     p.fm_w_bf16 = fm->w_bf16;
     p.fm_sums = fm->sums;
+    p.fm_add = fm->add;
     p.fm_y = fm->y;
   }
   const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);

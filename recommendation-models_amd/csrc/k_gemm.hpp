@@ -108,6 +108,7 @@ struct GemmArgs {
   // models' Scatter term, bit-identical to encoder_k16_kernel<0>) for any k = 16 gather layer 1.
   const void* fm_w;    // first-order weights [V] (bf16 when fm_w_bf16)
   int fm_w_bf16, fm_sums;
+  int fm_add;          // 1: fm_y already holds y1 (a first-order kernel ran): fm_y = fm_y + y2
   float* fm_y;         // [M], nullptr = off
   // kEpiRelu variants for the backward's dX = dPre W (train.hip): raw = store acc (+ bias when
   // bias != nullptr) without the ReLU; mask [M][ldmask]: zero the entries whose mask is <= 0 (the
@@ -753,6 +754,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         }
         // y1: lane group g loads the weights of fields g, g + 4, ...; they are summed in field order
         // (loading them before the main loop measured slower: it holds 10 more registers through it)
+        const int m = m0 + arow[i];
+        if (p.fm_add) {
+          if (g == 0 && wn == 0 && m < M) p.fm_y[m] = p.fm_y[m] + 0.5f * (a / 16.0f);
+          continue;
+        }
         float wv[kFmMaxF / 4];
 #pragma unroll
         for (int u = 0; u < kFmMaxF / 4; ++u) {
@@ -770,7 +776,6 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int f = 0; f < kFmMaxF; ++f)
           if (f < F) y1 += __shfl(wv[f >> 2], (f & 3) * 16 + r16);
-        const int m = m0 + arow[i];
         if (g == 0 && wn == 0 && m < M) p.fm_y[m] = fm_sums ? y1 + 0.5f * (a / 16.0f) : y1;
       }
     }

@@ -109,6 +109,7 @@ struct FmArgs {
   const void* w;   // first-order weights [V] (table element type)
   int w_bf16;      // 1: bf16 weights
   int sums;        // 1: y = y1 + y2 (DeepFM, split-GEMM layer 1); 0: y = y1
+  int add;         // 1 (with sums): y already holds y1, y = y + y2
   float* y;        // [M]
 };
 
