@@ -251,6 +251,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 
   constexpr bool IDRING = kIdRing<T, AMODE, PREC>;
   int* idring = reinterpret_cast<int*>(extra);  // IDRING: [2 slots][2 fields][BM] ids
+  // IDRING + fused first order: the first-order weights of the same (row, field) pairs ride the same
+  // DMA ring ([2 slots][2 fields][BM] floats after the ids), summed per step in field order
+  float* wring = reinterpret_cast<float*>(extra) + 4 * BM;
   if constexpr ((AMODE == kGatherK16 || AMODE == kGatherAny) && !IDRING) {
     for (int i = tid; i < BM * F; i += NTHR) {
       const int r = i / F, f = i - r * F;
@@ -291,6 +294,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   constexpr bool FMS = FM && S3;
   const bool fm_on = FM && p.fm_y != nullptr && by == 0;
   const bool fm_sums = FMS && fm_on && p.fm_sums;
+  const bool wfuse = IDRING && fm_on && !p.fm_add && !p.fm_w_bf16;
+  float y1acc[FMS ? MT : 1];
+#pragma unroll
+  for (int i = 0; i < (FMS ? MT : 1); ++i) y1acc[i] = 0.f;
   f32x4 fm_s[FMS ? MT : 1], fm_q[FMS ? MT : 1];
 #pragma unroll
   for (int i = 0; i < (FMS ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -422,8 +429,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
   // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
   // DMA instructions per wave per stage (ring kernels); kPrecS3 spreads them over the MFMA tiles
-  constexpr int kQID = IDRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;  // id-ring DMAs per wave
-  constexpr int kIPW = kQID + (ROWS / 16 + T::NW - 1) / T::NW;
+  constexpr int kQID = IDRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;  // id-ring (and w-ring) DMAs per wave
+  constexpr int kIPW = 2 * kQID + (ROWS / 16 + T::NW - 1) / T::NW;
   auto compute_step_s3 = [&](const float* cur, int c, auto&& dma) {
     f32x4 a0[MT], a1[MT];
     if constexpr (A_LDS) {
@@ -437,6 +444,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         if (fm_sums)
 #pragma unroll
           for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
+      if constexpr (IDRING && FMS)
+        if (wfuse)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            y1acc[i] += wring[((c & 1) * 2) * BM + arow[i]];
+            y1acc[i] += wring[((c & 1) * 2 + 1) * BM + arow[i]];
+          }
     } else {
       if (c == 0) {
         cin_x0(0, x0q[0]);
@@ -648,6 +662,17 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                                          4, 0, 0);
       }
     };
+    // the first-order weights of stage c (ids of slot c & 1, landed) -> w slot c & 1
+    auto issue_w = [&](int c, int q) {
+      const int ins = wid + q * NW;
+      if (ins < 2 * BM / 64) {
+        const int v = ins * 64 + lane, part = v / BM, r = v - part * BM;
+        const int id = idring[((c & 1) * 2 + part) * BM + r];
+        const void* src = id >= 0 ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + id) : (const void*)g_rmx_zero16;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + (c & 1) * 2 * BM + ins * 64),
+                                         4, 0, 0);
+      }
+    };
     if constexpr (IDRING) {
 #pragma unroll
       for (int q = 0; q < kQID; ++q) {
@@ -656,6 +681,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (wfuse)
+#pragma unroll
+        for (int q = 0; q < kQID; ++q) issue_w(0, q);
     }
     for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
     for (int c = 0; c < nchunks; ++c) {
@@ -674,8 +702,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
           // ran before this step's barrier)
           if constexpr (IDRING)
             if (c + 2 < nchunks) issue_id(c + 2, q);
+        } else if (q < 2 * kQID) {
+          // weights of stage c + 1 into the w slot of step c - 1 (read before this step's barrier)
+          if constexpr (IDRING)
+            if (wfuse && cn < nchunks) issue_w(cn, q - kQID);
         } else if (cn < nchunks) {
-          issue_one(cn, q - kQID);
+          issue_one(cn, q - 2 * kQID);
         }
       });
     }
@@ -758,6 +790,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         if (p.fm_add) {
           if (g == 0 && wn == 0 && m < M) p.fm_y[m] = p.fm_y[m] + 0.5f * (a / 16.0f);
           continue;
+        }
+        if constexpr (IDRING && FMS) {
+          if (wfuse) {  // y1 summed per K step from the w ring
+            if (g == 0 && wn == 0 && m < M) p.fm_y[m] = fm_sums ? y1acc[i] + 0.5f * (a / 16.0f) : y1acc[i];
+            continue;
+          }
         }
         float wv[kFmMaxF / 4];
 #pragma unroll
@@ -882,7 +920,7 @@ int launch_cfg(hipStream_t s, GemmArgs& p) {
       set_error("gemm: the id-ring gather needs an explicit id array");
       return RMX_E_INVALID;
     }
-    lds += sizeof(int) * 4 * T::BM;
+    lds += sizeof(int) * 8 * T::BM;  // id ring + first-order weight ring
   } else if (AMODE == kGatherK16 || AMODE == kGatherAny) {
     lds += sizeof(int) * T::BM * p.ga.F;
   }

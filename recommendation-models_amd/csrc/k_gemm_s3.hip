@@ -144,15 +144,24 @@ int launch_out_finish(hipStream_t s, int M, int ny, const OutArgs& oa) {
 //   2  MT = 1, register-staged double buffer.
 constexpr int kS3NT = 13;
 
+// the 32-row tile (MT = 2): on dense A and on k = 16 gathers with an id array, while its blocks
+// still cover every CU (M = 16,384 x 400: 128 blocks of 256 rows ran 0.055 ms vs 0.038 with 256
+// blocks of 128 rows)
+static bool s3_mt2(int M, int Npad, int amode, bool ids) {
+  const int64_t blocks2 = (int64_t)(M + 255) / 256 * (Npad / (kS3NT * 16));
+  return tuning_get("s3_tower", 1) == 1 && (amode == kDenseA || (amode == kGatherK16 && ids)) && blocks2 >= 256;
+}
+
+bool tower_s3_idring(const DenseLayer& L, int M, const AGatherArgs* ga) {
+  return ga && ga->k == 16 && ga->ids && L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0 &&
+         s3_mt2(M, L.Npad, kGatherK16, true);
+}
+
 int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   const int var = tuning_get("s3_tower", 1);
   p.prio = tuning_get("gemm_prio", 0);
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
-  // MT = 2 only while its blocks still cover every CU (M = 16,384 x 400: 128 blocks of 256 rows
-  // ran 0.055 ms vs 0.038 with 256 blocks of 128 rows)
-  const int64_t blocks2 = (int64_t)(p.M + 255) / 256 * (p.Npad / (kS3NT * 16));
-  // k = 16 gathers with an id array take MT = 2 too (their ids stream through an LDS ring)
-  if (var == 1 && (amode == kDenseA || (amode == kGatherK16 && p.ga.ids)) && blocks2 >= 256)
+  if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr))
     return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
   return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
 }

@@ -667,7 +667,11 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // the first order by its own kernel (fm_y1 = 0, default) and the FM sums in layer 1: the sums are
   // free there, while summing the first-order weights in layer 1's epilogue exposes their gather
   // latency (bench: 0.213 ms layer 1 vs 0.022 + 0.172; DeepFM 154M -> 161M ex/s)
-  const bool fm_add = fm_fused && deepfm && tuning_get("fm_y1", 0) == 0;
+  // fm_y1: 0 = first-order kernel, 1 = layer 1's epilogue gathers, 2 (default) = summed from the id
+  // ring's weight DMAs when layer 1 runs the id-ring tile (free), else the first-order kernel
+  const int fm_y1 = tuning_get("fm_y1", 2);
+  const bool fm_add = fm_fused && deepfm &&
+                      (fm_y1 == 0 || (fm_y1 == 2 && !tower_s3_idring(m.layers[0], B, &ga)));
   if (fm_add) {
     StageTimer t(m, s, "first_order");
     if ((st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr))) return st;

@@ -141,6 +141,8 @@ int launch_pack_linear_t(hipStream_t s, const float* mats_dev, DenseLayer& L);
 int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, int lda, float* dx, int ldx,
                  const float* mask, int ldmask);
 bool dx_s3_usable(const DenseLayer& L, int ldx);
+// true when gathered layer 1 runs the split GEMM's id-ring tile (which can also sum the first order)
+bool tower_s3_idring(const DenseLayer& L, int M, const AGatherArgs* ga);
 // fp32 packed [n16][Npad][16] -> the three bf16 planes of the split GEMM (k_gemm_s3.hip)
 int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3);
 int64_t split3_elems(int n16, int Npad);  // bf16 elements of W3

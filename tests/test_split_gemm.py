@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 0, "fm_y1": 0}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 0, "fm_y1": 2}.items():
         rmx.set_tuning(k, v)
 
 
@@ -150,7 +150,7 @@ def test_split_host_arrays_path(ctx):
     assert np.abs(np.asarray(got) - ref).max() <= TOL
 
 
-@pytest.mark.parametrize("y1_in_gemm", [0, 1])
+@pytest.mark.parametrize("y1_in_gemm", [0, 1, 2])
 @pytest.mark.parametrize("B", [1, 300, 4099, 40000])  # 40000: BM = 256 tiles (id ring), ragged tail
 def test_fused_fm_bitwise_equals_encoder(ctx, B, y1_in_gemm):
     """DeepFM's FM (and, with fm_y1 = 1, the first order) computed inside tower layer 1 (fm_fuse, the
