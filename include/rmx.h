@@ -79,7 +79,9 @@ int rmx_abi_version(void);
 
 /* Process-wide tuning knobs (kernel variant selection for A/B timing in one process).
  * Known keys: "tower_variant" (see k_tower.hip), "cin_variant" (k_cin.hip).  Unknown keys are
- * stored and ignored.  rmx_get_tuning returns def when the key was never set. */
+ * stored and ignored.  rmx_get_tuning returns def when the key was never set; setting
+ * RMX_TUNING_DEFAULT removes the key (back to the built-in default). */
+#define RMX_TUNING_DEFAULT (-2147483647 - 1)
 int rmx_set_tuning(const char* key, int value);
 int rmx_get_tuning(const char* key, int def);
 

@@ -45,12 +45,15 @@ extern "C" int rmx_set_tuning(const char* key, int value) {
     return RMX_E_INVALID;
   }
   std::lock_guard<std::mutex> lk(g_tune_mu);
-  for (auto& kv : g_tune)
-    if (kv.first == key) {
-      kv.second = value;
+  for (size_t i = 0; i < g_tune.size(); ++i)
+    if (g_tune[i].first == key) {
+      if (value == RMX_TUNING_DEFAULT)
+        g_tune.erase(g_tune.begin() + i);
+      else
+        g_tune[i].second = value;
       return RMX_OK;
     }
-  g_tune.emplace_back(key, value);
+  if (value != RMX_TUNING_DEFAULT) g_tune.emplace_back(key, value);
   return RMX_OK;
 }
 

@@ -122,21 +122,33 @@ static int tower_nt_for(int Npad) {
 
 static bool use_s3(const DenseLayer& L) { return L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0; }
 
-bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* ga, bool sums) {
+bool tower_wring(const DenseLayer& L, int M, const AGatherArgs* ga) {
+  if (!ga || ga->k != 16 || M <= 0) return false;
+  if (L.W16) {  // bf16: the 2-deep ring variants of launch_tower_nt (M >= 65,536, 26 tiles)
+    if (M < 65536 || tower_nt_for(L.Npad) != 26) return false;
+    const int var = tower_variant_for(26, Epi::kReluStore, true, L.K);
+    return var == 4 || var == 5;
+  }
+  return use_s3(L) && tuning_get("s3_tower", 1) != 2;  // every split-GEMM tile but the register-staged one
+}
+
+bool tower_fm_fusable(const DenseLayer& L, int M, const AGatherArgs* ga, bool sums) {
   // every k = 16 gather kernel has the first-order epilogue; the FM sums need fp32 A fragments
-  // (the split GEMM)
-  // knobs: fm_fuse (DeepFM first order + FM, default on: +4 % at the bench), fo_fuse (first order
-  // alone for xDeepFM / DCN, default off: neutral for xDeepFM, -1 % for DCN bf16 at the bench, where
-  // the epilogue's weight gathers miss the caches)
-  if (tuning_get(sums ? "fm_fuse" : "fo_fuse", sums ? 1 : 0) == 0) return false;
-  return ga && ga->k == 16 && ga->F <= kFmMaxF && (!sums || (!L.W16 && use_s3(L)));
+  // (the split GEMM).  Knobs: fm_fuse (DeepFM first order + FM, default on: +4 % at the bench);
+  // fo_fuse (the first order alone, xDeepFM / DCN): 0 off, 1 always, 2 (default) when layer 1
+  // runs a w-ring tile (tower_wring: summed from LDS, free) -- the epilogue's own weight gathers
+  // miss the caches (DCN bf16 -1 % at the bench)
+  if (!ga || ga->k != 16 || ga->F > kFmMaxF) return false;
+  if (sums) return tuning_get("fm_fuse", 1) != 0 && !L.W16 && use_s3(L);
+  const int fo = tuning_get("fo_fuse", 2);
+  return fo == 1 || (fo == 2 && tower_wring(L, M, ga));
 }
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa, const XColArgs* xc,
                        const FmArgs* fm) {
   if (M <= 0) return RMX_OK;
-  if (fm && (epi != Epi::kReluStore || !tower_fm_fusable(L, ga, fm->sums != 0))) {
+  if (fm && (epi != Epi::kReluStore || !tower_fm_fusable(L, M, ga, fm->sums != 0))) {
     set_error("gemm: the fused first order + FM needs a gathered split-GEMM layer 1");
     return RMX_E_INVALID;
   }

@@ -165,6 +165,10 @@ enum Prec : int { kPrecF32 = 0, kPrecBF16 = 1, kPrecS3 = 2 };
 // LDS ring by DMA (2 slots x 2 fields x BM) instead of a [BM][F] id tile, so a BM = 256 ring fits
 template <class T, int AMODE, int PREC>
 constexpr bool kIdRing = AMODE == kGatherK16 && PREC == kPrecS3 && T::RING == 2 && T::MT >= 2;
+// 2-deep ring kernels of k = 16 gathers in 32-wide K steps (two fields per step): the first-order
+// weights of each step's (row, field) pairs can ride the ring ([2 slots][2 fields][BM] elements)
+template <class T, int AMODE, int PREC>
+constexpr bool kWRing = AMODE == kGatherK16 && (PREC == kPrecS3 || PREC == kPrecBF16) && T::RING == 2;
 
 template <class T, int AMODE, int PREC = kPrecF32>
 struct StageGeom {
@@ -251,9 +255,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 
   constexpr bool IDRING = kIdRing<T, AMODE, PREC>;
   int* idring = reinterpret_cast<int*>(extra);  // IDRING: [2 slots][2 fields][BM] ids
-  // IDRING + fused first order: the first-order weights of the same (row, field) pairs ride the same
-  // DMA ring ([2 slots][2 fields][BM] floats after the ids), summed per step in field order
-  float* wring = reinterpret_cast<float*>(extra) + 4 * BM;
+  // WRING + fused first order: the first-order weights of each step's (row, field) pairs ride the
+  // DMA ring ([2 slots][2 fields][BM] table elements after the ids), summed per step in field order
+  constexpr bool WRING = kWRing<T, AMODE, PREC> && EPI == kEpiRelu;
+  float* wring = IDRING ? reinterpret_cast<float*>(extra) + 4 * BM : reinterpret_cast<float*>(sids + BM * F);
   if constexpr ((AMODE == kGatherK16 || AMODE == kGatherAny) && !IDRING) {
     for (int i = tid; i < BM * F; i += NTHR) {
       const int r = i / F, f = i - r * F;
@@ -294,10 +299,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   constexpr bool FMS = FM && S3;
   const bool fm_on = FM && p.fm_y != nullptr && by == 0;
   const bool fm_sums = FMS && fm_on && p.fm_sums;
-  const bool wfuse = IDRING && fm_on && !p.fm_add && !p.fm_w_bf16;
-  float y1acc[FMS ? MT : 1];
+  const bool wfuse = WRING && fm_on && !p.fm_add;
+  float y1acc[WRING ? MT : 1];
 #pragma unroll
-  for (int i = 0; i < (FMS ? MT : 1); ++i) y1acc[i] = 0.f;
+  for (int i = 0; i < (WRING ? MT : 1); ++i) y1acc[i] = 0.f;
   f32x4 fm_s[FMS ? MT : 1], fm_q[FMS ? MT : 1];
 #pragma unroll
   for (int i = 0; i < (FMS ? MT : 1); ++i) fm_s[i] = fm_q[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -379,6 +384,20 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < MT; ++i) arow[i] = wm * MT * 16 + i * 16 + r16;
   const int bt0 = wn * NTW;  // first column tile of this wave
+  // w-ring element e of slot (c & 1): an fp32 weight, or a bf16 one zero-extended to a dword (a
+  // 2-byte LDS DMA writes lane L at base + 4 L, tools/probe/glds_sizes.hip), widened exactly
+  auto wget = [&](int c, int part, int r) -> float {
+    const int e = ((c & 1) * 2 + part) * BM + r;
+    return p.fm_w_bf16 ? __uint_as_float(__float_as_uint(wring[e]) << 16) : wring[e];
+  };
+  // the weights of fields 2c, 2c + 1 of this lane's rows, in field order
+  auto wsum = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < (WRING ? MT : 1); ++i) {
+      y1acc[i] += wget(c, 0, arow[i]);
+      y1acc[i] += wget(c, 1, arow[i]);
+    }
+  };
 
   // kCinOuter: the row's u[h-chunk] for the current hc, reloaded when hc changes (kPrecS3: one
   // cache per half of the 32-wide step, whose two 16-wide chunks may sit in different h-chunks)
@@ -429,8 +448,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
   // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
   // DMA instructions per wave per stage (ring kernels); kPrecS3 spreads them over the MFMA tiles
-  constexpr int kQID = IDRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;  // id-ring (and w-ring) DMAs per wave
-  constexpr int kIPW = 2 * kQID + (ROWS / 16 + T::NW - 1) / T::NW;
+  constexpr int kQID = IDRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;  // id-ring DMAs per wave
+  constexpr int kQW = WRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;    // w-ring DMAs per wave
+  constexpr int kIPW = kQID + kQW + (ROWS / 16 + T::NW - 1) / T::NW;
   auto compute_step_s3 = [&](const float* cur, int c, auto&& dma) {
     f32x4 a0[MT], a1[MT];
     if constexpr (A_LDS) {
@@ -444,13 +464,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         if (fm_sums)
 #pragma unroll
           for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
-      if constexpr (IDRING && FMS)
-        if (wfuse)
-#pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            y1acc[i] += wring[((c & 1) * 2) * BM + arow[i]];
-            y1acc[i] += wring[((c & 1) * 2 + 1) * BM + arow[i]];
-          }
+      if constexpr (WRING)
+        if (wfuse) wsum(c);
     } else {
       if (c == 0) {
         cin_x0(0, x0q[0]);
@@ -540,6 +555,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
           a[i] = *reinterpret_cast<const f32x4*>(At + arow[i] * 16 + swz_slot(arow[i], g) * 4);
+        if constexpr (WRING)
+          if (wfuse) wsum(c);
       } else {
         cin_a(0, c, a);
       }
@@ -662,15 +679,27 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                                          4, 0, 0);
       }
     };
-    // the first-order weights of stage c (ids of slot c & 1, landed) -> w slot c & 1
+    // the first-order weights of stage c (ids of slot c & 1 landed, or the id tile) -> w slot c & 1,
+    // one dword per lane (a 2-byte DMA of a bf16 weight fills the low half, zero-extended)
     auto issue_w = [&](int c, int q) {
       const int ins = wid + q * NW;
       if (ins < 2 * BM / 64) {
         const int v = ins * 64 + lane, part = v / BM, r = v - part * BM;
-        const int id = idring[((c & 1) * 2 + part) * BM + r];
-        const void* src = id >= 0 ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + id) : (const void*)g_rmx_zero16;
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + (c & 1) * 2 * BM + ins * 64),
-                                         4, 0, 0);
+        int id;
+        if constexpr (IDRING) {
+          id = idring[((c & 1) * 2 + part) * BM + r];
+        } else {
+          const int f = 2 * c + part;
+          id = (f < F && m0 + r < M) ? sids[r * F + f] : -1;
+        }
+        const int e = (c & 1) * 2 * BM + ins * 64;
+        if (p.fm_w_bf16) {
+          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const bf16_t*>(p.fm_w) + id) : (const void*)g_rmx_zero16;
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 2, 0, 0);
+        } else {
+          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + id) : (const void*)g_rmx_zero16;
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 4, 0, 0);
+        }
       }
     };
     if constexpr (IDRING) {
@@ -681,10 +710,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+    }
+    if constexpr (WRING)
       if (wfuse)
 #pragma unroll
-        for (int q = 0; q < kQID; ++q) issue_w(0, q);
-    }
+        for (int q = 0; q < kQW; ++q) issue_w(0, q);
     for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
     for (int c = 0; c < nchunks; ++c) {
       const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
@@ -702,12 +732,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
           // ran before this step's barrier)
           if constexpr (IDRING)
             if (c + 2 < nchunks) issue_id(c + 2, q);
-        } else if (q < 2 * kQID) {
+        } else if (q < kQID + kQW) {
           // weights of stage c + 1 into the w slot of step c - 1 (read before this step's barrier)
-          if constexpr (IDRING)
+          if constexpr (WRING)
             if (wfuse && cn < nchunks) issue_w(cn, q - kQID);
         } else if (cn < nchunks) {
-          issue_one(cn, q - 2 * kQID);
+          issue_one(cn, q - kQID - kQW);
         }
       });
     }
@@ -791,7 +821,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
           if (g == 0 && wn == 0 && m < M) p.fm_y[m] = p.fm_y[m] + 0.5f * (a / 16.0f);
           continue;
         }
-        if constexpr (IDRING && FMS) {
+        if constexpr (WRING) {
           if (wfuse) {  // y1 summed per K step from the w ring
             if (g == 0 && wn == 0 && m < M) p.fm_y[m] = fm_sums ? y1acc[i] + 0.5f * (a / 16.0f) : y1acc[i];
             continue;
@@ -923,6 +953,7 @@ int launch_cfg(hipStream_t s, GemmArgs& p) {
     lds += sizeof(int) * 8 * T::BM;  // id ring + first-order weight ring
   } else if (AMODE == kGatherK16 || AMODE == kGatherAny) {
     lds += sizeof(int) * T::BM * p.ga.F;
+    if (kWRing<T, AMODE, PREC> && EPI == kEpiRelu) lds += sizeof(float) * 4 * T::BM;  // first-order weight ring
   }
   if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
   if (EPI != kEpiOutput) lds = std::max(lds, sizeof(float) * EpiGeom<T, SG::FLOATS>::FLOATS);
@@ -967,6 +998,13 @@ int launch_epi(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 #undef RMX_EPI
 }
 
+// the tower_variant launch_tower_nt uses at M >= 65536 (knob, else the default below)
+inline int tower_variant_for(int NT, Epi epi, bool bf16, int K) {
+  const bool even = NT % 2 == 0 && NT >= 8;
+  const int def = NT == 26 ? ((epi == Epi::kOutput && !bf16) ? 5 : (bf16 && K >= 1024 ? 3 : 4)) : (even ? 3 : 0);
+  return tuning_get("tower_variant", def);
+}
+
 template <int NT, int PREC>
 int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // Large batches (M >= 65536, >= 2 blocks of 128 rows per CU).  Knob "tower_variant":
@@ -986,9 +1024,7 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // fp32 output layer prefers 32 rows per wave (variant 5: 0.171 vs 0.177 ms)
   // bf16 layers with a long K (PNN layer 1: K = 624 + 741) prefer the 16-wave 3-deep ring
   // (0.098 vs 0.119 ms at B = 65,536)
-  const int def = NT == 26 ? ((epi == Epi::kOutput && PREC == kPrecF32) ? 5 : (PREC == kPrecBF16 && p.K >= 1024 ? 3 : 4))
-                           : (kEven ? 3 : 0);
-  int var = tuning_get("tower_variant", def);
+  int var = tower_variant_for(NT, epi, PREC == kPrecBF16, p.K);
   if (p.M >= 65536) {
     if constexpr (kEven) {
       if (var == 2) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 1, 3>, PREC>(s, p, amode, epi);

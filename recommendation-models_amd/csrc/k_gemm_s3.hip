@@ -152,11 +152,6 @@ static bool s3_mt2(int M, int Npad, int amode, bool ids) {
   return tuning_get("s3_tower", 1) == 1 && (amode == kDenseA || (amode == kGatherK16 && ids)) && blocks2 >= 256;
 }
 
-bool tower_s3_idring(const DenseLayer& L, int M, const AGatherArgs* ga) {
-  return ga && ga->k == 16 && ga->ids && L.W3 && f32_split_enabled() && L.Npad % kS3BN == 0 &&
-         s3_mt2(M, L.Npad, kGatherK16, true);
-}
-
 int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   const int var = tuning_get("s3_tower", 1);
   p.prio = tuning_get("gemm_prio", 0);

@@ -663,15 +663,15 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   const bool deepfm = m.type == RMX_MODEL_DEEPFM;
   const bool fm_fused = (deepfm || m.type == RMX_MODEL_XDEEPFM || m.type == RMX_MODEL_DCN) && !in.y1 &&
                         (!deepfm || in.dtype == kF32) && gather_first && m.layers.size() > 1 &&
-                        tower_fm_fusable(m.layers[0], &ga, deepfm);
+                        tower_fm_fusable(m.layers[0], B, &ga, deepfm);
   // the first order by its own kernel (fm_y1 = 0, default) and the FM sums in layer 1: the sums are
   // free there, while summing the first-order weights in layer 1's epilogue exposes their gather
   // latency (bench: 0.213 ms layer 1 vs 0.022 + 0.172; DeepFM 154M -> 161M ex/s)
-  // fm_y1: 0 = first-order kernel, 1 = layer 1's epilogue gathers, 2 (default) = summed from the id
-  // ring's weight DMAs when layer 1 runs the id-ring tile (free), else the first-order kernel
+  // fm_y1: 0 = first-order kernel, 1 = layer 1's epilogue gathers, 2 (default) = summed from the
+  // ring's weight DMAs when layer 1 runs a w-ring tile (free), else the first-order kernel
   const int fm_y1 = tuning_get("fm_y1", 2);
   const bool fm_add = fm_fused && deepfm &&
-                      (fm_y1 == 0 || (fm_y1 == 2 && !tower_s3_idring(m.layers[0], B, &ga)));
+                      (fm_y1 == 0 || (fm_y1 == 2 && !tower_wring(m.layers[0], B, &ga)));
   if (fm_add) {
     StageTimer t(m, s, "first_order");
     if ((st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr))) return st;

@@ -116,8 +116,11 @@ struct FmArgs {
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa,
                        const XColArgs* xc = nullptr, const FmArgs* fm = nullptr);
-// true when launch_tower_layer(L, gather, kReluStore) can compute the FmArgs outputs (sums: + FM)
-bool tower_fm_fusable(const DenseLayer& L, const AGatherArgs* gather, bool sums);
+// true when launch_tower_layer(L, M, gather, kReluStore) computes the FmArgs outputs (sums: + FM)
+bool tower_fm_fusable(const DenseLayer& L, int M, const AGatherArgs* gather, bool sums);
+// true when gathered layer 1 runs a 2-deep ring tile whose DMAs also carry the first-order weights
+// (k_gemm.hpp kWRing): the first order is then summed from LDS at no cost
+bool tower_wring(const DenseLayer& L, int M, const AGatherArgs* ga);
 
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
@@ -141,8 +144,6 @@ int launch_pack_linear_t(hipStream_t s, const float* mats_dev, DenseLayer& L);
 int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, int lda, float* dx, int ldx,
                  const float* mask, int ldmask);
 bool dx_s3_usable(const DenseLayer& L, int ldx);
-// true when gathered layer 1 runs the split GEMM's id-ring tile (which can also sum the first order)
-bool tower_s3_idring(const DenseLayer& L, int M, const AGatherArgs* ga);
 // fp32 packed [n16][Npad][16] -> the three bf16 planes of the split GEMM (k_gemm_s3.hip)
 int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3);
 int64_t split3_elems(int n16, int Npad);  // bf16 elements of W3

@@ -58,8 +58,9 @@ class CooLongFloatMatrix:
 
 
 def set_tuning(key, value):
-    """Process-wide kernel variant knob (rmx_set_tuning), for A/B timing in one process."""
-    check(_lib.lib.rmx_set_tuning(key.encode(), int(value)))
+    """Process-wide kernel variant knob (rmx_set_tuning), for A/B timing in one process;
+    value None restores the built-in default."""
+    check(_lib.lib.rmx_set_tuning(key.encode(), -(2 ** 31) if value is None else int(value)))
 
 
 def get_tuning(key, default=0):

@@ -51,6 +51,17 @@ def test_abi_version():
     assert _lib.lib.rmx_abi_version() >= 1
 
 
+def test_tuning_knob_set_and_reset():
+    """rmx_set_tuning stores a knob; RMX_TUNING_DEFAULT (set_tuning(key, None)) removes it."""
+    assert rmx.get_tuning("abi_test_knob", 7) == 7
+    rmx.set_tuning("abi_test_knob", 3)
+    assert rmx.get_tuning("abi_test_knob", 7) == 3
+    rmx.set_tuning("abi_test_knob", None)
+    assert rmx.get_tuning("abi_test_knob", 7) == 7
+    rmx.set_tuning("abi_test_knob", None)  # removing an absent key is a no-op
+    assert rmx.get_tuning("abi_test_knob", 5) == 5
+
+
 KINDS = [
     (rmx.DeepFM, (1000, 39, 16, [400, 400, 400]), oc.DEEPFM, dict(fc=(400, 400, 400))),
     (rmx.DNN, (1000, 39, 16, [64, 32]), oc.DNN, dict(fc=(64, 32))),

@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 0, "fm_y1": 2}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
         rmx.set_tuning(k, v)
 
 
@@ -166,10 +166,12 @@ def test_fused_fm_bitwise_equals_encoder(ctx, B, y1_in_gemm):
 
 
 @pytest.mark.parametrize("kind,bf16", [("xdeepfm", False), ("dcn", False), ("dcn", True)])
-@pytest.mark.parametrize("B", [300, 65536])
-def test_fused_first_order_bitwise(ctx, kind, bf16, B):
-    """xDeepFM / DCN: the first order (Scatter) computed in tower layer 1's epilogue (fo_fuse) gives
-    the same bits as the standalone first-order kernel, fp32 and bf16 tables."""
+@pytest.mark.parametrize("B", [300, 16384, 65536, 65537])
+@pytest.mark.parametrize("ring", [True, False])
+def test_fused_first_order_bitwise(ctx, kind, bf16, B, ring):
+    """xDeepFM / DCN: the first order (Scatter) computed in tower layer 1 gives the same bits as the
+    standalone first-order kernel, fp32 and bf16 tables -- summed from the ring's weight DMAs
+    (ring=True: the default tiles) or gathered in the epilogue (ring=False: register-staged tiles)."""
     V = 50000
     m = _model(kind, V)
     if bf16:
@@ -181,6 +183,8 @@ def test_fused_first_order_bitwise(ctx, kind, bf16, B):
     ids_dev = rmx.DeviceArray(ctx, B * F, np.int32)
     rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_dev)
     out = rmx.DeviceArray(ctx, B, np.float32)
+    if not ring:
+        rmx.set_tuning("tower_variant" if bf16 else "s3_tower", 0 if bf16 else 2)
     res = []
     for fuse in (0, 1):
         rmx.set_tuning("fo_fuse", fuse)
