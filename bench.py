@@ -209,7 +209,15 @@ def main():
     B = args.batch or ({"xdeepfm": 16384, "xdeepfm_train": 4096}.get(args.workload, 65536))
     sharded = args.workload == "deepfm_sharded"
     Vw = args.vocab or (100_000_000 if sharded else V)
-    rmx.set_device(local)
+    # one rank per GPU; fewer GPUs than ranks (a rehearsal on a 1-GPU box) wraps ranks onto them
+    # (torch.cuda.device_count() does not initialise the GPU on this image)
+    ndev = 1
+    if world > 1:
+        import torch
+        ndev = max(1, torch.cuda.device_count())
+    if sharded and world > ndev:
+        raise SystemExit("deepfm_sharded needs one GPU per rank (RCCL rejects ranks sharing a GPU)")
+    rmx.set_device(local % ndev)
     ctx = rmx.default_context()
     stream = ctx.stream
     bf16 = args.workload.endswith("bf16")
