@@ -36,7 +36,9 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 # fp32 GEMMs on the exact 3-way bf16 split (csrc/k_gemm_s3.hip): 6 bf16 MFMAs per fp32 product,
 # so the ceiling of that arithmetic is the dense bf16 peak / 6 in fp32-equivalent FLOP/s
 PEAK_S3_TFLOPS = PEAK_BF16_TFLOPS / 6
-S3_STAGES = ("tower_layer", "cin_layer")
+# stages whose GEMMs run on the split (f32_split on): priced against its peak.  The backward stages
+# (dW and dX on the split; the CIN backward's rocBLAS part is fp32) take the higher peak too.
+S3_STAGES = ("tower_layer", "cin_layer", "tower_back", "cin_back")
 
 
 def parse():

@@ -437,6 +437,144 @@ __global__ __launch_bounds__(256) void wgrad_kernel(int rows, int N, int K, cons
     }
 }
 
+// The same "TN" GEMM on the bf16 matrix cores through the exact 3-way split (k_gemm.hpp kPrecS3,
+// DESIGN.md §4): both operands are fp32 activations / gradients, so they are split while staged --
+// each element once per block -- into three bf16 planes of LDS images [col][32 rows] (64-B rows,
+// 16-B slots of 8 rows XOR-swizzled by wg_slot); a wave's fragment of a 16-column tile is one
+// ds_read_b128 per plane, and a 32-row chunk costs 6 v_mfma_f32_16x16x32_bf16 per output tile
+// (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid, smallest first) against 8 f32 MFMAs per 16 rows.
+typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kWgR = 32;  // rows per chunk (the MFMA K)
+
+__device__ __forceinline__ void wg_split(const float* v, wg_bf16x8& hi, wg_bf16x8& mi, wg_bf16x8& lo) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const __bf16 h = (__bf16)v[q];
+    const float r = v[q] - (float)h;
+    const __bf16 m = (__bf16)r;
+    hi[q] = h;
+    mi[q] = m;
+    lo[q] = (__bf16)(r - (float)m);
+  }
+}
+
+// TT x TT output tile per block (TT = 64: 2 x 2 waves of 32 x 32; TT = 128: 2 x 4 waves of 64 x 32,
+// halving the L2 reads and LDS fragment reads per output), LDS [buf][A | X][plane][col][32 rows] bf16
+template <int TT>
+__global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows, int N, int K,
+                                                                        const float* __restrict__ A, int lda,
+                                                                        const float* __restrict__ X, int ldx,
+                                                                        int rows_per_slice, int tiles,
+                                                                        float* __restrict__ part) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int WJ = TT == 64 ? 2 : 4, TI = TT == 64 ? 2 : 4, TJ = 2;  // waves along k; tiles per wave
+  extern __shared__ __attribute__((aligned(16))) wg_bf16x8 wlds[];
+  auto L = [&](int buf, int op, int pl) { return wlds + ((buf * 2 + op) * 3 + pl) * TT * 4; };
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = blockIdx.x, xcd = bid & 7, idx = bid >> 3;
+  const int slice = (idx / tiles) * 8 + xcd, tile = idx % tiles;
+  const int ntn = (N + TT - 1) / TT;
+  const int n0 = (tile % ntn) * TT, k0 = (tile / ntn) * TT;
+  const int r_begin = slice * rows_per_slice;
+  const int r_end = min(rows, r_begin + rows_per_slice);
+  const int nch = r_end > r_begin ? (r_end - r_begin + kWgR - 1) / kWgR : 0;
+  // staging item: column tid % TT, row octet h = tid / TT (rows 8h..8h+7 of the chunk)
+  const int col = tid % TT, h = tid / TT;
+  const bool a_ok = n0 + col < N, x_ok = k0 + col < K;
+  // two register sets: the loads of chunk c + 2 are in flight while chunk c computes and chunk c + 1
+  // (loaded two steps earlier) is split into LDS
+  float a0[8], x0[8], a1[8], x1[8];
+  auto gload = [&](int c, float* va, float* vx) {
+    const int r0 = r_begin + c * kWgR + 8 * h;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = r0 + q;
+      const bool ok = r < r_end;
+      va[q] = (ok && a_ok) ? A[(int64_t)r * lda + n0 + col] : 0.f;
+      vx[q] = (ok && x_ok) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
+    }
+  };
+  auto sstore = [&](int buf, const float* va, const float* vx) {
+    const int o = col * 4 + wg_slot(col, h);
+    wg_bf16x8 p0, p1, p2;
+    wg_split(va, p0, p1, p2);
+    L(buf, 0, 0)[o] = p0;
+    L(buf, 0, 1)[o] = p1;
+    L(buf, 0, 2)[o] = p2;
+    wg_split(vx, p0, p1, p2);
+    L(buf, 1, 0)[o] = p0;
+    L(buf, 1, 1)[o] = p1;
+    L(buf, 1, 2)[o] = p2;
+  };
+  const int wi = wid / WJ, wj = wid - (wid / WJ) * WJ, g = lane >> 4, r16 = lane & 15;
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int cur) {
+    wg_bf16x8 fa[TI][3], fx[TJ][3];
+#pragma unroll
+    for (int t = 0; t < TI; ++t) {
+      const int ca = wi * TI * 16 + t * 16 + r16;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fa[t][pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+    }
+#pragma unroll
+    for (int t = 0; t < TJ; ++t) {
+      const int cx = wj * TJ * 16 + t * 16 + r16;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fx[t][pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
+    }
+#pragma unroll
+    for (int a = 0; a < TI; ++a)
+#pragma unroll
+      for (int b = 0; b < TJ; ++b) {
+        f32x4 d = acc[a][b];
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fx[b][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][2], fx[b][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][2], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fx[b][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][1], d, 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][0], d, 0, 0, 0);
+      }
+  };
+  if (nch > 0) {
+    gload(0, a0, x0);
+    sstore(0, a0, x0);
+  }
+  if (nch > 1) gload(1, a0, x0);
+  if (nch > 2) gload(2, a1, x1);
+  __syncthreads();
+  for (int c = 0; c < nch; c += 2) {
+    compute(0);  // chunk c (even) in buffer 0
+    if (c + 1 < nch) {
+      sstore(1, a0, x0);
+      if (c + 3 < nch) gload(c + 3, a0, x0);
+    }
+    __syncthreads();
+    if (c + 1 >= nch) break;
+    compute(1);  // chunk c + 1 in buffer 1
+    if (c + 2 < nch) {
+      sstore(0, a1, x1);
+      if (c + 4 < nch) gload(c + 4, a1, x1);
+    }
+    __syncthreads();
+  }
+  float* out = part + (int64_t)slice * N * K;
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int b = 0; b < TJ; ++b) {
+      const int k = k0 + wj * TJ * 16 + b * 16 + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wi * TI * 16 + a * 16 + 4 * g + r;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][b][r];
+      }
+    }
+}
+
 // out[i] (=, or += when accum) sum_s part[s][i]: a block covers 64 outputs with 4 wave-groups, group
 // q summing slices q, q + 4, ...; the 4 group sums are added in fixed order (deterministic).
 __global__ __launch_bounds__(256) void slice_reduce_kernel(int S, int64_t n, const float* __restrict__ part,
@@ -491,16 +629,34 @@ int ensure_part(TrainState& T, int64_t n) {
 int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, int lda, const float* X, int ldx,
           float* out, bool accum) {
   if (rows <= 0 || N <= 0 || K <= 0) return RMX_OK;
-  const int tiles = ((N + kWgT - 1) / kWgT) * ((K + kWgT - 1) / kWgT);
+  // knob "wgrad_s3": 0 = the f32 MFMA kernel, 1 = split GEMM with 64 x 64 tiles, 2 = 128 x 128 tiles
+  const int var = f32_split_enabled() ? tuning_get("wgrad_s3", 1) : 0;
+  const int TT = var == 2 ? 128 : kWgT;
+  const int tiles = ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
   // slices of ~1024 rows (one slice of both operands, (N + K) * 4 KiB, stays in an XCD's 4 MiB L2),
   // at least ~1024 blocks in flight, S a multiple of the 8 XCDs
   int S = std::max((rows + 1023) / 1024, std::min((1024 + tiles - 1) / tiles, std::max(1, rows / 64)));
   S = round_up(std::min(S, 512), 8);
-  const int rps = round_up((rows + S - 1) / S, 16);
+  const int rps = round_up((rows + S - 1) / S, var ? kWgR : 16);
   int st = ensure_part(T, (int64_t)S * N * K);
   if (st) return st;
-  hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, rows, N, K, A, lda, X, ldx, rps, tiles,
-                     T.part2);
+  if (var == 2) {
+    const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * 128 * 4;
+    static bool attr = false;
+    if (!attr) {
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_s3_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      attr = true;
+    }
+    hipLaunchKernelGGL(wgrad_s3_kernel<128>, dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx, rps,
+                       tiles, T.part2);
+  } else if (var) {
+    hipLaunchKernelGGL(wgrad_s3_kernel<64>, dim3(tiles * S), dim3(256), sizeof(wg_bf16x8) * 2 * 2 * 3 * 64 * 4, s,
+                       rows, N, K, A, lda, X, ldx, rps, tiles, T.part2);
+  } else {
+    hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, rows, N, K, A, lda, X, ldx, rps, tiles,
+                       T.part2);
+  }
   RMX_HIP(hipGetLastError());
   hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)N * K + 63) / 64)), dim3(256), 0, s, S,
                      (int64_t)N * K, T.part2, out, accum ? 1 : 0);

@@ -214,6 +214,20 @@ def test_backward_ids_matches_oracle(kind, B, fc):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn"])
+def test_backward_weight_grad_variants(kind, variant):
+    """dW on the f32 MFMA kernel (0) and the split GEMM with 64 x 64 (1) / 128 x 128 (2) tiles: all
+    within the same oracle bar (tower, CIN and cross weight gradients)."""
+    import rmx
+    rmx.set_tuning("wgrad_s3", variant)
+    try:
+        test_backward_ids_matches_oracle(kind, 512, (400, 400, 400))
+    finally:
+        rmx.set_tuning("wgrad_s3", None)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", GPU_KINDS)
 def test_backward_host_arrays_in_place(kind):
     """L-A RecModel.backward: the caller's arrays come back holding the gradients."""
