@@ -445,6 +445,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(int rows, int N, int K, cons
 // (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid, smallest first) against 8 f32 MFMAs per 16 rows.
 typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kWgR = 32;  // rows per chunk (the MFMA K)
+// timing-only diagnostic builds (tools/diag_build.sh-style, results wrong): 1 = no LDS stores in the
+// loop, 2 = no MFMAs, 4 = no global loads in the loop
+#ifndef RMX_WGRAD_DIAG
+#define RMX_WGRAD_DIAG 0
+#endif
 
 __device__ __forceinline__ void wg_split(const float* v, wg_bf16x8& hi, wg_bf16x8& mi, wg_bf16x8& lo) {
 #pragma unroll
@@ -513,6 +518,7 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows
 #pragma unroll
     for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int cur) {
+    if constexpr (RMX_WGRAD_DIAG & 2) return;
     wg_bf16x8 fa[TI][3], fx[TJ][3];
 #pragma unroll
     for (int t = 0; t < TI; ++t) {
@@ -549,15 +555,15 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows
   for (int c = 0; c < nch; c += 2) {
     compute(0);  // chunk c (even) in buffer 0
     if (c + 1 < nch) {
-      sstore(1, a0, x0);
-      if (c + 3 < nch) gload(c + 3, a0, x0);
+      if (!(RMX_WGRAD_DIAG & 1)) sstore(1, a0, x0);
+      if (!(RMX_WGRAD_DIAG & 4) && c + 3 < nch) gload(c + 3, a0, x0);
     }
     __syncthreads();
     if (c + 1 >= nch) break;
     compute(1);  // chunk c + 1 in buffer 1
     if (c + 2 < nch) {
-      sstore(0, a1, x1);
-      if (c + 4 < nch) gload(c + 4, a1, x1);
+      if (!(RMX_WGRAD_DIAG & 1)) sstore(0, a1, x1);
+      if (!(RMX_WGRAD_DIAG & 4) && c + 4 < nch) gload(c + 4, a1, x1);
     }
     __syncthreads();
   }
