@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="Zipf exponent of the ids within a field (SURVEY.md §8d secondary; 0 = uniform)")
-    ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step")
+    ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step (default: auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--set", default="", help="kernel knobs before building the model, k=v,k=v (rmx_set_tuning)")
@@ -241,7 +241,7 @@ def main():
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
         table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
-        table.set_dedupe(not args.no_dedupe)
+        table.set_dedupe(False if args.no_dedupe else "auto")
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
     table.fill_synthetic(SEED_TAB)
@@ -407,7 +407,7 @@ def main():
                 "global_batch": world * B, "rows_per_gpu_set": nrows,
                 "ids": ("zipf%g" % args.zipf) if args.zipf else "uniform",
                 "parallelism": ("hashshard%d_rccl" % world) if sharded else "replicas%d" % world},
-            **({"exchange": {"dedupe": not args.no_dedupe, "ids_sent_last_step": table.last_sent(),
+            **({"exchange": {"dedupe": "off" if args.no_dedupe else "auto", "ids_sent_last_step": table.last_sent(),
                              "nnz_per_step": B * F}} if sharded else {}),
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -7,7 +7,7 @@
 // Partitioning: owner(id) = id mod N, local row = id div N (Criteo ids are feature hashes, so
 // modulo partitioning balances; it is a bijection [0, V) -> [N] x [ceil(V/N)]).
 // One exchange step per batch on the caller's stream:
-//   0. dedupe  : (default on; rmx_shard_set_dedupe) the batch's distinct ids, as
+//   0. dedupe  : (rmx_shard_set_dedupe: off / on / auto, default auto) the batch's distinct ids, as
 //                ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull: an
 //                open-addressing hash set in HBM (atomicCAS insert, linear probing) gives every
 //                nnz its set slot; steps 1-5 then move one row per DISTINCT id and the final
@@ -64,8 +64,11 @@ struct rmx_shard {
   float* send_w = nullptr;              // [recv]
   float* recv_emb = nullptr;            // [nnz][k] rows for this rank's batch (bucket order)
   float* recv_w = nullptr;              // [nnz]
-  // dedupe (step 0)
-  bool dedupe = true;
+  // dedupe (step 0): 0 off, 1 on, 2 auto -- on for one batch, then off for the next kAutoSkip
+  // batches when it removed under 10 % of the ids (uniform ids over a large V: the hash pass costs
+  // more than the rows it saves), re-probed after them
+  int dedupe = 2;
+  int dedupe_skip = 0;
   int64_t cap_hash = 0;                 // hash-set slots (power of two >= 2 nnz)
   int32_t* hkeys = nullptr;             // [cap_hash] distinct ids (-1 = empty)
   int32_t* hvals = nullptr;             // [cap_hash] bucket slot of the distinct id
@@ -405,6 +408,17 @@ int shard_fill_synthetic(rmx_shard& sh, uint64_t seed) {
   return RMX_OK;
 }
 
+constexpr int kAutoSkip = 63;
+
+// dedupe = auto: after a deduped batch, skip the step for kAutoSkip batches when it removed < 10 %
+void dedupe_auto(rmx_shard& sh, bool dd, int64_t nnz) {
+  if (sh.dedupe != 2 || nnz <= 0) return;
+  if (dd)
+    sh.dedupe_skip = sh.last_sent * 10 > nnz * 9 ? kAutoSkip : 0;
+  else if (sh.dedupe_skip > 0)
+    --sh.dedupe_skip;
+}
+
 // Steps 1-5 of the exchange: fills sh.perm / sh.recv_emb / sh.recv_w for this rank's batch.
 int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids) {
   const int N = sh.N, k = sh.k;
@@ -413,12 +427,13 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   int32_t* cnt = sh.counts;           // [N] send counts
   int32_t* rcnt = sh.counts + N;      // [N] recv counts
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
+  const bool dd = nnz > 0 && (sh.dedupe == 1 || (sh.dedupe == 2 && sh.dedupe_skip == 0));
   if (nnz > 0) {
     // route the batch's ids, or (dedupe) the distinct ids held by the hash set's slots
     const int32_t* rids = d_ids;
     int64_t rn = nnz;
     int32_t* rslot = sh.perm;
-    if (sh.dedupe) {
+    if (dd) {
       RMX_HIP(hipMemsetAsync(sh.hkeys, 0xFF, sizeof(int32_t) * sh.cap_hash, s));
       hipLaunchKernelGGL(dedupe_insert_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, d_ids,
                          (uint32_t)(sh.cap_hash - 1), 64 - __builtin_ctzll((unsigned long long)sh.cap_hash),
@@ -437,7 +452,7 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, cnt, sh.bcnt,
                        sh.send_ids, rslot);
     RMX_HIP(hipGetLastError());
-    if (sh.dedupe) {
+    if (dd) {
       hipLaunchKernelGGL(dedupe_perm_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, sh.hslot,
                          sh.hvals, sh.perm);
       RMX_HIP(hipGetLastError());
@@ -450,6 +465,7 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     int64_t off = 0;
     sh.last_sent = 0;
     for (int o = 0; o < N; ++o) sh.last_sent += sh.h_counts[o];
+    dedupe_auto(sh, dd, nnz);
     for (int o = 0; o < N; ++o) {
       const int64_t c = sh.h_counts[o];
       if ((st = launch_owner_gather(s, c, k, sh.send_ids + off, sh.emb[o], sh.w[o], sh.recv_emb + off * k,
@@ -476,6 +492,7 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     nrecv += hr[o];
     sh.last_sent += hc[o];
   }
+  dedupe_auto(sh, dd, nnz);
   if ((st = ensure_recv(sh, nrecv))) return st;
   // 3. ids to owners
   RMX_NCCL(ncclGroupStart());
@@ -544,7 +561,8 @@ extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
     set_error("rmx_shard_set_dedupe: NULL shard");
     return RMX_E_INVALID;
   }
-  sh->dedupe = on != 0;
+  sh->dedupe = on == 2 ? 2 : (on != 0 ? 1 : 0);
+  sh->dedupe_skip = 0;
   return RMX_OK;
 }
 

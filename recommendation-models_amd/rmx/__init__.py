@@ -252,8 +252,9 @@ class ShardedTable:
         return int(_lib.lib.rmx_shard_local_rows(self.handle))
 
     def set_dedupe(self, on):
-        """Send each distinct id of a batch once (default on; ParRecModel.distinctIntIndices)."""
-        check(_lib.lib.rmx_shard_set_dedupe(self.handle, 1 if on else 0))
+        """Send each distinct id of a batch once (ParRecModel.distinctIntIndices): True, False or
+        "auto" (the default: on, then off for 63 batches when it removed < 10 % of the ids)."""
+        check(_lib.lib.rmx_shard_set_dedupe(self.handle, 2 if on == "auto" else (1 if on else 0)))
 
     def last_sent(self):
         """Ids this rank sent to owners in its last exchange."""

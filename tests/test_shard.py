@@ -83,6 +83,39 @@ def test_loopback_shard_gather_bit_exact(N, zipf, dedupe):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("zipf", [0.0, 1.1])
+def test_loopback_shard_dedupe_auto(zipf):
+    """dedupe "auto" (the default): the first batch is deduplicated; when that removed < 10 % of the
+    ids (uniform ids over a large V) the next batches skip the step, with heavy reuse (Zipf) they keep
+    it -- the gathered rows are bit-exact either way."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B, N = 5_000_011, 300, 4
+    _, ids = _setup(ctx, V, B, zipf=zipf)
+    sh = rmx.ShardedTable(ctx, V, K, N)
+    sh.set_dedupe("auto")
+    sh.fill_synthetic(SEED_TAB)
+    n = B * F
+    h_ids = ids.numpy().astype(np.int64)
+    distinct = len(np.unique(h_ids))
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    w_ref, e_ref = oc.gather(wt, et, 1, h_ids)
+    w = rmx.DeviceArray(ctx, n, np.float32)
+    e = rmx.DeviceArray(ctx, n * K, np.float32)
+    sent = []
+    for _ in range(3):
+        sh.gather(ids, n, w, e)
+        ctx.sync()
+        assert np.array_equal(w.numpy(), w_ref) and np.array_equal(e.numpy(), e_ref)
+        sent.append(sh.last_sent())
+    assert sent[0] == distinct
+    if distinct * 10 > n * 9:
+        assert sent[1:] == [n, n]
+    else:
+        assert sent[1:] == [distinct, distinct]
+
+
+@pytest.mark.gpu
 def test_gen_ids_zipf_shape():
     """Zipf-like ids: inside each field's range, deterministic, rank 0 the most frequent."""
     import rmx
