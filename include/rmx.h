@@ -244,8 +244,8 @@ int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);
 int64_t rmx_shard_local_rows(const rmx_shard* sh);
 /* Step 0 of the exchange: send each DISTINCT id of the batch once, as
  * ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull; results are identical.
- * on: 0 off, 1 on, 2 auto (default: on for a batch, then off for the next 63 batches when it removed
- * fewer than 10 % of the ids, re-probed after them). */
+ * on: 0 off, 1 on, 2 auto (default: off at one rank; else on for a batch, then off for the next 63
+ * batches when it removed fewer than 10 % of the ids, re-probed after them). */
 int rmx_shard_set_dedupe(rmx_shard* sh, int on);
 /* Ids this rank sent to owners in its last exchange (the distinct ids when deduplicating). */
 int64_t rmx_shard_last_sent(const rmx_shard* sh);

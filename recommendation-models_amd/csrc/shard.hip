@@ -20,6 +20,7 @@
 //   3. ids     : grouped send/recv of each bucket to its owner.
 //   4. gather  : the owner copies emb[local][0..k) and w[local] for every received id.
 //   5. rows    : grouped send/recv of the rows back, into the requester's bucket order.
+//   (steps 3-5 skip this rank's own bucket: its rows are gathered straight into their slots)
 //   6. forward : the model runs on (ids = perm, table = received rows): every kernel already
 //                gathers through an id list, so nothing else changes and the outputs are bitwise
 //                those of the replicated table (tests/test_shard.py).
@@ -427,7 +428,8 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   int32_t* cnt = sh.counts;           // [N] send counts
   int32_t* rcnt = sh.counts + N;      // [N] recv counts
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
-  const bool dd = nnz > 0 && (sh.dedupe == 1 || (sh.dedupe == 2 && sh.dedupe_skip == 0));
+  // (auto at one rank: off -- no link traffic to save, the duplicates' rows are local reads)
+  const bool dd = nnz > 0 && (sh.dedupe == 1 || (sh.dedupe == 2 && sh.N > 1 && sh.dedupe_skip == 0));
   if (nnz > 0) {
     // route the batch's ids, or (dedupe) the distinct ids held by the hash set's slots
     const int32_t* rids = d_ids;
@@ -494,18 +496,37 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   }
   dedupe_auto(sh, dd, nnz);
   if ((st = ensure_recv(sh, nrecv))) return st;
+  // this rank's own bucket never goes through RCCL: its rows are gathered straight into the
+  // requester-order slots (hr[me] == hc[me]); at one rank the exchange is that gather alone
+  const int me = sh.rank;
+  int64_t so_me = 0, ro_me = 0;
+  for (int o = 0; o < me; ++o) {
+    so_me += hc[o];
+    ro_me += hr[o];
+  }
   // 3. ids to owners
   RMX_NCCL(ncclGroupStart());
   for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += hr[o], ++o) {
+    if (o == me) continue;
     if (hc[o]) RMX_NCCL(ncclSend(sh.send_ids + so, hc[o], ncclInt32, (int)o, sh.comm, s));
     if (hr[o]) RMX_NCCL(ncclRecv(sh.recv_ids + ro, hr[o], ncclInt32, (int)o, sh.comm, s));
   }
   RMX_NCCL(ncclGroupEnd());
-  // 4. owner gather
-  if ((st = launch_owner_gather(s, nrecv, k, sh.recv_ids, sh.emb[0], sh.w[0], sh.send_emb, sh.send_w))) return st;
+  // 4. owner gather: the peers' requests (the ranges before and after this rank's own), then the own bucket
+  if (ro_me > 0 &&
+      (st = launch_owner_gather(s, ro_me, k, sh.recv_ids, sh.emb[0], sh.w[0], sh.send_emb, sh.send_w)))
+    return st;
+  const int64_t r1 = ro_me + hr[me];
+  if (nrecv > r1 && (st = launch_owner_gather(s, nrecv - r1, k, sh.recv_ids + r1, sh.emb[0], sh.w[0],
+                                              sh.send_emb + r1 * k, sh.send_w + r1)))
+    return st;
+  if ((st = launch_owner_gather(s, hc[me], k, sh.send_ids + so_me, sh.emb[0], sh.w[0], sh.recv_emb + so_me * k,
+                                sh.recv_w + so_me)))
+    return st;
   // 5. rows back, into the requester's bucket order
   RMX_NCCL(ncclGroupStart());
   for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += hr[o], ++o) {
+    if (o == me) continue;
     if (hr[o]) {
       RMX_NCCL(ncclSend(sh.send_emb + ro * k, (size_t)hr[o] * k, ncclFloat32, (int)o, sh.comm, s));
       RMX_NCCL(ncclSend(sh.send_w + ro, hr[o], ncclFloat32, (int)o, sh.comm, s));

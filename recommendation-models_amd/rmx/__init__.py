@@ -253,7 +253,8 @@ class ShardedTable:
 
     def set_dedupe(self, on):
         """Send each distinct id of a batch once (ParRecModel.distinctIntIndices): True, False or
-        "auto" (the default: on, then off for 63 batches when it removed < 10 % of the ids)."""
+        "auto" (the default: off at one rank, else on, then off for 63 batches when it removed < 10 %
+        of the ids)."""
         check(_lib.lib.rmx_shard_set_dedupe(self.handle, 2 if on == "auto" else (1 if on else 0)))
 
     def last_sent(self):
