@@ -235,12 +235,21 @@ def main():
         model.setPrecision(rmx.DTYPE_BF16)
     if sharded:
         # configs[3]: table hash-sharded over the ranks, RCCL exchange per batch
-        uid = rmx.comm_unique_id() if rank == 0 else None
-        if dist:
-            box = [uid]
-            dist.broadcast_object_list(box, src=0)
-            uid = box[0]
-        table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
+        # RCCL prints its version banner on fd 1 at init; keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved_fd1 = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            uid = rmx.comm_unique_id() if rank == 0 else None
+            if dist:
+                box = [uid]
+                dist.broadcast_object_list(box, src=0)
+                uid = box[0]
+            table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved_fd1, 1)
+            os.close(saved_fd1)
         table.set_dedupe(False if args.no_dedupe else "auto")
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
