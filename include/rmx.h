@@ -71,6 +71,7 @@ typedef struct rmx_ctx rmx_ctx;
 typedef struct rmx_model rmx_model;
 typedef struct rmx_table rmx_table;
 typedef struct rmx_shard rmx_shard;
+typedef struct rmx_group rmx_group;
 typedef struct rmx_samples rmx_samples;
 
 /* ------------------------------------------------------------------ misc -- */
@@ -78,8 +79,10 @@ const char* rmx_last_error(void);
 int rmx_abi_version(void);
 
 /* Process-wide tuning knobs (kernel variant selection for A/B timing in one process).
- * Known keys: "tower_variant" (see k_tower.hip), "cin_variant" (k_cin.hip).  Unknown keys are
- * stored and ignored.  rmx_get_tuning returns def when the key was never set; setting
+ * Known keys (README.md lists them): "f32_split", "s3_tower", "s3_cin", "tower_variant" (GEMM
+ * engine and tile variants, csrc/k_gemm.hpp, k_gemm_s3.hip), "fm_fuse", "fm_y1", "fo_fuse" (first
+ * order / FM inside tower layer 1), "wgrad_s3" (training dW kernel, csrc/train.hip).  Unknown keys
+ * are stored and ignored.  rmx_get_tuning returns def when the key was never set; setting
  * RMX_TUNING_DEFAULT removes the key (back to the built-in default). */
 #define RMX_TUNING_DEFAULT (-2147483647 - 1)
 int rmx_set_tuning(const char* key, int value);
@@ -141,7 +144,8 @@ int rmx_forward(rmx_model* m, int32_t batch_size, int64_t nnz, const int64_t* in
  * Same arrays and checks as rmx_forward plus targets[batch_size] (label > 0 -> 1).  On return the
  * caller's bias / weights / embedding / mats arrays hold the GRADIENTS, as the reference writes
  * them back in place (yr/util/GradUtil.scala:7-42, BackwardUtil.scala:6-30), and *loss the mean
- * BCE loss (BigDL BCECriterion, sizeAverage).  fp32 models; LR, DeepFM and DNN so far. */
+ * BCE loss (BigDL BCECriterion, sizeAverage).  fp32 models; every model kind (LR, DeepFM, xDeepFM,
+ * DCN, PNN, DNN). */
 int rmx_backward(rmx_model* m, int32_t batch_size, int64_t nnz, const int64_t* index,
                  const int64_t* feats, float* bias, float* weights, float* embedding,
                  int32_t embedding_dim, float* mats, const int32_t* mat_sizes, int32_t n_sizes,
@@ -253,6 +257,17 @@ int64_t rmx_shard_last_sent(const rmx_shard* sh);
  * from the owners (makeWeights / makeEmbeddings through the exchange).  Bit-exact copies. */
 int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
                      void* stream);
+/* In-process exchange group: nranks VIRTUAL ranks in one process (one host thread, context and
+ * stream each, all on one GPU or several).  A shard created on a group runs the same exchange
+ * schedule as the RCCL one (counts, ids to owners, owner gather, rows back, own bucket local), with
+ * every grouped send/recv replaced by a device copy from the peer's posted buffer; the ranks
+ * rendezvous inside each grouped step, so every rank must make the same collective calls, each from
+ * its own thread (a rank missing for 120 s fails the step with RMX_E_COMM).  Used to run the
+ * N > 1 exchange on a single GPU.  The group lives until it and all its shards are destroyed. */
+int rmx_group_create(int nranks, rmx_group** out);
+int rmx_group_destroy(rmx_group* g);
+int rmx_shard_create_group(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, rmx_group* group, int rank,
+                           rmx_shard** out);
 /* Collective: L-B forward of this rank's batch (d_ids [batch * nFields]) over the sharded table. */
 int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t batch, const int32_t* d_ids,
                             float* d_out, void* stream);

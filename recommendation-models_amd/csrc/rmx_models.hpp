@@ -169,7 +169,8 @@ struct StageTimer {
   StageTimer(rmx_model& mm, hipStream_t ss, const char* name);
   ~StageTimer();
 };
-int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* unique_id, rmx_shard** out);
+int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* unique_id, rmx_group* group,
+                 rmx_shard** out);
 int shard_destroy(rmx_shard* sh);
 
 // kernels specific to the interaction encoders

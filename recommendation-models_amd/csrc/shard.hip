@@ -24,14 +24,22 @@
 //   6. forward : the model runs on (ids = perm, table = received rows): every kernel already
 //                gathers through an id list, so nothing else changes and the outputs are bitwise
 //                those of the replicated table (tests/test_shard.py).
-// A "loopback" shard (unique_id == NULL) keeps all N partitions in this process on one GPU and
-// replaces steps 2-5's transport by in-place reads: it exercises the routing and owner-gather
-// kernels at N > 1 on a single device.
+// Steps 2, 3 and 5 go through a Transport: RCCL between processes (one rank per GPU, the product
+// path), or an in-process exchange group (rmx_group: N virtual ranks, one host thread and one stream
+// each, every grouped send/recv a device copy from the peer's posted buffer) that runs the SAME
+// schedule -- offsets, own-bucket skip, buffer sizing -- at N > 1 on a single GPU.
+// At one rank there is no exchange at all: route + the own-bucket gather, sized on the device (no
+// host sync).
+// A "loopback" shard (unique_id == NULL, no group) keeps all N partitions in this process on one
+// GPU and serves every bucket in place: a single-thread check of the routing at N > 1.
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "rmx_models.hpp"
@@ -46,12 +54,41 @@
     }                                                                                           \
   } while (0)
 
+namespace rmx {
+// The exchange's grouped point-to-point ops (NCCL group semantics: every op between start() and
+// end() is posted together; the k-th send from p to q pairs with the k-th recv of q from p).
+struct Transport {
+  virtual ~Transport() {}
+  virtual int start() = 0;
+  virtual int send(const void* p, size_t bytes, int peer, hipStream_t s) = 0;
+  virtual int recv(void* p, size_t bytes, int peer, hipStream_t s) = 0;
+  virtual int end(hipStream_t s) = 0;
+};
+}  // namespace rmx
+
+// In-process exchange group: N virtual ranks (one host thread each) rendezvous in end().
+struct rmx_group {
+  int N = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool broken = false;                      // a rank timed out: every later rendezvous fails
+  struct Msg { const void* src; size_t bytes; };
+  std::vector<std::vector<Msg>> posted;     // [from * N + to] sends of the current group
+  std::vector<hipEvent_t> ev_send, ev_done; // per rank: its posted data ready / its copies done
+  std::vector<int> attached;                // ranks with a shard
+  int refs = 1;                             // the creator + one per attached shard
+};
+
 struct rmx_shard {
   rmx_ctx* ctx = nullptr;
   int64_t V = 0;
   int k = 0, N = 1, rank = 0;
   bool loopback = false;
   ncclComm_t comm = nullptr;
+  rmx_group* group = nullptr;           // in-process exchange group (or null)
+  std::unique_ptr<rmx::Transport> tr;   // RCCL or group transport (null: loopback)
   int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
   std::vector<float*> emb, w;           // partitions held here: [rows_per][k], [rows_per] (loopback: N)
   // per-batch buffers (grow only)
@@ -60,8 +97,8 @@ struct rmx_shard {
   int32_t* h_counts = nullptr;          // pinned host [2N]
   int32_t* send_ids = nullptr;          // [nnz] local rows, bucketed by owner
   int32_t* perm = nullptr;              // [nnz] slot of id n
-  int32_t* recv_ids = nullptr;          // [recv] local rows requested from this rank
-  float* send_emb = nullptr;            // [recv][k] rows gathered for requesters
+  int32_t* recv_ids = nullptr;          // [recv] local rows requested by the PEERS (own bucket excluded)
+  float* send_emb = nullptr;            // [recv][k] rows gathered for them
   float* send_w = nullptr;              // [recv]
   float* recv_emb = nullptr;            // [nnz][k] rows for this rank's batch (bucket order)
   float* recv_w = nullptr;              // [nnz]
@@ -74,7 +111,8 @@ struct rmx_shard {
   int32_t* hkeys = nullptr;             // [cap_hash] distinct ids (-1 = empty)
   int32_t* hvals = nullptr;             // [cap_hash] bucket slot of the distinct id
   int32_t* hslot = nullptr;             // [nnz] set slot of id n
-  int64_t last_sent = 0;                // ids sent by the last exchange (distinct ids when deduped)
+  mutable int64_t last_sent = 0;        // ids sent by the last exchange (distinct ids when deduped)
+  mutable bool last_sent_dev = false;   // one rank: last_sent is still on the device (counts[0])
   int32_t* bcnt = nullptr;              // [N][tiles] per-tile owner counts -> tile start offsets
   int64_t cap_tiles = 0;
 };
@@ -190,10 +228,14 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nn
   }
 }
 
-// rows for requested local ids: 4 lanes per row at k = 16 (one float4 each), generic otherwise
-__global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, int k, const int32_t* __restrict__ rows,
+// rows for requested local ids: 4 lanes per row at k = 16 (one float4 each), generic otherwise.
+// dcount (nullable): the row count lives on the device (the one-rank exchange, no host sync); n is
+// then the grid's upper bound.
+__global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, const int32_t* __restrict__ dcount, int k,
+                                                          const int32_t* __restrict__ rows,
                                                           const float* __restrict__ emb, const float* __restrict__ w,
                                                           float* __restrict__ out_emb, float* __restrict__ out_w) {
+  if (dcount) n = min(n, (int64_t)*dcount);
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k == 16) {
     const int64_t i = t >> 2;
@@ -320,18 +362,155 @@ int ensure_recv(rmx_shard& sh, int64_t n) {
 }
 
 int launch_owner_gather(hipStream_t s, int64_t n, int k, const int32_t* rows, const float* emb, const float* w,
-                        float* out_emb, float* out_w) {
+                        float* out_emb, float* out_w, const int32_t* dcount = nullptr) {
   if (n <= 0) return RMX_OK;
   const int64_t threads = k == 16 ? n * 4 : n;
-  hipLaunchKernelGGL(owner_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, k, rows, emb,
-                     w, out_emb, out_w);
+  hipLaunchKernelGGL(owner_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, dcount, k,
+                     rows, emb, w, out_emb, out_w);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
 
 }  // namespace
 
-int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* unique_id, rmx_shard** out) {
+// ---------------------------------------------------------------- transports --
+namespace {
+
+struct RcclTransport : Transport {
+  ncclComm_t comm;
+  explicit RcclTransport(ncclComm_t c) : comm(c) {}
+  int start() override {
+    RMX_NCCL(ncclGroupStart());
+    return RMX_OK;
+  }
+  int send(const void* p, size_t bytes, int peer, hipStream_t s) override {
+    RMX_NCCL(ncclSend(p, bytes, ncclInt8, peer, comm, s));
+    return RMX_OK;
+  }
+  int recv(void* p, size_t bytes, int peer, hipStream_t s) override {
+    RMX_NCCL(ncclRecv(p, bytes, ncclInt8, peer, comm, s));
+    return RMX_OK;
+  }
+  int end(hipStream_t) override {
+    RMX_NCCL(ncclGroupEnd());
+    return RMX_OK;
+  }
+};
+
+// Host rendezvous of the group's N threads; fails (and breaks the group) after kGroupTimeout.
+constexpr auto kGroupTimeout = std::chrono::seconds(120);
+
+int group_barrier(rmx_group& g) {
+  std::unique_lock<std::mutex> lk(g.mu);
+  if (g.broken) {
+    set_error("exchange group: a rank failed to arrive earlier; the group is unusable");
+    return RMX_E_COMM;
+  }
+  const uint64_t my = g.gen;
+  if (++g.arrived == g.N) {
+    g.arrived = 0;
+    ++g.gen;
+    g.cv.notify_all();
+    return RMX_OK;
+  }
+  if (!g.cv.wait_for(lk, kGroupTimeout, [&] { return g.gen != my || g.broken; }) || g.broken) {
+    g.broken = true;
+    g.cv.notify_all();
+    set_error("exchange group: peers did not reach the exchange (every rank must call it)");
+    return RMX_E_COMM;
+  }
+  return RMX_OK;
+}
+
+// Every recv is a device copy from the matching send's buffer on the receiver's stream:
+//   1. record ev_send[me] (this rank's posted data is ready), post the sends, rendezvous;
+//   2. per recv: wait for ev_send[peer], copy; record ev_done[me] (my reads are done), rendezvous;
+//   3. wait for ev_done[peer] of every peer I sent to, so later writes to my send buffers are safe.
+// ev_send[p] / ev_done[p] are re-recorded only after a rendezvous that every reader has passed.
+struct LocalTransport : Transport {
+  rmx_group* g;
+  int me;
+  struct Op { void* p; size_t bytes; int peer; };
+  std::vector<Op> sends, recvs;
+  LocalTransport(rmx_group* gg, int r) : g(gg), me(r) {}
+  int start() override {
+    sends.clear();
+    recvs.clear();
+    return RMX_OK;
+  }
+  int send(const void* p, size_t bytes, int peer, hipStream_t) override {
+    sends.push_back({const_cast<void*>(p), bytes, peer});
+    return RMX_OK;
+  }
+  int recv(void* p, size_t bytes, int peer, hipStream_t) override {
+    recvs.push_back({p, bytes, peer});
+    return RMX_OK;
+  }
+  int end(hipStream_t s) override {
+    const int N = g->N;
+    // a failing HIP call must not skip the rendezvous (the peers would wait for this rank)
+    int err = RMX_OK;
+    auto hip = [&](hipError_t e, const char* what) {
+      if (e != hipSuccess && err == RMX_OK) {
+        set_error(std::string("exchange group: ") + what + ": " + hipGetErrorString(e));
+        err = RMX_E_HIP;
+      }
+    };
+    hip(hipEventRecord(g->ev_send[me], s), "hipEventRecord");
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      for (int to = 0; to < N; ++to) g->posted[(size_t)me * N + to].clear();
+      for (const Op& o : sends) g->posted[(size_t)me * N + o.peer].push_back({o.p, o.bytes});
+    }
+    int st = group_barrier(*g);
+    if (st) return st;
+    std::vector<size_t> nth(N, 0);
+    std::vector<char> waited(N, 0);
+    for (const Op& o : recvs) {
+      const auto& lst = g->posted[(size_t)o.peer * N + me];
+      if (nth[o.peer] >= lst.size() || lst[nth[o.peer]].bytes != o.bytes) {
+        if (err == RMX_OK) {
+          set_error("exchange group: rank " + std::to_string(me) + " receives " + std::to_string(o.bytes) +
+                    " bytes from rank " + std::to_string(o.peer) + " that posted no matching send");
+          err = RMX_E_COMM;
+        }
+        continue;
+      }
+      if (!waited[o.peer]) {
+        hip(hipStreamWaitEvent(s, g->ev_send[o.peer], 0), "hipStreamWaitEvent");
+        waited[o.peer] = 1;
+      }
+      hip(hipMemcpyAsync(o.p, lst[nth[o.peer]].src, o.bytes, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+      ++nth[o.peer];
+    }
+    hip(hipEventRecord(g->ev_done[me], s), "hipEventRecord");
+    if ((st = group_barrier(*g))) return st;
+    std::vector<char> sent(N, 0);
+    for (const Op& o : sends) sent[o.peer] = 1;
+    for (int p = 0; p < N; ++p)
+      if (sent[p]) hip(hipStreamWaitEvent(s, g->ev_done[p], 0), "hipStreamWaitEvent");
+    return err;
+  }
+};
+
+void group_unref(rmx_group* g) {
+  bool last;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    last = --g->refs == 0;
+  }
+  if (!last) return;
+  for (hipEvent_t e : g->ev_send)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : g->ev_done)
+    if (e) (void)hipEventDestroy(e);
+  delete g;
+}
+
+}  // namespace
+
+int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* unique_id, rmx_group* group,
+                 rmx_shard** out) {
   if (N < 1 || N > kMaxRanks || rank < 0 || rank >= N || V < N || k <= 0) {
     set_error("rmx_shard_create: bad arguments (need 1 <= nranks <= 64, 0 <= rank < nranks, rows >= nranks)");
     return RMX_E_INVALID;
@@ -340,6 +519,17 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
     set_error("rmx_shard_create: rows must fit int32 (ParRecModel.scala:282 .toInt)");
     return RMX_E_INVALID;
   }
+  if (group) {
+    std::lock_guard<std::mutex> lk(group->mu);
+    if (group->N != N) {
+      set_error("rmx_shard_create_group: nranks differs from the group's size");
+      return RMX_E_INVALID;
+    }
+    if (group->attached[rank]) {
+      set_error("rmx_shard_create_group: rank " + std::to_string(rank) + " of the group already has a shard");
+      return RMX_E_INVALID;
+    }
+  }
   RMX_HIP(hipSetDevice(ctx->device));
   std::unique_ptr<rmx_shard> sh(new rmx_shard());
   sh->ctx = ctx;
@@ -347,7 +537,7 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
   sh->k = k;
   sh->N = N;
   sh->rank = rank;
-  sh->loopback = unique_id == nullptr;
+  sh->loopback = unique_id == nullptr && group == nullptr;
   sh->rows_per = (V + N - 1) / N;
   const int parts = sh->loopback ? N : 1;
   for (int p = 0; p < parts; ++p) {
@@ -367,10 +557,21 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
   }
   RMX_HIP(hipMalloc(&sh->counts, sizeof(int32_t) * 4 * N));
   RMX_HIP(hipHostMalloc(&sh->h_counts, sizeof(int32_t) * 2 * N));
-  if (!sh->loopback) {
+  if (group) {
+    std::lock_guard<std::mutex> lk(group->mu);
+    if (!group->ev_send[rank]) {
+      RMX_HIP(hipEventCreateWithFlags(&group->ev_send[rank], hipEventDisableTiming));
+      RMX_HIP(hipEventCreateWithFlags(&group->ev_done[rank], hipEventDisableTiming));
+    }
+    group->attached[rank] = 1;
+    ++group->refs;
+    sh->group = group;
+    sh->tr.reset(new LocalTransport(group, rank));
+  } else if (!sh->loopback) {
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     RMX_NCCL(ncclCommInitRank(&sh->comm, N, id, rank));
+    sh->tr.reset(new RcclTransport(sh->comm));
   }
   *out = sh.release();
   return RMX_OK;
@@ -379,8 +580,16 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
 int shard_destroy(rmx_shard* sh) {
   if (!sh) return RMX_OK;
   (void)hipSetDevice(sh->ctx->device);
-  (void)hipStreamSynchronize(sh->ctx->stream);
+  (void)hipDeviceSynchronize();  // the exchange may have run on any stream
+  sh->tr.reset();
   if (sh->comm) ncclCommDestroy(sh->comm);
+  if (sh->group) {
+    {
+      std::lock_guard<std::mutex> lk(sh->group->mu);
+      sh->group->attached[sh->rank] = 0;
+    }
+    group_unref(sh->group);
+  }
   for (size_t i = 0; i < sh->emb.size(); ++i) {
     (void)hipFree(sh->emb[i]);
     (void)hipFree(sh->w[i]);
@@ -430,10 +639,10 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
   // (auto at one rank: off -- no link traffic to save, the duplicates' rows are local reads)
   const bool dd = nnz > 0 && (sh.dedupe == 1 || (sh.dedupe == 2 && sh.N > 1 && sh.dedupe_skip == 0));
+  int64_t rn = nnz;
   if (nnz > 0) {
     // route the batch's ids, or (dedupe) the distinct ids held by the hash set's slots
     const int32_t* rids = d_ids;
-    int64_t rn = nnz;
     int32_t* rslot = sh.perm;
     if (dd) {
       RMX_HIP(hipMemsetAsync(sh.hkeys, 0xFF, sizeof(int32_t) * sh.cap_hash, s));
@@ -460,12 +669,13 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
       RMX_HIP(hipGetLastError());
     }
   }
-  if (!sh.comm) {
+  if (sh.loopback) {
     // loopback: partition o serves bucket o in place
     RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * N, hipMemcpyDeviceToHost, s));
     RMX_HIP(hipStreamSynchronize(s));
     int64_t off = 0;
     sh.last_sent = 0;
+    sh.last_sent_dev = false;
     for (int o = 0; o < N; ++o) sh.last_sent += sh.h_counts[o];
     dedupe_auto(sh, dd, nnz);
     for (int o = 0; o < N; ++o) {
@@ -477,67 +687,72 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     }
     return RMX_OK;
   }
-  // 2. counts
-  RMX_NCCL(ncclGroupStart());
-  for (int o = 0; o < N; ++o) {
-    RMX_NCCL(ncclSend(cnt + o, 1, ncclInt32, o, sh.comm, s));
-    RMX_NCCL(ncclRecv(rcnt + o, 1, ncclInt32, o, sh.comm, s));
+  if (N == 1) {
+    // one rank: no exchange.  The bucket is this rank's own; its size (nnz, or the distinct ids
+    // when deduplicating) stays on the device and bounds the gather there -- no host sync.
+    sh.last_sent = nnz;
+    sh.last_sent_dev = dd;
+    dedupe_auto(sh, dd, nnz);
+    return launch_owner_gather(s, nnz, k, sh.send_ids, sh.emb[0], sh.w[0], sh.recv_emb, sh.recv_w,
+                               dd ? cnt : nullptr);
   }
-  RMX_NCCL(ncclGroupEnd());
+  Transport& tr = *sh.tr;
+  const int me = sh.rank;
+  // 2. counts: one int to every peer, then one D2H of the 2N counts (the only host sync: the
+  //    transport needs host-side message sizes); this rank's own entry is a local copy
+  if ((st = tr.start())) return st;
+  for (int o = 0; o < N; ++o) {
+    if (o == me) continue;
+    if ((st = tr.send(cnt + o, sizeof(int32_t), o, s)) || (st = tr.recv(rcnt + o, sizeof(int32_t), o, s))) return st;
+  }
+  if ((st = tr.end(s))) return st;
   RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * 2 * N, hipMemcpyDeviceToHost, s));
   RMX_HIP(hipStreamSynchronize(s));
   const int32_t* hc = sh.h_counts;
-  const int32_t* hr = sh.h_counts + N;
-  int64_t nrecv = 0;
+  int32_t* hr = sh.h_counts + N;
+  hr[me] = hc[me];
   sh.last_sent = 0;
-  for (int o = 0; o < N; ++o) {
-    nrecv += hr[o];
-    sh.last_sent += hc[o];
-  }
+  sh.last_sent_dev = false;
+  for (int o = 0; o < N; ++o) sh.last_sent += hc[o];
   dedupe_auto(sh, dd, nnz);
-  if ((st = ensure_recv(sh, nrecv))) return st;
-  // this rank's own bucket never goes through RCCL: its rows are gathered straight into the
-  // requester-order slots (hr[me] == hc[me]); at one rank the exchange is that gather alone
-  const int me = sh.rank;
-  int64_t so_me = 0, ro_me = 0;
-  for (int o = 0; o < me; ++o) {
-    so_me += hc[o];
-    ro_me += hr[o];
+  // Owner-side buffers hold the PEERS' requests only: peer o's range starts at ro(o) = sum of
+  // hr[p] over p < o, p != me.  The own bucket never goes through the transport: its rows are
+  // gathered straight into their requester-order slots [so_me, so_me + hc[me]).
+  int64_t npeer = 0, so_me = 0;
+  for (int o = 0; o < N; ++o) {
+    if (o != me) npeer += hr[o];
+    if (o < me) so_me += hc[o];
   }
+  if ((st = ensure_recv(sh, npeer))) return st;
   // 3. ids to owners
-  RMX_NCCL(ncclGroupStart());
-  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += hr[o], ++o) {
+  if ((st = tr.start())) return st;
+  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += (o == me ? 0 : hr[o]), ++o) {
     if (o == me) continue;
-    if (hc[o]) RMX_NCCL(ncclSend(sh.send_ids + so, hc[o], ncclInt32, (int)o, sh.comm, s));
-    if (hr[o]) RMX_NCCL(ncclRecv(sh.recv_ids + ro, hr[o], ncclInt32, (int)o, sh.comm, s));
+    if (hc[o] && (st = tr.send(sh.send_ids + so, sizeof(int32_t) * hc[o], (int)o, s))) return st;
+    if (hr[o] && (st = tr.recv(sh.recv_ids + ro, sizeof(int32_t) * hr[o], (int)o, s))) return st;
   }
-  RMX_NCCL(ncclGroupEnd());
-  // 4. owner gather: the peers' requests (the ranges before and after this rank's own), then the own bucket
-  if (ro_me > 0 &&
-      (st = launch_owner_gather(s, ro_me, k, sh.recv_ids, sh.emb[0], sh.w[0], sh.send_emb, sh.send_w)))
-    return st;
-  const int64_t r1 = ro_me + hr[me];
-  if (nrecv > r1 && (st = launch_owner_gather(s, nrecv - r1, k, sh.recv_ids + r1, sh.emb[0], sh.w[0],
-                                              sh.send_emb + r1 * k, sh.send_w + r1)))
-    return st;
+  if ((st = tr.end(s))) return st;
+  // 4. owner gather: every peer's request in one launch, then the own bucket
+  if ((st = launch_owner_gather(s, npeer, k, sh.recv_ids, sh.emb[0], sh.w[0], sh.send_emb, sh.send_w))) return st;
   if ((st = launch_owner_gather(s, hc[me], k, sh.send_ids + so_me, sh.emb[0], sh.w[0], sh.recv_emb + so_me * k,
                                 sh.recv_w + so_me)))
     return st;
   // 5. rows back, into the requester's bucket order
-  RMX_NCCL(ncclGroupStart());
-  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += hr[o], ++o) {
+  if ((st = tr.start())) return st;
+  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += (o == me ? 0 : hr[o]), ++o) {
     if (o == me) continue;
     if (hr[o]) {
-      RMX_NCCL(ncclSend(sh.send_emb + ro * k, (size_t)hr[o] * k, ncclFloat32, (int)o, sh.comm, s));
-      RMX_NCCL(ncclSend(sh.send_w + ro, hr[o], ncclFloat32, (int)o, sh.comm, s));
+      if ((st = tr.send(sh.send_emb + ro * k, sizeof(float) * hr[o] * k, (int)o, s)) ||
+          (st = tr.send(sh.send_w + ro, sizeof(float) * hr[o], (int)o, s)))
+        return st;
     }
     if (hc[o]) {
-      RMX_NCCL(ncclRecv(sh.recv_emb + so * k, (size_t)hc[o] * k, ncclFloat32, (int)o, sh.comm, s));
-      RMX_NCCL(ncclRecv(sh.recv_w + so, hc[o], ncclFloat32, (int)o, sh.comm, s));
+      if ((st = tr.recv(sh.recv_emb + so * k, sizeof(float) * hc[o] * k, (int)o, s)) ||
+          (st = tr.recv(sh.recv_w + so, sizeof(float) * hc[o], (int)o, s)))
+        return st;
     }
   }
-  RMX_NCCL(ncclGroupEnd());
-  return RMX_OK;
+  return tr.end(s);
 }
 
 }  // namespace rmx
@@ -562,7 +777,36 @@ extern "C" int rmx_shard_create(rmx_ctx* ctx, int64_t num_rows, int embedding_di
     set_error("rmx_shard_create: bad args");
     return RMX_E_INVALID;
   }
-  return shard_create(ctx, num_rows, embedding_dim, nranks, rank, unique_id, out);
+  return shard_create(ctx, num_rows, embedding_dim, nranks, rank, unique_id, nullptr, out);
+}
+
+extern "C" int rmx_group_create(int nranks, rmx_group** out) {
+  if (!out || nranks < 1 || nranks > kMaxRanks) {
+    set_error("rmx_group_create: need 1 <= nranks <= 64");
+    return RMX_E_INVALID;
+  }
+  auto* g = new rmx_group();
+  g->N = nranks;
+  g->posted.resize((size_t)nranks * nranks);
+  g->ev_send.assign(nranks, nullptr);
+  g->ev_done.assign(nranks, nullptr);
+  g->attached.assign(nranks, 0);
+  *out = g;
+  return RMX_OK;
+}
+
+extern "C" int rmx_group_destroy(rmx_group* g) {
+  if (g) group_unref(g);  // the group lives on until its last shard is destroyed
+  return RMX_OK;
+}
+
+extern "C" int rmx_shard_create_group(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, rmx_group* group, int rank,
+                                      rmx_shard** out) {
+  if (!ctx || !out || !group) {
+    set_error("rmx_shard_create_group: bad args");
+    return RMX_E_INVALID;
+  }
+  return shard_create(ctx, num_rows, embedding_dim, group->N, rank, nullptr, group, out);
 }
 
 extern "C" int rmx_shard_destroy(rmx_shard* sh) { return shard_destroy(sh); }
@@ -582,12 +826,27 @@ extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
     set_error("rmx_shard_set_dedupe: NULL shard");
     return RMX_E_INVALID;
   }
-  sh->dedupe = on == 2 ? 2 : (on != 0 ? 1 : 0);
+  if (on < 0 || on > 2) {
+    set_error("rmx_shard_set_dedupe: on must be 0 (off), 1 (on) or 2 (auto)");
+    return RMX_E_INVALID;
+  }
+  sh->dedupe = on;
   sh->dedupe_skip = 0;
   return RMX_OK;
 }
 
-extern "C" int64_t rmx_shard_last_sent(const rmx_shard* sh) { return sh ? sh->last_sent : -1; }
+extern "C" int64_t rmx_shard_last_sent(const rmx_shard* sh) {
+  if (!sh) return -1;
+  if (sh->last_sent_dev) {  // one rank, deduplicated: the distinct count is counts[0] on the device
+    int32_t c = 0;
+    if (hipSetDevice(sh->ctx->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(&c, sh->counts, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+    sh->last_sent = c;
+    sh->last_sent_dev = false;
+  }
+  return sh->last_sent;
+}
 
 extern "C" int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
                                 void* stream) {

@@ -21,7 +21,7 @@ from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT
 import ctypes
 
 __all__ = ["RecModelType", "CooLongFloatMatrix", "RecModel", "LR", "DeepFM", "XDeepFM", "DCN", "PNN", "DNN",
-           "Context", "DeviceArray", "EmbeddingTable", "ShardedTable", "comm_unique_id", "SampleParser", "RmxError", "IllegalArgumentError",
+           "Context", "DeviceArray", "EmbeddingTable", "ShardedTable", "ExchangeGroup", "comm_unique_id", "SampleParser", "RmxError", "IllegalArgumentError",
            "ShapeError", "MatsError", "default_context", "set_device"]
 
 MODEL_LR, MODEL_DEEPFM, MODEL_XDEEPFM, MODEL_DCN, MODEL_PNN, MODEL_DNN = range(6)
@@ -224,20 +224,50 @@ def comm_unique_id():
     return buf.raw
 
 
+class ExchangeGroup:
+    """In-process exchange group of nranks virtual ranks (rmx_group): ShardedTable(..., group=g) per
+    rank, each driven from its own thread with its own Context, runs the RCCL exchange schedule with
+    device copies as the transport (the N > 1 exchange on one GPU)."""
+
+    def __init__(self, nranks):
+        h = ctypes.c_void_p()
+        check(_lib.lib.rmx_group_create(int(nranks), ctypes.byref(h)))
+        self.handle = h
+        self.nranks = int(nranks)
+
+    def close(self):
+        if self.handle:
+            _lib.lib.rmx_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ShardedTable:
     """Hash-sharded table (owner = id mod nranks) over nranks processes, one GPU each, exchanging ids
     and rows over RCCL (replaces the PS partitions + sparse pulls, ParRecModel.scala:74-105, :165-199).
     unique_id=None makes a loopback shard: all partitions in this process (single-GPU testing)."""
 
-    def __init__(self, ctx, num_rows, embedding_dim, nranks, rank=0, unique_id=None):
+    def __init__(self, ctx, num_rows, embedding_dim, nranks, rank=0, unique_id=None, group=None):
         h = ctypes.c_void_p()
         uid = None
-        if unique_id is not None:
+        self.group = group  # keeps the ExchangeGroup alive as long as this shard
+        if group is not None:
+            if unique_id is not None or group.nranks != int(nranks):
+                raise ValueError("a group shard takes no unique_id and the group's nranks")
+            check(_lib.lib.rmx_shard_create_group(ctx.handle, int(num_rows), int(embedding_dim), group.handle,
+                                                  int(rank), ctypes.byref(h)))
+        elif unique_id is not None:
             if len(unique_id) != _lib.UNIQUE_ID_BYTES:
                 raise ValueError("unique_id must have %d bytes" % _lib.UNIQUE_ID_BYTES)
             uid = ctypes.create_string_buffer(bytes(unique_id), _lib.UNIQUE_ID_BYTES)
-        check(_lib.lib.rmx_shard_create(ctx.handle, int(num_rows), int(embedding_dim), int(nranks), int(rank),
-                                        uid, ctypes.byref(h)))
+        if group is None:
+            check(_lib.lib.rmx_shard_create(ctx.handle, int(num_rows), int(embedding_dim), int(nranks), int(rank),
+                                            uid, ctypes.byref(h)))
         self.handle = h
         self.ctx = ctx
         self.rows = int(num_rows)
@@ -255,7 +285,13 @@ class ShardedTable:
         """Send each distinct id of a batch once (ParRecModel.distinctIntIndices): True, False or
         "auto" (the default: off at one rank, else on, then off for 63 batches when it removed < 10 %
         of the ids)."""
-        check(_lib.lib.rmx_shard_set_dedupe(self.handle, 2 if on == "auto" else (1 if on else 0)))
+        if on == "auto":
+            mode = 2
+        elif on is True or on is False:
+            mode = int(on)
+        else:
+            raise ValueError('set_dedupe takes True, False or "auto", got %r' % (on,))
+        check(_lib.lib.rmx_shard_set_dedupe(self.handle, mode))
 
     def last_sent(self):
         """Ids this rank sent to owners in its last exchange."""

@@ -90,6 +90,9 @@ SIGNATURES = [
     ("rmx_comm_unique_id", c_int, [c_vp, c_sz]),
     ("rmx_shard_create", c_int, [c_vp, c_i64, c_int, c_int, c_int, c_vp, P(c_vp)]),
     ("rmx_shard_destroy", c_int, [c_vp]),
+    ("rmx_group_create", c_int, [c_int, P(c_vp)]),
+    ("rmx_group_destroy", c_int, [c_vp]),
+    ("rmx_shard_create_group", c_int, [c_vp, c_i64, c_int, c_vp, c_int, P(c_vp)]),
     ("rmx_shard_fill_synthetic", c_int, [c_vp, c_u64]),
     ("rmx_shard_local_rows", c_i64, [c_vp]),
     ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),

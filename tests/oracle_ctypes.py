@@ -122,6 +122,19 @@ def gen_table(seed, V, k, id0=0, nrows=None):
     return w, emb.reshape(nrows, k)
 
 
+def gen_rows(seed, V, k, ids):
+    """Gathered rows (w[n], E[n*k:(n+1)*k]) of the generated table for arbitrary ids, generating
+    only those rows (a V = 100M table need not exist on the host)."""
+    ids = np.asarray(ids, np.int64)
+    w = np.zeros(len(ids), np.float32)
+    e = np.zeros((len(ids), k), np.float32)
+    for i, idv in enumerate(ids):
+        wi, ei = gen_table(seed, V, k, int(idv), 1)
+        w[i] = wi[0]
+        e[i] = ei[0]
+    return w, e.ravel()
+
+
 def init_mats(m, seed):
     mats = np.zeros(mats_len(m), np.float32)
     lib().orc_init_mats(ctypes.byref(m), seed, _p(mats, ctypes.c_float))

@@ -3,8 +3,13 @@
 CPU (gloo, world_size 2): the exchange protocol restated in tests/shard_ref.py over a real
 torch.distributed all-to-all reproduces the global table's rows bit-exactly and the same forward.
 GPU: librmx's sharded path gives BITWISE the outputs of the replicated table -- the exchange only
-copies rows -- for loopback shards (N partitions on one GPU: routing / owner gather at N > 1) and for
-an RCCL communicator of one rank (the grouped send/recv code path).
+copies rows -- for
+  * exchange-group shards (rmx_group: N virtual ranks, one thread + context + stream each, on one
+    GPU): the product's N > 1 schedule -- counts, ids to owners, owner gather, rows back, the
+    own-bucket skip and the peer-only owner buffers -- with device copies as the transport;
+  * loopback shards (N partitions in one shard: routing / owner gather at N > 1, single thread);
+  * an RCCL communicator of one rank (no exchange: route + the own-bucket gather, sized on the
+    device).
 """
 import os
 import socket
@@ -173,7 +178,8 @@ def test_sharded_forward_bitwise_equals_replicated(kind, N, zipf, dedupe):
 
 @pytest.mark.gpu
 def test_rccl_single_rank_shard_matches_replicated():
-    """The RCCL code path (grouped send/recv to self) on a one-rank communicator."""
+    """A one-rank RCCL communicator: no exchange (route + the own-bucket gather, no RCCL op and no
+    host sync); the group tests above run the N > 1 schedule."""
     import rmx
     ctx = rmx.default_context()
     V, B = 200_000, 2048
@@ -208,3 +214,174 @@ def test_shard_bad_args():
         rmx.ShardedTable(ctx, 10, K, 0)
     with pytest.raises(rmx.RmxError):
         rmx.ShardedTable(ctx, 10, K, 2, 2)
+
+
+# --------------------------------------------------- exchange group (N virtual ranks) ----
+def _run_ranks(N, fn, timeout=300):
+    """fn(rank) on N threads (each rank drives its own context / stream, like N processes)."""
+    import threading
+    res, errs = [None] * N, []
+
+    def run(r):
+        try:
+            res[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below with the rank
+            errs.append((r, e))
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(N)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in ts), "a rank hung"
+    if errs:
+        raise AssertionError("rank %d failed: %r" % errs[0])
+    return res
+
+
+def _group_forward(kind, N, V, B, zipf, dedupe, reps=2):
+    import rmx
+    g = rmx.ExchangeGroup(N)
+
+    def rank(r):
+        ctx = rmx.Context(0)
+        sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+        sh.set_dedupe(dedupe)
+        sh.fill_synthetic(SEED_TAB)
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        rmx.gen_ids(ctx, SEED_IDS, 11 + r * B, B, F, V, ids, zipf=zipf)
+        m = _models_v(V)[kind]()
+        m.setMats(m.initMats(SEED_MATS))
+        m.setBias(0.01)
+        got = rmx.DeviceArray(ctx, B, np.float32)
+        for _ in range(reps):  # buffers are reused across batches
+            m.forward_ids_sharded(sh, B, ids, got, ctx.stream)
+        ctx.sync()
+        out = (got.numpy(), ids.numpy(), sh.last_sent())
+        sh.close()
+        return out
+
+    return _run_ranks(N, rank)
+
+
+def _models_v(V):
+    import rmx
+    return {
+        "deepfm": lambda: rmx.DeepFM(V, F, K, [400, 400, 400]),
+        "xdeepfm": lambda: rmx.XDeepFM(V, F, K, [64, 32], [48, 32]),
+        "dcn": lambda: rmx.DCN(V, F, K, 3, [64, 32]),
+        "pnn": lambda: rmx.PNN(V, F, K, [48, 32]),
+        "lr": lambda: rmx.LR(V, F),
+    }
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dedupe", [True, False])
+@pytest.mark.parametrize("zipf", [0.0, 1.1])
+@pytest.mark.parametrize("N", [2, 4, 8])
+def test_group_exchange_forward_bitwise_equals_replicated(N, zipf, dedupe):
+    """The product's N > 1 exchange schedule (csrc/shard.hip steps 2-5) at N virtual ranks: every
+    rank's DeepFM forward is bitwise the replicated table's, and the ids it sent are its distinct ids
+    (dedupe) or all of them."""
+    import rmx
+    V, B = 100_003, 1000
+    outs = _group_forward("deepfm", N, V, B, zipf, dedupe)
+    ctx = rmx.default_context()
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    m = _models_v(V)["deepfm"]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    for r, (got, h_ids, sent) in enumerate(outs):
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        ids.upload(h_ids)
+        ref = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(table, B, ids, ref)
+        ctx.sync()
+        assert np.array_equal(got, ref.numpy()), r
+        assert sent == (len(np.unique(h_ids)) if dedupe else B * F), r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["xdeepfm", "dcn", "pnn", "lr"])
+def test_group_exchange_every_model(kind):
+    import rmx
+    V, B, N = 100_003, 600, 4
+    outs = _group_forward(kind, N, V, B, 1.1, True, reps=1)
+    ctx = rmx.default_context()
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    m = _models_v(V)[kind]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    for got, h_ids, _ in outs:
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        ids.upload(h_ids)
+        ref = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(table, B, ids, ref)
+        ctx.sync()
+        assert np.array_equal(got, ref.numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [2, 8])
+def test_group_exchange_gather_ragged(N):
+    """rmx_shard_gather through the group with different id counts per rank (one rank sends none):
+    the received rows are the generator's, bit for bit."""
+    import rmx
+    V = 50_021
+    g = rmx.ExchangeGroup(N)
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+
+    def rank(r):
+        ctx = rmx.Context(0)
+        sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+        sh.set_dedupe(r % 2 == 0)
+        sh.fill_synthetic(SEED_TAB)
+        n = 0 if r == 1 else 997 * (r + 1)
+        h_ids = np.random.default_rng(r).integers(0, V, max(n, 1)).astype(np.int32)[:n]
+        ids = rmx.DeviceArray(ctx, max(n, 1), np.int32)
+        if n:
+            ids.upload(h_ids)
+        w = rmx.DeviceArray(ctx, max(n, 1), np.float32)
+        e = rmx.DeviceArray(ctx, max(n, 1) * K, np.float32)
+        for _ in range(2):
+            sh.gather(ids, n, w, e, ctx.stream)
+        ctx.sync()
+        out = (h_ids, w.numpy()[:n], e.numpy()[:n * K])
+        sh.close()
+        return out
+
+    for h_ids, w, e in _run_ranks(N, rank):
+        w_ref, e_ref = oc.gather(wt, et, 1, h_ids.astype(np.int64))
+        assert np.array_equal(w, w_ref) and np.array_equal(e, e_ref)
+
+
+@pytest.mark.gpu
+def test_group_of_one_rank_dedupe_device_count():
+    """One rank: no exchange; with dedupe on, the gather is sized by the device-side distinct count
+    (no host sync) and last_sent reads it back."""
+    V, B = 100_003, 700
+    (got, h_ids, sent), = _group_forward("deepfm", 1, V, B, 1.1, True)
+    assert sent == len(np.unique(h_ids))
+
+
+@pytest.mark.gpu
+def test_group_exchange_100m_rows_vs_fp64_oracle():
+    """configs[3] at full size: V = 100M rows hash-sharded over 4 virtual ranks, B = 65,536 rows per
+    rank; head and tail slices of every rank's probabilities against the fp64 oracle, whose table rows
+    come from the same generator (only the rows the slices use are generated)."""
+    V, B, N = 100_000_000, 65536, 4
+    outs = _group_forward("deepfm", N, V, B, 0.0, "auto", reps=1)
+    om = oc.make_model(oc.DEEPFM, F, K, fc=(400, 400, 400))
+    mats = oc.init_mats(om, SEED_MATS)
+    n = 64
+    for got, h_ids, _ in outs:
+        ids2 = h_ids.reshape(B, F)
+        for rows in (slice(0, n), slice(B - n, B)):
+            sl = ids2[rows].astype(np.int64).ravel()
+            w, e = oc.gen_rows(SEED_TAB, V, K, sl)
+            index = np.repeat(np.arange(n, dtype=np.int64), F)
+            ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 1)
+            err = float(np.abs(got[rows] - ref).max())
+            assert err <= 1e-5, err
