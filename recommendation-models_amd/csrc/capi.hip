@@ -217,6 +217,8 @@ extern "C" int rmx_model_set_mats(rmx_model* m, const float* mats, int64_t n) {
               std::to_string(m->mats_len));
     return RMX_E_MATS;
   }
+  ModelUse use(*m, m->ctx->stream);  // in-flight calls on other streams still read the old weights
+  if (use.st) return use.st;
   return model_load_mats(*m, mats, /*sync=*/true);
 }
 
@@ -224,6 +226,8 @@ extern "C" int rmx_model_set_precision(rmx_model* m, int dtype) {
   CHECK_ARG(m, "rmx_model_set_precision: model is NULL");
   CHECK_ARG(m->ctx, "rmx_model_set_precision: host-only model (created without a context)");
   CHECK_ARG(dtype == RMX_DTYPE_F32 || dtype == RMX_DTYPE_BF16, "rmx_model_set_precision: dtype must be F32 or BF16");
+  ModelUse use(*m, m->ctx->stream);
+  if (use.st) return use.st;
   if (dtype == m->precision) return RMX_OK;
   if (dtype == RMX_DTYPE_BF16 && m->type == RMX_MODEL_XDEEPFM) {
     set_error("rmx_model_set_precision: the xDeepFM CIN runs in fp32 only");
@@ -234,6 +238,7 @@ extern "C" int rmx_model_set_precision(rmx_model* m, int dtype) {
 
 extern "C" int rmx_model_set_bias(rmx_model* m, float bias) {
   CHECK_ARG(m, "rmx_model_set_bias: model is NULL");
+  std::lock_guard<std::mutex> lk(m->mu);
   m->beta = bias;
   m->beta_set = true;
   return RMX_OK;
@@ -241,6 +246,7 @@ extern "C" int rmx_model_set_bias(rmx_model* m, float bias) {
 
 extern "C" int rmx_model_set_timing(rmx_model* m, int enable) {
   CHECK_ARG(m, "rmx_model_set_timing: model is NULL");
+  std::lock_guard<std::mutex> lk(m->mu);
   m->timing = enable != 0;
   m->stage_names.clear();
   m->stage_ms.clear();
@@ -251,6 +257,7 @@ extern "C" int rmx_model_set_timing(rmx_model* m, int enable) {
 extern "C" int rmx_model_get_timing(rmx_model* m, char* names, int name_stride, float* ms, int cap, int* n,
                                     int* calls) {
   CHECK_ARG(m && n, "rmx_model_get_timing: bad args");
+  std::lock_guard<std::mutex> lk(m->mu);
   const int st = model_collect_timing(*m);
   if (st != RMX_OK) return st;
   *n = (int)m->stage_names.size();
@@ -410,6 +417,8 @@ extern "C" int rmx_forward_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
   }
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  ModelUse use(*m, s);
+  if (use.st) return use.st;
   FwdInputs in;
   in.B = B;
   in.ids = d_ids;
@@ -494,6 +503,8 @@ extern "C" int rmx_forward(rmx_model* m, int32_t B, int64_t nnz, const int64_t* 
   if (st) return st;
   if (B == 0) return RMX_OK;
   RMX_HIP(hipSetDevice(m->ctx->device));
+  ModelUse use(*m, m->ctx->stream);
+  if (use.st) return use.st;
   return model_forward_host(*m, B, nnz, index, regular, sorted, bias[0], weights, embedding, mats, out);
 }
 
@@ -523,6 +534,8 @@ extern "C" int rmx_backward_ids(rmx_model* m, const rmx_table* t, int32_t B, con
   }
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  ModelUse use(*m, s);
+  if (use.st) return use.st;
   FwdInputs in;
   in.B = B;
   in.ids = d_ids;
@@ -561,12 +574,14 @@ extern "C" int rmx_backward(rmx_model* m, int32_t B, int64_t nnz, const int64_t*
   }
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = m->ctx->stream;
+  ModelUse use(*m, s);
+  if (use.st) return use.st;
   FwdInputs in;
   if ((st = model_stage_host(*m, B, nnz, index, regular, sorted, bias[0], weights, embedding, mats, &in))) return st;
   rmx_model::LaGrad* lb = &m->la_grad;
   const bool use_w = m->type != RMX_MODEL_DNN, use_e = m->type != RMX_MODEL_LR;
   if (nnz > lb->nnz || B > lb->B || m->mats_len > lb->ml) {
-    RMX_HIP(hipStreamSynchronize(s));
+    RMX_HIP(hipDeviceSynchronize());
     for (void* p : {(void*)lb->gw, (void*)lb->ge, (void*)lb->gm, (void*)lb->gb, (void*)lb->tg, (void*)lb->idx})
       if (p) (void)hipFree(p);
     *lb = rmx_model::LaGrad{};

@@ -170,6 +170,8 @@ extern "C" int rmx_predict_ids(rmx_model* m, const rmx_table* t, int64_t n_rows,
   }
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  ModelUse use(*m, s);
+  if (use.st) return use.st;
   for (int64_t r0 = 0; r0 < n_rows; r0 += batch) {
     FwdInputs in;
     in.B = (int)std::min<int64_t>(batch, n_rows - r0);

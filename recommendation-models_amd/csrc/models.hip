@@ -408,7 +408,9 @@ void model_release(rmx_model& m) {
   m.la_grad = rmx_model::LaGrad{};
   if (!m.ctx) return;
   (void)hipSetDevice(m.ctx->device);
-  (void)hipStreamSynchronize(m.ctx->stream);
+  (void)hipDeviceSynchronize();  // the last calls may have run on any stream
+  if (m.ws_fence) (void)hipEventDestroy(m.ws_fence);
+  m.ws_fence = nullptr;
   dev_free(m.mats_dev);
   for (auto& L : m.layers) {
     dev_free(L.W);
@@ -551,7 +553,7 @@ namespace {
 
 int ensure_ws(rmx_model& m, int B) {
   if (B <= m.ws_B) return RMX_OK;
-  RMX_HIP(hipStreamSynchronize(m.ctx->stream));
+  RMX_HIP(hipDeviceSynchronize());  // earlier calls on any stream may still read the old buffers
   dev_free(m.h[0]);
   dev_free(m.h[1]);
   dev_free(m.y12);
@@ -770,7 +772,7 @@ int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, boo
   hipStream_t s = m.ctx->stream;
   int st;
   if (nnz > m.la_nnz) {
-    RMX_HIP(hipStreamSynchronize(s));
+    RMX_HIP(hipDeviceSynchronize());
     dev_free(m.la_E);
     dev_free(m.la_w);
     if (m.type != RMX_MODEL_LR && (st = dev_alloc(&m.la_E, (size_t)nnz * m.k))) return st;
@@ -778,7 +780,7 @@ int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, boo
     m.la_nnz = nnz;
   }
   if (B > m.la_B) {
-    RMX_HIP(hipStreamSynchronize(s));
+    RMX_HIP(hipDeviceSynchronize());
     dev_free(m.la_out);
     dev_free(m.la_rowptr);
     if ((st = dev_alloc(&m.la_out, B))) return st;
@@ -813,7 +815,7 @@ int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, boo
     // a bf16 model reads the caller's fp32 arrays as a bf16 table: round them once on the device
     // (la_w in place too, so the Scatter first order below sums the rounded weights)
     if (nnz * std::max(m.k, 1) > m.la16_cap) {
-      RMX_HIP(hipStreamSynchronize(s));
+      RMX_HIP(hipDeviceSynchronize());
       dev_free(m.la_E16);
       dev_free(m.la_w16);
       if (hipMalloc(&m.la_E16, sizeof(bf16_t) * nnz * std::max(m.k, 1)) != hipSuccess ||

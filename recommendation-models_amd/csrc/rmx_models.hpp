@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -119,6 +120,12 @@ struct rmx_model {
     int32_t* idx = nullptr;
   } la_grad;
 
+  // ---- reentrancy (rmx.h "Threading"): one caller at a time; calls on different streams are
+  //      ordered on the device by an event (rmx::ModelUse) ----
+  std::mutex mu;
+  hipStream_t ws_stream = nullptr;  // stream of the last call that used the workspace
+  hipEvent_t ws_fence = nullptr;    // recorded on it at the end of that call
+
   // ---- stage timing ----
   bool timing = false;
   int timed_calls = 0;
@@ -159,6 +166,32 @@ struct TrainOutputs {
 };
 int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOutputs& o);
 void train_release(rmx_model& m);
+
+// Serialises the callers of one model (its workspace, staging buffers and timing state are shared):
+// the host lock is held for the whole call, and the call's last queued work is marked by an event;
+// a call on another stream than the previous one first makes its stream wait for that event, so
+// the previous call's kernels are done with the workspace before this call's run.  (The event is
+// recorded at the end of every call, while the caller's stream is known to be alive.)
+template <class T>
+struct StreamUse {
+  T& o;
+  hipStream_t s;
+  std::unique_lock<std::mutex> lk;
+  int st = RMX_OK;
+  StreamUse(T& oo, hipStream_t ss) : o(oo), s(ss), lk(oo.mu) {
+    if (!o.ws_fence && hipEventCreateWithFlags(&o.ws_fence, hipEventDisableTiming) != hipSuccess) {
+      o.ws_fence = nullptr;
+      st = RMX_E_HIP;
+    } else if (o.ws_stream && o.ws_stream != s && hipStreamWaitEvent(s, o.ws_fence, 0) != hipSuccess) {
+      st = RMX_E_HIP;
+    }
+    if (st) set_error("stream hand-over: HIP event create / wait failed");
+  }
+  ~StreamUse() {
+    if (o.ws_fence && hipEventRecord(o.ws_fence, s) == hipSuccess) o.ws_stream = s;
+  }
+};
+typedef StreamUse<rmx_model> ModelUse;
 
 // Records HIP events around a stage on stream s when the model's timing is enabled.
 struct StageTimer {

@@ -115,6 +115,11 @@ struct rmx_shard {
   mutable bool last_sent_dev = false;   // one rank: last_sent is still on the device (counts[0])
   int32_t* bcnt = nullptr;              // [N][tiles] per-tile owner counts -> tile start offsets
   int64_t cap_tiles = 0;
+  // one exchange at a time per shard; the per-batch buffers are ordered across streams like a
+  // model's workspace (rmx::ModelUse)
+  std::mutex mu;
+  hipStream_t ws_stream = nullptr;
+  hipEvent_t ws_fence = nullptr;
 };
 
 namespace rmx {
@@ -361,6 +366,9 @@ int ensure_recv(rmx_shard& sh, int64_t n) {
   return RMX_OK;
 }
 
+// the shard's lock + cross-stream order of its per-batch buffers (see rmx::StreamUse)
+typedef StreamUse<rmx_shard> ShardUse;
+
 int launch_owner_gather(hipStream_t s, int64_t n, int k, const int32_t* rows, const float* emb, const float* w,
                         float* out_emb, float* out_w, const int32_t* dcount = nullptr) {
   if (n <= 0) return RMX_OK;
@@ -582,6 +590,7 @@ int shard_destroy(rmx_shard* sh) {
   (void)hipSetDevice(sh->ctx->device);
   (void)hipDeviceSynchronize();  // the exchange may have run on any stream
   sh->tr.reset();
+  if (sh->ws_fence) (void)hipEventDestroy(sh->ws_fence);
   if (sh->comm) ncclCommDestroy(sh->comm);
   if (sh->group) {
     {
@@ -830,6 +839,7 @@ extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
     set_error("rmx_shard_set_dedupe: on must be 0 (off), 1 (on) or 2 (auto)");
     return RMX_E_INVALID;
   }
+  std::lock_guard<std::mutex> lk(sh->mu);
   sh->dedupe = on;
   sh->dedupe_skip = 0;
   return RMX_OK;
@@ -856,6 +866,8 @@ extern "C" int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, 
   }
   RMX_HIP(hipSetDevice(sh->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : sh->ctx->stream;
+  ShardUse use(*sh, s);
+  if (use.st) return use.st;
   int st = shard_exchange(*sh, s, n, d_ids);
   if (st) return st;
   // un-permute into id order: d_emb[i] = recv_emb[perm[i]]
@@ -886,6 +898,10 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
   }
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  ShardUse suse(*sh, s);  // lock order: shard, then model
+  if (suse.st) return suse.st;
+  ModelUse use(*m, s);
+  if (use.st) return use.st;
   int st;
   {
     StageTimer t(*m, s, "shard_exchange");
