@@ -4,7 +4,10 @@
 Workload (default, configs[1]): DeepFM fp32, 39 fields / 1M vocab / k = 16, fcDims 400,400,400,
 over a 1M-row synthetic set whose ids and table live in HBM before timing starts.  One step =
 one forward (gather + first order + FM + tower + sigmoid) over one batch of --batch rows of that
-set; successive steps walk the set.  --workload xdeepfm runs configs[2] (CIN 200,200,200).
+set; successive steps walk the set.  The default line also carries an "models.xdeepfm" sub-record
+(configs[2], CIN 200,200,200 at B = 16,384): BASELINE.json's metric names DeepFM and xDeepFM.
+Other workloads: xdeepfm, deepfm_sharded (configs[3]), dcn_bf16 / pnn_bf16 (configs[4]),
+lr_plumbing (configs[0]: LIBSVM text -> parse -> LR predict -> AUC), deepfm_train / xdeepfm_train.
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank owns a replica of the 1M-row
 table and its own batches (replicas only: the V = 1M forward has no exchange step), so
@@ -27,7 +30,8 @@ F, K, V = 39, 16, 1_000_000
 FC = [400, 400, 400]
 CIN = [200, 200, 200]
 ROWS = 1 << 20  # the "1M-row synthetic" set
-SEED_IDS, SEED_TAB, SEED_MATS = 0x5EED2026, 0x7AB1E, 0x3A75
+SEED_IDS, SEED_TAB, SEED_MATS, SEED_LAB = 0x5EED2026, 0x7AB1E, 0x3A75, 0x1AB3
+PLUMB_ROWS, PLUMB_BATCH = 1000, 100  # configs[0]: 1k-row LIBSVM slice, batchSize 100 (LRLocalExample.scala:16)
 
 # Peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
@@ -47,14 +51,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded", "dcn_bf16", "pnn_bf16",
-                                           "deepfm_train", "xdeepfm_train"],
+                                           "deepfm_train", "xdeepfm_train", "lr_plumbing"],
                     default="deepfm")
+    ap.add_argument("--no-companion", action="store_true",
+                    help="deepfm: skip the xDeepFM sub-record (BASELINE.json's metric names both models)")
     ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="Zipf exponent of the ids within a field (SURVEY.md §8d secondary; 0 = uniform)")
     ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step (default: auto)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline budget")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--set", default="", help="kernel knobs before building the model, k=v,k=v (rmx_set_tuning)")
     return ap.parse_args()
@@ -65,6 +71,8 @@ def stage_work(workload, stage, B):
     D = F * K
     P = F * (F - 1) // 2
     es = 2 if workload.endswith("bf16") else 4  # table element bytes
+    if stage == "first_order_sigmoid":  # LR: ids + w + p
+        return "byte", B * (F * 4 + F * es + 4)
     if stage == "shard_exchange":  # ids out + (k+1)-float rows back, all ranks' shares incl. self
         return "byte", B * F * (4 + 4 + (K + 1) * 4 * 2)
     if stage == "encoder_fm":  # ids + w + emb rows + y  (2,812 B / example)
@@ -101,29 +109,37 @@ def stage_work(workload, stage, B):
     return None, 0
 
 
-def cpu_baseline(workload, budget_s, threads):
-    """Oracle (C restatement, OpenMP) on the host cores: examples/s on bounded batches."""
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ctypes as oc
+    return oc
+
+
+def _oracle_model(oc, workload):
+    if workload.startswith("xdeepfm"):
+        return oc.make_model(oc.XDEEPFM, F, K, fc=tuple(FC), cin=tuple(CIN))
     if workload == "dcn_bf16":
-        om = oc.make_model(oc.DCN, F, K, fc=tuple(FC), cross_depth=3)
-        B = 4096
-    elif workload == "pnn_bf16":
-        om = oc.make_model(oc.PNN, F, K, fc=tuple(FC))
-        B = 4096
-    elif workload != "xdeepfm":  # deepfm_sharded: same per-example CPU work (V = 1M table on the host)
-        om = oc.make_model(oc.DEEPFM, F, K, fc=tuple(FC))
-        B = 4096
-    else:
-        om = oc.make_model(oc.XDEEPFM, F, K, fc=tuple(FC), cin=tuple(CIN))
-        B = 16
+        return oc.make_model(oc.DCN, F, K, fc=tuple(FC), cross_depth=3)
+    if workload == "pnn_bf16":
+        return oc.make_model(oc.PNN, F, K, fc=tuple(FC))
+    return oc.make_model(oc.DEEPFM, F, K, fc=tuple(FC))
+
+
+def cpu_baseline(workload, budget_s, threads):
+    """Oracle (C restatement, OpenMP) on the host cores: examples/s on bounded batches, the gather
+    (makeWeights / makeEmbeddings) included.  deepfm_sharded runs the same per-example CPU work on
+    the V = 1M table (the host cannot hold the sharded table's point: it is the same math)."""
+    oc = _oracle()
+    if workload == "lr_plumbing":
+        return cpu_baseline_plumbing(oc, budget_s, threads)
+    om = _oracle_model(oc, workload)
+    B = 16 if workload == "xdeepfm" else 4096
     mats = oc.init_mats(om, SEED_MATS)
-    # the table slice for the rows we touch is regenerated on the host (same generator)
     done, t_tot, row0 = 0, 0.0, 0
     wt, et = oc.gen_table(SEED_TAB, V, K)
+    bf16 = workload.endswith("bf16")
     while t_tot < budget_s:
         ids = oc.gen_ids(SEED_IDS, row0, B, F, V).astype(np.int64)
-        w, e = oc.gather(wt, et, 1, ids)  # makeWeights / makeEmbeddings are part of the CPU path
         index = np.repeat(np.arange(B, dtype=np.int64), F)
         t0 = time.perf_counter()
         w, e = oc.gather(wt, et, 1, ids)
@@ -133,30 +149,57 @@ def cpu_baseline(workload, budget_s, threads):
         row0 += B
     return {"value": done / t_tot, "unit": "examples/s", "cores": threads, "kind": "port",
             "sample": "%d rows (%d batches of %d) of the same synthetic %s workload, fp32 oracle "
-                      "(oracle/rmx_oracle.c, OpenMP, gather + forward), %.1f s"
-                      % (done, done // B, B, workload, t_tot)}
+                      "(oracle/rmx_oracle.c, OpenMP, gather + forward%s), %.1f s"
+                      % (done, done // B, B, workload, "; fp32 arithmetic on the bf16 model's shapes" if bf16 else "",
+                         t_tot)}
 
 
-def parity_check(workload, got, row0, n=512):
+def cpu_baseline_plumbing(oc, budget_s, threads):
+    """configs[0] on the host: the Python restatement of SampleParser (tests/ref_parser.py) + the
+    oracle's makeWeights gather and LR forward per 100-line batch + the AUC, over the 1k-row slice."""
+    import ref_parser
+    from test_metric import auc_ref
+    from rmx import synthetic
+    text, _, _ = synthetic.libsvm_text(SEED_IDS, SEED_LAB, 0, PLUMB_ROWS, F, V)
+    lines = text.splitlines()
+    wt, _ = oc.gen_table(SEED_TAB, V, 0)
+    om = oc.make_model(oc.LR)
+    bias = np.array([0.01], np.float32)
+    done, t_tot = 0, 0.0
+    while t_tot < budget_s:
+        t0 = time.perf_counter()
+        rows, cols, _, targets, _ = ref_parser.parse(lines)
+        scores = np.zeros(PLUMB_ROWS, np.float32)
+        for b0 in range(0, PLUMB_ROWS, PLUMB_BATCH):
+            lo, hi = np.searchsorted(rows, [b0, b0 + PLUMB_BATCH])
+            w, _ = oc.gather(wt, np.zeros((V, 0), np.float32), 1, cols[lo:hi])
+            scores[b0:b0 + PLUMB_BATCH] = oc.forward(om, PLUMB_BATCH, rows[lo:hi] - b0, bias, w, None, None, 0,
+                                                     threads)
+        auc_ref(targets, scores)
+        t_tot += time.perf_counter() - t0
+        done += PLUMB_ROWS
+    return {"value": done / t_tot, "unit": "examples/s", "cores": threads, "kind": "port",
+            "sample": "%d passes over the 1k-row LIBSVM slice: Python SampleParser restatement "
+                      "(tests/ref_parser.py) + oracle makeWeights + LR forward per 100-line batch "
+                      "(oracle/rmx_oracle.c) + Mann-Whitney AUC, %.1f s" % (done // PLUMB_ROWS, t_tot)}
+
+
+def parity_check(workload, got, row0, n=512, vocab=V):
     """The checker beside the CPU baseline: GPU probabilities of rows [row0, row0 + n) of the bench
     set against the oracle on the same rows (fp64 oracle; bf16 workloads: the oracle's bf16-storage
-    emulation, precision 2)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ctypes as oc
-    base = workload
-    if base == "xdeepfm":
-        om = oc.make_model(oc.XDEEPFM, F, K, fc=tuple(FC), cin=tuple(CIN))
+    emulation, precision 2).  A V = 100M table is not materialised on the host: the
+    oracle generates just the rows the checked ids use (same generator as the device)."""
+    oc = _oracle()
+    om = _oracle_model(oc, workload)
+    if workload == "xdeepfm":
         n = min(n, 64)
-    elif base == "dcn_bf16":
-        om = oc.make_model(oc.DCN, F, K, fc=tuple(FC), cross_depth=3)
-    elif base == "pnn_bf16":
-        om = oc.make_model(oc.PNN, F, K, fc=tuple(FC))
-    else:
-        om = oc.make_model(oc.DEEPFM, F, K, fc=tuple(FC))
     mats = oc.init_mats(om, SEED_MATS)
-    wt, et = oc.gen_table(SEED_TAB, V, K)
-    ids = oc.gen_ids(SEED_IDS, row0, n, F, V).astype(np.int64)
-    w, e = oc.gather(wt, et, 1, ids)
+    ids = oc.gen_ids(SEED_IDS, row0, n, F, vocab).astype(np.int64)
+    if vocab == V:
+        wt, et = oc.gen_table(SEED_TAB, V, K)
+        w, e = oc.gather(wt, et, 1, ids)
+    else:
+        w, e = oc.gen_rows(SEED_TAB, vocab, K, ids)
     index = np.repeat(np.arange(n, dtype=np.int64), F)
     bias = np.array([0.01], np.float32)
     if workload.endswith("bf16"):
@@ -166,7 +209,7 @@ def parity_check(workload, got, row0, n=512):
         ref = oc.forward(om, n, index, bias, w, e, mats, 1)
         tol, against = 1e-5, "fp64 oracle"
     err = float(np.abs(got[:n] - ref).max())
-    return {"rows": n, "max_abs_diff": err, "tol": tol, "against": against, "ok": err <= tol}
+    return {"rows": n, "row0": row0, "max_abs_diff": err, "tol": tol, "against": against, "ok": err <= tol}
 
 
 def cpu_model():
@@ -179,60 +222,151 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline_sweep(workload, budget_s, threads):
-    """All-core baseline (the reported value) + 1 and 2 threads (Spark local[1] / local[2]
-    analogues) on shorter bounded samples."""
-    res = cpu_baseline(workload, budget_s, threads)
-    res["by_threads"] = {str(threads): round(res["value"], 1)}
-    for t in (1, 2):
-        if t < threads:
-            res["by_threads"][str(t)] = round(cpu_baseline(workload, max(2.0, budget_s * 0.3), t)["value"], 1)
+def cpu_counts():
+    """(logical CPUs of the machine, CPUs this process may run on, cgroup CPU quota or None, physical
+    cores): the box shows the whole machine's CPUs while its cgroup grants a share of them."""
+    logical = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = logical
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    phys = set()
+    try:
+        pid = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                phys.add((pid, core))
+    except OSError:
+        pass
+    return logical, avail, quota, len(phys) or None
+
+
+def cpu_baseline_sweep(workload, budget_s, short=False):
+    """The baseline at all the cores this job may use (the reported value), plus 1 and 2 threads
+    (Spark local[1] / local[2] analogues) on shorter bounded samples."""
+    logical, avail, quota, phys = cpu_counts()
+    allc = min(avail, quota) if quota else avail
+    if workload == "lr_plumbing":
+        res = cpu_baseline(workload, budget_s, 2)  # configs[0] is the Spark local[2] run
+        res["by_threads"] = {"2": round(res["value"], 1)}
+    else:
+        res = cpu_baseline(workload, budget_s, allc)
+        res["by_threads"] = {str(allc): round(res["value"], 1)}
+        for t in (() if short else (1, 2)):
+            if t < allc:
+                res["by_threads"][str(t)] = round(cpu_baseline(workload, max(2.0, budget_s * 0.3), t)["value"], 1)
     res["cpu_model"] = cpu_model()
-    res["nproc"] = os.cpu_count()
+    res["logical_cpus"] = logical
+    res["physical_cores"] = phys
+    res["cpus_in_affinity"] = avail
+    res["cgroup_cpu_quota"] = quota
+    res["cores_note"] = ("all cores available to this job: min(affinity, cgroup quota)"
+                         if workload != "lr_plumbing" else "Spark local[2]: 2 threads")
     return res
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # CPU (gloo) barrier / max only: the GPU work is librmx
-        dist.init_process_group("gloo")
-    import rmx
-    for kv in filter(None, args.set.split(",")):
-        k_, v_ = kv.split("=")
-        rmx.set_tuning(k_, int(v_))
-
-    train = args.workload.endswith("_train")
-    base = args.workload[:-len("_train")] if train else args.workload
-    B = args.batch or ({"xdeepfm": 16384, "xdeepfm_train": 4096}.get(args.workload, 65536))
-    sharded = args.workload == "deepfm_sharded"
-    Vw = args.vocab or (100_000_000 if sharded else V)
-    # one rank per GPU; fewer GPUs than ranks (a rehearsal on a 1-GPU box) wraps ranks onto them
-    # (torch.cuda.device_count() does not initialise the GPU on this image)
-    ndev = 1
-    if world > 1:
-        import torch
-        ndev = max(1, torch.cuda.device_count())
-    if sharded and world > ndev:
-        raise SystemExit("deepfm_sharded needs one GPU per rank (RCCL rejects ranks sharing a GPU)")
-    rmx.set_device(local % ndev)
-    ctx = rmx.default_context()
-    stream = ctx.stream
-    bf16 = args.workload.endswith("bf16")
+def make_model(rmx, workload, Vw, ctx):
+    base = workload[:-len("_train")] if workload.endswith("_train") else workload
     if base == "xdeepfm":
-        model = rmx.XDeepFM(Vw, F, K, FC, CIN, ctx=ctx)
-    elif args.workload == "dcn_bf16":  # configs[4]: DCN depth 3 + fcDims 400^3, bf16 table / weights
-        model = rmx.DCN(Vw, F, K, 3, FC, ctx=ctx)
-    elif args.workload == "pnn_bf16":  # configs[4]: PNN (IPNN) D1 = 400, fcDims 400^3, bf16
-        model = rmx.PNN(Vw, F, K, FC, ctx=ctx)
-    else:
-        model = rmx.DeepFM(Vw, F, K, FC, ctx=ctx)
+        return rmx.XDeepFM(Vw, F, K, FC, CIN, ctx=ctx)
+    if base == "dcn_bf16":  # configs[4]: DCN depth 3 + fcDims 400^3, bf16 table / weights
+        return rmx.DCN(Vw, F, K, 3, FC, ctx=ctx)
+    if base == "pnn_bf16":  # configs[4]: PNN (IPNN) D1 = 400, fcDims 400^3, bf16
+        return rmx.PNN(Vw, F, K, FC, ctx=ctx)
+    if base == "lr_plumbing":
+        return rmx.LR(Vw, F, ctx=ctx)
+    return rmx.DeepFM(Vw, F, K, FC, ctx=ctx)
+
+
+def run_plumbing(args, rmx, ctx, rank, world, dist, steps, warmup):
+    """configs[0]: one step = one pass over a 1k-row LIBSVM slice (example/LRLocalExample.scala:13-58):
+    native parse at 2 threads (Spark local[2]) -> ids + labels to HBM -> LR predict loop of
+    100-row forwards (ParRecModel.predict, batchSize 100) -> device AUC."""
+    from rmx import synthetic
+    text, _, _ = synthetic.libsvm_text(SEED_IDS, SEED_LAB, rank * PLUMB_ROWS, PLUMB_ROWS, F, V)
+    blob = text.encode()
+    model = make_model(rmx, "lr_plumbing", V, ctx)
+    table = rmx.EmbeddingTable(ctx, V, 0)
+    table.fill_synthetic(SEED_TAB)
+    model.setBias(0.01)
+    ids = rmx.DeviceArray(ctx, PLUMB_ROWS * F, np.int32)
+    lab = rmx.DeviceArray(ctx, PLUMB_ROWS, np.float32)
+    scores = rmx.DeviceArray(ctx, PLUMB_ROWS, np.float32)
+    stream = ctx.stream
+    res = {}
+
+    def step():
+        s = rmx.Samples(blob, rmx.FORMAT_LIBSVM, 2)
+        ids.upload(s.ids(F))
+        lab.upload(s.targets)
+        model.predict_ids(table, PLUMB_ROWS, ids, scores, batch=PLUMB_BATCH, stream=stream)
+        res["auc"] = rmx.auc(ctx, lab, scores, stream=stream)  # synchronises
+
+    for _ in range(warmup):
+        step()
+    if dist:
+        dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.sync()
+    t_rank = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    t_rank = max_over_ranks(dist, t_rank)
+    model.set_timing(True)
+    step()
+    stages, calls = model.get_timing()
+    model.set_timing(False)
+    B = PLUMB_ROWS
+    per_stage = {n: {"avg_ms_per_pass": round(t, 4)} for n, t in stages.items()}
+    kind, work = stage_work("lr_plumbing", "first_order_sigmoid", PLUMB_BATCH)
+    launches = PLUMB_ROWS // PLUMB_BATCH
+    avg_s = stages.get("first_order_sigmoid", 0.0) / 1e3 / launches
+    roof = {"bound": "hbm", "achieved": round(work / avg_s / 1e9, 2) if avg_s else None, "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": round(work / avg_s / 1e9 / PEAK_HBM_GBS, 6) if avg_s else None,
+            "traffic": None, "kernel": "first_order_sigmoid", "algorithmic_per_launch": work,
+            "note": "100-row launches: latency-bound plumbing (the parse on the host dominates the pass)"}
+    return {"value": world * B * steps / t_rank, "ms_per_step": t_rank * 1e3 / steps, "B": B, "Vw": V,
+            "nrows": PLUMB_ROWS, "roofline": roof, "stages": per_stage, "auc": res.get("auc"),
+            "out": scores.numpy()}
+
+
+def max_over_ranks(dist, t):
+    if not dist:
+        return t
+    import torch
+    x = torch.tensor([t], dtype=torch.float64)
+    dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    return float(x.item())
+
+
+def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
+    """Builds the workload, times K steps after W warm-up steps (max over ranks), then measures the
+    per-stage kernel times (HIP events on the launch stream) for the roofline of the dominant kernel."""
+    if workload == "lr_plumbing":
+        return run_plumbing(args, rmx, ctx, rank, world, dist, steps, warmup)
+    train = workload.endswith("_train")
+    B = B or args.batch or ({"xdeepfm": 16384, "xdeepfm_train": 4096}.get(workload, 65536))
+    sharded = workload == "deepfm_sharded"
+    Vw = args.vocab or (100_000_000 if sharded else V)
+    stream = ctx.stream
+    bf16 = workload.endswith("bf16")
+    model = make_model(rmx, workload, Vw, ctx)
     if bf16:
         model.setPrecision(rmx.DTYPE_BF16)
+    table = None
     if sharded:
         # configs[3]: table hash-sharded over the ranks, RCCL exchange per batch (DESIGN.md §8)
         # RCCL prints its version banner on fd 1 at init; keep stdout for the one JSON line
@@ -286,7 +420,7 @@ def main():
         else:
             model.forward_ids(table, B, ids_v, out_v, stream)
 
-    for i in range(args.warmup):
+    for i in range(warmup):
         step(i)
     ctx.sync()
 
@@ -298,8 +432,8 @@ def main():
     ctx.sync()
     t0 = time.perf_counter()
     rmx._lib.lib.rmx_event_record(ev0, stream)
-    for i in range(args.steps):
-        step(args.warmup + i)
+    for i in range(steps):
+        step(warmup + i)
     rmx._lib.lib.rmx_event_record(ev1, stream)
     ctx.sync()
     wall = time.perf_counter() - t0
@@ -307,17 +441,12 @@ def main():
         dist.barrier()
     ms = ctypes.c_float()
     rmx._lib.lib.rmx_event_elapsed_ms(ev0, ev1, ctypes.byref(ms))
-    t_rank = max(wall, ms.value / 1e3)
-    if dist:
-        import torch
-        t = torch.tensor([t_rank], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_rank = float(t.item())
-    value = world * B * args.steps / t_rank
+    t_rank = max_over_ranks(dist, max(wall, ms.value / 1e3))
+    value = world * B * steps / t_rank
 
     # ---- roofline of the dominant kernel: per-stage HIP events on the launch stream ----
     model.set_timing(True)
-    nt = max(5, min(args.steps, 20))
+    nt = max(5, min(steps, 20))
     for i in range(nt):
         step(i)
     ctx.sync()
@@ -333,7 +462,7 @@ def main():
     per_stage = {}
     for name, tot in stages.items():
         avg_ms = tot / max(calls, 1)
-        kind, work = stage_work(args.workload, name, B)
+        kind, work = stage_work(workload, name, B)
         ent = {"avg_ms": round(avg_ms, 4)}
         if kind == "flop":
             ent["tflops"] = round(work / (avg_ms / 1e3) / 1e12, 2)
@@ -342,8 +471,9 @@ def main():
             ent["gbs"] = round(work / (avg_ms / 1e3) / 1e9, 1)
             ent["frac_hbm_peak"] = round(ent["gbs"] / PEAK_HBM_GBS, 3)
         per_stage[name] = ent
+    stage_sum = sum(stages.values()) / max(calls, 1)
     dom = max(stages.items(), key=lambda kv: kv[1])[0]
-    kind, work = stage_work(args.workload, dom, B)
+    kind, work = stage_work(workload, dom, B)
     avg_s = stages[dom] / max(calls, 1) / 1e3
     if kind == "byte":
         roof = {"bound": "hbm", "achieved": round(work / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
@@ -359,7 +489,7 @@ def main():
     roof["traffic"] = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
-        ent = json.load(open(tpath)).get(args.workload, {}).get(dom if not dom.startswith("cin") else "cin_layer")
+        ent = json.load(open(tpath)).get(workload, {}).get(dom if not dom.startswith("cin") else "cin_layer")
         if ent and ent.get("batch") == B:
             roof["traffic"] = ent["hbm_bytes"]
             roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
@@ -381,56 +511,128 @@ def main():
         t2 = time.perf_counter()
         pa = {"rows": nrows, "predict_ms": round((t1 - t0) * 1e3, 3), "auc_ms": round((t2 - t1) * 1e3, 3),
               "auc": round(a, 6), "labels": "Bernoulli(0.25), independent of the scores (AUC ~ 0.5)"}
+    elif sharded:
+        step(0)  # rows [0, B) of this rank again, for the parity check below
+        ctx.sync()
+    res = {"value": value, "ms_per_step": t_rank * 1e3 / steps, "B": B, "Vw": Vw, "nrows": nrows,
+           "roofline": roof, "stages": per_stage, "stage_sum_ms": round(stage_sum, 4), "predict_auc": pa,
+           "out": out.numpy()[:512], "bf16": bf16, "split": split}
+    if sharded:
+        res["exchange"] = {"dedupe": "off" if args.no_dedupe else "auto", "ids_sent_last_step": table.last_sent(),
+                           "nnz_per_step": B * F}
+    return res
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not train:
-        threads = min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline_sweep(args.workload, args.cpu_seconds, threads)
-        if not sharded and Vw == V and not args.zipf:
+
+def config_of(workload, r, world, zipf):
+    base = workload[:-len("_train")] if workload.endswith("_train") else workload
+    Vw, B = r["Vw"], r["B"]
+    if workload == "lr_plumbing":
+        return {"workload": "lr_plumbing_F39_V1M_libsvm1k_B100", "global_batch": world * PLUMB_BATCH,
+                "rows_per_gpu_set": PLUMB_ROWS, "ids": "uniform", "parallelism": "replicas%d" % world,
+                "step": "parse (2 threads) + ids to HBM + 10 LR forwards of 100 rows + AUC"}
+    return {"workload": "%s%s_F39_V%s_k16_fc400x3%s_B%d" % (
+        workload, "" if r["bf16"] else "_fp32",
+        ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
+        {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(base, ""), B),
+        "global_batch": world * B, "rows_per_gpu_set": r["nrows"],
+        "ids": ("zipf%g" % zipf) if zipf else "uniform",
+        "parallelism": ("hashshard%d_rccl" % world) if workload == "deepfm_sharded" else "replicas%d" % world}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # CPU (gloo) barrier / max only: the GPU work is librmx
+        dist.init_process_group("gloo")
+    import rmx
+    for kv in filter(None, args.set.split(",")):
+        k_, v_ = kv.split("=")
+        rmx.set_tuning(k_, int(v_))
+
+    train = args.workload.endswith("_train")
+    # one rank per GPU; fewer GPUs than ranks (a rehearsal on a 1-GPU box) wraps ranks onto them
+    # (torch.cuda.device_count() does not initialise the GPU on this image)
+    ndev = 1
+    if world > 1:
+        import torch
+        ndev = max(1, torch.cuda.device_count())
+    if args.workload == "deepfm_sharded" and world > ndev:
+        raise SystemExit("deepfm_sharded needs one GPU per rank (RCCL rejects ranks sharing a GPU)")
+    rmx.set_device(local % ndev)
+    ctx = rmx.default_context()
+
+    r = run(args, args.workload, rmx, ctx, rank, world, dist, args.steps, args.warmup)
+    # BASELINE.json's metric names DeepFM AND xDeepFM: the default line measures both (xDeepFM as a
+    # sub-record with its own steps, roofline, parity and CPU baseline; configs[2])
+    companion = None
+    if args.workload == "deepfm" and not args.no_companion:
+        companion = run(args, "xdeepfm", rmx, ctx, rank, world, dist, args.steps, args.warmup, B=16384)
+
+    cpu = cpu2 = None
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not train
+    if want_cpu:
+        cpu = cpu_baseline_sweep(args.workload, args.cpu_seconds)
+        if args.workload == "lr_plumbing":
+            pass
+        elif args.workload == "deepfm_sharded" and not args.zipf:
+            cpu["parity_check"] = parity_check(args.workload, r["out"], 0, vocab=r["Vw"])
+        elif r["Vw"] == V and not args.zipf:
             # out holds the predict loop's probabilities of the whole rank-0 row set
-            cpu["parity_check"] = parity_check(args.workload, out.numpy(), 0)
+            cpu["parity_check"] = parity_check(args.workload, r["out"], 0)
+        if companion:
+            cpu2 = cpu_baseline_sweep("xdeepfm", max(3.0, args.cpu_seconds * 0.5), short=True)
+            cpu2["parity_check"] = parity_check("xdeepfm", companion["out"], 0)
 
     if rank == 0:
         line = {
             "metric": ("CTR-train examples/sec (forward + RecModel.backward gradients; the optimizer lives on "
                        "the parameter server, out of scope)") if train else
                       "CTR-forward examples/sec on Criteo-shaped batch, DeepFM & xDeepFM, 1/2/4/8 GPU",
-            "value": round(value, 1),
+            "value": round(r["value"], 1),
             "unit": "examples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(t_rank * 1e3 / args.steps, 4),
+            "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16 (fp32 accumulate)" if bf16 else "f32",
+            "dtype": "bf16 (fp32 accumulate)" if r.get("bf16") else "f32",
             **({"gemm_arith": "fp32 operands and accumulation; products on v_mfma_f32_16x16x32_bf16 via the exact "
                               "3-way bf16 split (6 products, dropped terms <= 2^-24 |xy|; parity vs the fp64 oracle "
-                              "identical to the f32 MFMA engine)"} if split else {}),
-            "data": "synthetic (splitmix64 Criteo-shaped ids, U(-0.05,0.05) table, Xavier mats)",
-            "config": {"workload": "%s%s_F39_V%s_k16_fc400x3%s_B%d" % (
-                args.workload, "" if bf16 else "_fp32",
-                ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
-                {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(base, ""), B),
-                "global_batch": world * B, "rows_per_gpu_set": nrows,
-                "ids": ("zipf%g" % args.zipf) if args.zipf else "uniform",
-                "parallelism": ("hashshard%d_rccl" % world) if sharded else "replicas%d" % world},
-            **({"exchange": {"dedupe": "off" if args.no_dedupe else "auto", "ids_sent_last_step": table.last_sent(),
-                             "nnz_per_step": B * F}} if sharded else {}),
-            "roofline": roof,
+                              "identical to the f32 MFMA engine)"} if r.get("split") else {}),
+            "data": ("synthetic (splitmix64 Criteo-shaped ids, U(-0.05,0.05) table, Xavier mats)"
+                     + ("; LIBSVM text of the same ids, Bernoulli(0.25) labels" if args.workload == "lr_plumbing"
+                        else "")),
+            "config": config_of(args.workload, r, world, args.zipf),
+            **({"exchange": r["exchange"]} if "exchange" in r else {}),
+            "roofline": r["roofline"],
             "cpu_baseline": cpu,
-            **({"predict_auc": pa} if pa else {}),
-            "stages": per_stage,
+            **({"predict_auc": r["predict_auc"]} if r.get("predict_auc") else {}),
+            **({"auc": r["auc"]} if "auc" in r else {}),
+            "stages": r["stages"],
+            **({"stage_sum_ms": r["stage_sum_ms"]} if "stage_sum_ms" in r else {}),
         }
-        if not train:
+        if companion:
+            line["models"] = {"xdeepfm": {
+                "config": config_of("xdeepfm", companion, world, args.zipf),
+                "value": round(companion["value"], 1), "unit": "examples/s",
+                "ms_per_step": round(companion["ms_per_step"], 4), "steps": args.steps, "warmup": args.warmup,
+                "roofline": companion["roofline"], "stages": companion["stages"],
+                "stage_sum_ms": companion["stage_sum_ms"], "cpu_baseline": cpu2,
+                **({"predict_auc": companion["predict_auc"]} if companion.get("predict_auc") else {})}}
+        if not train and args.workload != "lr_plumbing":
             # BASELINE.json asks for the HBM-roofline fraction too: the whole forward's algorithmic
             # bytes per example (ids + first-order weights + embedding rows + output)
-            es = 2 if bf16 else 4
+            es = 2 if r.get("bf16") else 4
             bpe = F * 4 + F * es + F * K * es + 4
             line["forward_hbm"] = {"algorithmic_bytes_per_example": bpe,
-                                   "gbs": round(value * bpe / 1e9, 1), "peak": PEAK_HBM_GBS,
-                                   "frac": round(value * bpe / 1e9 / PEAK_HBM_GBS, 4),
+                                   "gbs": round(r["value"] * bpe / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                   "frac": round(r["value"] * bpe / 1e9 / PEAK_HBM_GBS, 4),
                                    "note": "compute-bound: the dense tower / CIN, not the gather, sets the rate"}
         print(json.dumps(line), flush=True)
     if dist:
