@@ -135,6 +135,38 @@ def test_split_headline_deepfm_full_batch(ctx):
     assert np.array_equal(out.numpy(), got)
 
 
+def test_split_headline_xdeepfm_full_batch(ctx):
+    """configs[2] at its bench batch (CIN 200,200,200 + fcDims 400^3, B = 16,384, V = 1M), split on:
+    the fp64 oracle on head and tail slices (CINEncoder.scala:36-58, XDeepFM.scala:62-86) and
+    bitwise determinism across launches."""
+    B, V = 16384, 1_000_000
+    m = rmx.XDeepFM(V, F, K, [400, 400, 400], [200, 200, 200])
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids_dev = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_dev)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids_dev, out)
+    ctx.sync()
+    got = out.numpy().copy()
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    om = oc.make_model(oc.XDEEPFM, F, K, fc=(400, 400, 400), cin=(200, 200, 200))
+    for r0, n in ((0, 96), (B // 2 - 17, 64), (B - 96, 96)):
+        ids = oc.gen_ids(SEED_IDS, r0, n, F, V).astype(np.int64)
+        w, e = oc.gather(wt, et, 1, ids)
+        index = np.repeat(np.arange(n, dtype=np.int64), F)
+        ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 1, 16)
+        err = float(np.abs(got[r0:r0 + n] - ref).max())
+        print("xDeepFM B=%d rows [%d, %d): max|p - p_fp64| = %.3g" % (B, r0, r0 + n, err))
+        assert err <= TOL
+    m.forward_ids(table, B, ids_dev, out)
+    ctx.sync()
+    assert np.array_equal(out.numpy(), got)
+
+
 def test_split_host_arrays_path(ctx):
     """L-A (RecModel.forward host arrays, implicit ids) runs the split GEMM too."""
     B, V = 200, 5000
