@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="Zipf exponent of the ids within a field (SURVEY.md §8d secondary; 0 = uniform)")
     ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step (default: auto)")
+    ap.add_argument("--settle-ms", type=float, default=400.0,
+                    help="untimed steps run back to back for this long before the W warm-up steps, so the GPU "
+                         "leaves its idle clock state first (0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--set", default="", help="kernel knobs before building the model, k=v,k=v (rmx_set_tuning)")
@@ -420,6 +423,18 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         else:
             model.forward_ids(table, B, ids_v, out_v, stream)
 
+    # clock settle: an idle MI355X ramps its clocks over the first ~0.1-0.3 s of load, so 5 warm-up
+    # steps (~2 ms) leave the timed steps on a cold clock.  Untimed, before the W
+    # warm-up steps; the K timed steps are unchanged.
+    settle = 0
+    if args.settle_ms > 0:
+        ctx.sync()
+        t_s = time.perf_counter()
+        while (time.perf_counter() - t_s) * 1e3 < args.settle_ms:
+            for _ in range(8):
+                step(settle)
+                settle += 1
+            ctx.sync()
     for i in range(warmup):
         step(i)
     ctx.sync()
@@ -516,6 +531,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         ctx.sync()
     res = {"value": value, "ms_per_step": t_rank * 1e3 / steps, "B": B, "Vw": Vw, "nrows": nrows,
            "roofline": roof, "stages": per_stage, "stage_sum_ms": round(stage_sum, 4), "predict_auc": pa,
+           "settle_steps": settle,
            "out": out.numpy()[:512], "bf16": bf16, "split": split}
     if sharded:
         res["exchange"] = {"dedupe": "off" if args.no_dedupe else "auto", "ids_sent_last_step": table.last_sent(),
@@ -597,6 +613,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            **({"settle": {"ms": args.settle_ms, "untimed_steps": r["settle_steps"]}} if "settle_steps" in r else {}),
             "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",

@@ -29,6 +29,7 @@
 #pragma once
 
 #include <algorithm>
+#include <type_traits>
 
 #include "rmx_models.hpp"
 
@@ -60,14 +61,15 @@ __device__ __forceinline__ void vm_wait(int n) {
 }
 
 // Diagnostic builds only (tools/diag_build.sh; never set in librmx.so): 1 = no A split,
-// 2 = no per-step barrier, 4 = no MFMAs in the split GEMM.  Results are wrong; timings isolate costs.
+// 2 = no per-step barrier, 4 = no MFMAs in the split GEMM, 32 = no epilogue global stores of the
+// activations.  Results are wrong; timings isolate costs.
 #ifndef RMX_GEMM_DIAG
 #define RMX_GEMM_DIAG 0
 #endif
 
 #if RMX_GEMM_DIAG & 8
 // per-phase cycle sums of one wave (block 0, wave 0) of the last split-GEMM launch (tools/diag_phases.py)
-__device__ unsigned long long g_rmx_diag_t[8];
+__device__ unsigned long long g_rmx_diag_t[16];  // waves 0 and NW/2 of block 0
 #define RMX_TMARK(k)                                                             \
   do {                                                                           \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
@@ -78,6 +80,10 @@ __device__ unsigned long long g_rmx_diag_t[8];
 #define RMX_TMARK(k) \
   do {               \
   } while (0)
+#endif
+
+#ifndef RMX_STAG_PF
+#define RMX_STAG_PF 2
 #endif
 
 enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
@@ -118,6 +124,9 @@ struct GemmArgs {
   int ldmask;
 };
 
+template <int V>
+using IC = std::integral_constant<int, V>;
+
 constexpr int kFmMaxF = 40;  // fused FM: fields per sample it handles (F = 39 at the headline config)
 
 // FM sums of one A fragment pair (fields 2c, 2c + 1; j = 4g .. 4g + 3): s += e, q += e * e in field
@@ -139,11 +148,13 @@ __device__ __forceinline__ void fm_accum(const f32x4& a0, const f32x4& a1, f32x4
 // Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
 // tiles); the block spans BM = WM*MT*16 rows and BN = WN*NTW*16 columns.  BKC 16-wide K chunks per
 // LDS stage.  OCC = minimum waves per SIMD the register allocation must allow (launch bounds).
-template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_, int RING_ = 0>
+template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_, int RING_ = 0, int STAG_ = 0>
 struct Tile {
   // RING > 0: LDS-DMA (global_load_lds_dwordx4) ring of RING one-chunk stages, RING - 1 chunks in
   // flight, counted vmcnt + one raw barrier per chunk (needs BKC == 1); 0: register-staged double buffer
+  // STAG (kPrecS3, RING == 2): the two waves of each SIMD run half a K step apart (staggered loop below)
   static constexpr int MT = MT_, NTW = NTW_, WM = WM_, WN = WN_, BKC = BKC_, OCC = OCC_, RING = RING_;
+  static constexpr int STAG = STAG_;
   static constexpr int NBUF = RING > 0 ? RING : 2;  // stage buffers in LDS
   static constexpr int NW = WM * WN, NTHR = NW * 64, NT = NTW * WN;
   static constexpr int BM = WM * MT * 16, BN = NT * 16;
@@ -176,7 +187,11 @@ struct StageGeom {
   // bf16 planes [3][BN] (each a 64-B row of 32 values)
   static constexpr int AROWS = AMODE != kCinOuter ? T::BM * (PREC == kPrecS3 ? 2 : T::BKC) : 0;
   static constexpr int ROWS = AROWS + T::BN * (PREC == kPrecS3 ? 3 : T::BKC);  // 64-B rows per stage
-  static constexpr int FLOATS = ROWS * 16;
+  // kPrecS3 ring stages are padded to whole DMA instructions per wave (16 rows each), so every wave
+  // issues the same instructions every step with no per-wave branch (the padding rows take zeros)
+  static constexpr int NINS = ROWS / 16;
+  static constexpr int PADROWS = (PREC == kPrecS3 && T::RING > 0) ? 16 * (((NINS + T::NW - 1) / T::NW) * T::NW - NINS) : 0;
+  static constexpr int FLOATS = (ROWS + PADROWS) * 16;
 };
 
 // Epilogue slab geometry: each wave transposes NTH of its column tiles at a time through a
@@ -224,6 +239,14 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   constexpr int ITEMS = ROWS * 4;  // float4 items per stage
   constexpr int PER = (ITEMS + NTHR - 1) / NTHR;
 
+  // The DMA fill sources for out-of-range entries.  Under -fPIC a global's address comes from the GOT;
+  // left alone, the compiler rematerialises it inside the MFMA stream as s_getpc + s_load +
+  // s_waitcnt lgkmcnt(0) per DMA, which also drains the prefetched LDS fragment reads.  The empty
+  // asm makes each address an opaque value computed once (kept in SGPRs).
+  const float* zero16 = g_rmx_zero16;
+  const int* neg1 = g_rmx_neg1;
+  asm volatile("" : "+s"(zero16));
+  asm volatile("" : "+s"(neg1));
   constexpr int RING = T::RING;
   static_assert(RING == 0 || BKC == 1, "the LDS-DMA ring stages one K chunk at a time");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -309,7 +332,12 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   f32x4 acc[MT][NTW];
 #if RMX_GEMM_DIAG & 8
   // DIAG & 16: only CIN launches record (xDeepFM's last split-GEMM launch is a tower layer)
-  const bool dmark = blockIdx.x == 0 && blockIdx.y == 0 && wid == 0 && (!(RMX_GEMM_DIAG & 16) || AMODE == kCinOuter);
+  // DIAG & 64: dense-A tower launches record (the last one is the output layer); & 128: gathered
+  // layer 1; else the CIN layers (K > 100 steps)
+  constexpr bool kDiagSel = (RMX_GEMM_DIAG & 64)    ? AMODE == kDenseA
+                            : (RMX_GEMM_DIAG & 128) ? AMODE == kGatherK16
+                                                    : (!(RMX_GEMM_DIAG & 16) || AMODE == kCinOuter);
+  const bool dmark = blockIdx.x == 0 && blockIdx.y == 0 && (wid == 0 || wid == T::NW / 2) && kDiagSel;
   unsigned long long dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dlast = __builtin_amdgcn_s_memtime();
 #endif
 #pragma unroll
@@ -388,7 +416,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // 2-byte LDS DMA writes lane L at base + 4 L, tools/probe/glds_sizes.hip), widened exactly
   auto wget = [&](int c, int part, int r) -> float {
     const int e = ((c & 1) * 2 + part) * BM + r;
-    return p.fm_w_bf16 ? __uint_as_float(__float_as_uint(wring[e]) << 16) : wring[e];
+    return (!S3 && p.fm_w_bf16) ? __uint_as_float(__float_as_uint(wring[e]) << 16) : wring[e];
   };
   // the weights of fields 2c, 2c + 1 of this lane's rows, in field order
   auto wsum = [&](int c) {
@@ -451,7 +479,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   constexpr int kQID = IDRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;  // id-ring DMAs per wave
   constexpr int kQW = WRING ? (2 * BM / 64 + T::NW - 1) / T::NW : 0;    // w-ring DMAs per wave
   constexpr int kIPW = kQID + kQW + (ROWS / 16 + T::NW - 1) / T::NW;
-  auto compute_step_s3 = [&](const float* cur, int c, auto&& dma) {
+  auto compute_step_s3 = [&](const float* cur, int c, auto&& dma, auto&& dpre) {
     f32x4 a0[MT], a1[MT];
     if constexpr (A_LDS) {
 #pragma unroll
@@ -460,12 +488,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         a0[i] = *reinterpret_cast<const f32x4*>(cur + o);
         a1[i] = *reinterpret_cast<const f32x4*>(cur + BM * 16 + o);
       }
+      // unconditional (no branch inside the MFMA loop); read only when the launch asked for them
       if constexpr (FMS)
-        if (fm_sums)
 #pragma unroll
-          for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
-      if constexpr (WRING)
-        if (wfuse) wsum(c);
+        for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
+      if constexpr (WRING) wsum(c);
     } else {
       if (c == 0) {
         cin_x0(0, x0q[0]);
@@ -500,6 +527,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     // MFMA group waits only for its own reads (counted lgkmcnt), not for a drained LDS queue
     constexpr int PF = 2;
     f32x4 bq[PF + 1][3];
+    if (0 < kIPW) dpre(0);
 #pragma unroll
     for (int t = 0; t < PF && t < NTW; ++t) ldb(t, bq[t]);
 #pragma unroll
@@ -509,6 +537,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       // cycles (vector-memory queue), which here overlaps the partner wave's MFMAs instead of
       // idling the SIMD in a separate post-barrier phase
       if (t < kIPW) dma(t);
+      // the LDS-held operand (a ring id) of the next DMA is read one MFMA group ahead of its use
+      if (t + 1 < kIPW) dpre(t + 1);
       if constexpr (!A_LDS)
         if (t == 0) {
           cin_x0(2 * c + 2, x0q[0]);
@@ -544,9 +574,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // one K chunk c of the stage image at `cur` (chunk slot cc inside the stage)
   // dma(q): issue this wave's q-th DMA instruction of the next stage (ring kernels), spread over the
   // MFMA groups so its issue stall overlaps MFMAs (a no-op for the register-staged pipeline)
-  auto compute_chunk = [&](const float* cur, int cc, int c, auto&& dma) {
+  auto compute_chunk = [&](const float* cur, int cc, int c, auto&& dma, auto&& dpre) {
     if constexpr (S3) {
-      compute_step_s3(cur, c, dma);
+      compute_step_s3(cur, c, dma, dpre);
     } else {
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
       f32x4 a[MT];
@@ -610,7 +640,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       for (int cc = 0; cc < BKC; ++cc) {
         const int c = st * BKC + cc;
         if (BKC > 1 && c >= nchunks) break;
-        compute_chunk(cur, cc, c, [](int) {});
+        compute_chunk(cur, cc, c, [](int) {}, [](int) {});
       }
       if (more) sstore(nxt);
       __syncthreads();
@@ -622,7 +652,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     constexpr int NW = T::NW;
     constexpr int NINS = ROWS / 16;
     constexpr int IPW = (NINS + NW - 1) / NW;
-    const int my_n = wid < NINS ? (NINS - 1 - wid) / NW + 1 : 0;  // DMAs this wave issues per chunk
+    // DMAs this wave issues per chunk (kPrecS3: every wave IPW, padding included)
+    const int my_n = S3 ? IPW : (wid < NINS ? (NINS - 1 - wid) / NW + 1 : 0);
     // A wave's instructions are the same every step (ins is wave-uniform), so the A / B region
     // and the chunk / plane of an instruction are scalar; dense A and B sources are a 32-bit
     // per-lane element offset plus a per-step stride (launch_cfg checks M * lda < 2^32).
@@ -641,13 +672,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
               const uint32_t o = (uint32_t)m * (uint32_t)p.lda + (uint32_t)kk;
               src = (m < M && kk < p.K) ? (BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + o)
                                              : (const void*)(p.A + o))
-                                        : (const void*)g_rmx_zero16;
+                                        : (const void*)zero16;
             } else if constexpr (IDRING) {
               const int id = idring[((c & 1) * 2 + cc) * BM + r];
-              src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)g_rmx_zero16;
+              src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)zero16;
             } else {
               src = src_of(row, g, c);
-              if (!src) src = g_rmx_zero16;
+              if (!src) src = zero16;
             }
           } else {
             const int cc = (ins * 16 - AROWS) / BN;
@@ -665,39 +696,92 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         }
       }
     };
+    // kPrecS3: the same DMA instruction q of source step cs into ring slot `slot`, with no branch:
+    // whether q is an A or a B instruction is known at compile time (A rows are a whole number of
+    // instructions per wave), the padding instruction of a ragged last q reads zeros into the
+    // stage's padding rows, and the caller clamps cs to the last step instead of skipping it.
+    // (Branches here split the MFMA stream into basic blocks and the compiler then drains every
+    // prefetched LDS fragment read with lgkmcnt(0) at each join.)
+    constexpr int AINS_ = AROWS / 16;
+    // ring ids of DMA instruction q: A rows of source step cs (IDRING) / first-order weights of step c
+    auto a_id = [&](int cs, int q) -> int {
+      const int ins = wid + q * NW;
+      const int row = ins * 16 + (lane >> 2), cc = ins * 16 / BM;
+      return idring[((cs & 1) * 2 + cc) * BM + row - cc * BM];
+    };
+    auto w_id = [&](int c, int q) -> int {
+      const int ins = wid + q * NW;
+      const int v = ins * 64 + lane, part = v / BM, r = v - part * BM;
+      if constexpr (IDRING) {
+        return idring[((c & 1) * 2 + part) * BM + r];
+      } else {
+        const int f = 2 * c + part;
+        return (f < F && m0 + r < M) ? sids[r * F + f] : -1;
+      }
+    };
+    // get_id(): the ring id of an IDRING A instruction (read here, or one MFMA group earlier)
+    auto issue_s3 = [&](int cs, int slot, int q, auto&& get_id) {
+      if constexpr (S3) {
+        float* buf = smem + slot * STAGE;
+        const int ins = wid + q * NW;
+        const int row = ins * 16 + (lane >> 2), ps = lane & 3;
+        const void* src;
+        if ((q + 1) * NW <= AINS_ || (q * NW < AINS_ && ins < AINS_)) {
+          const int cc = ins * 16 / BM;
+          const int r = row - cc * BM, g = swz_slot(r, ps);
+          if constexpr (AMODE == kDenseA) {
+            const int m = m0 + r, kk = cs * KC + cc * KCA + g * KSA;
+            const uint32_t o = (uint32_t)m * (uint32_t)p.lda + (uint32_t)kk;
+            src = (m < M && kk < p.K) ? (const void*)(p.A + o) : (const void*)zero16;
+          } else if constexpr (IDRING) {
+            const int id = get_id();
+            src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)zero16;
+          } else {
+            src = src_of(row, g, cs);
+            if (!src) src = zero16;
+          }
+        } else {
+          const int cc = (ins * 16 - AROWS) / BN;
+          const int n = row - AROWS - cc * BN, g = swz_slot(n, ps);
+          src = reinterpret_cast<const bf16_t*>(p.Wp) + ((uint32_t)((cs * 3 + cc) * p.Npad + n0 + n) * 32u + (uint32_t)(g * 8));
+          if ((q + 1) * NW > NINS) src = ins < NINS ? src : (const void*)zero16;  // padding instruction
+        }
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
+      }
+    };
     auto issue = [&](int c) {
 #pragma unroll
-      for (int q = 0; q < IPW; ++q) issue_one(c, q);
+      for (int q = 0; q < IPW; ++q) {
+        if constexpr (S3)
+          issue_s3(c, c % RING, q, [&] { return a_id(c, q); });
+        else
+          issue_one(c, q);
+      }
     };
     // IDRING: the ids of fields 2c, 2c + 1 for the block's rows -> slot c & 1 (one dword per lane)
     auto issue_id = [&](int c, int q) {
       const int ins = wid + q * NW;
-      if (ins < 2 * BM / 64) {
+      if (kQID * NW == 2 * BM / 64 || ins < 2 * BM / 64) {
         const int v = ins * 64 + lane, part = v / BM, r = v - part * BM, m = m0 + r, f = 2 * c + part;
-        const void* src = (m < M && f < F) ? (const void*)(p.ga.ids + (int64_t)m * F + f) : (const void*)g_rmx_neg1;
+        const void* src = (m < M && f < F) ? (const void*)(p.ga.ids + (int64_t)m * F + f) : (const void*)neg1;
         __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(idring + (c & 1) * 2 * BM + ins * 64),
                                          4, 0, 0);
       }
     };
     // the first-order weights of stage c (ids of slot c & 1 landed, or the id tile) -> w slot c & 1,
     // one dword per lane (a 2-byte DMA of a bf16 weight fills the low half, zero-extended)
-    auto issue_w = [&](int c, int q) {
+    auto issue_w = [&](int c, int q, auto&& get_id) {
       const int ins = wid + q * NW;
-      if (ins < 2 * BM / 64) {
-        const int v = ins * 64 + lane, part = v / BM, r = v - part * BM;
-        int id;
-        if constexpr (IDRING) {
-          id = idring[((c & 1) * 2 + part) * BM + r];
-        } else {
-          const int f = 2 * c + part;
-          id = (f < F && m0 + r < M) ? sids[r * F + f] : -1;
-        }
+      if (kQW * NW == 2 * BM / 64 || ins < 2 * BM / 64) {
+        const int id = get_id();
         const int e = (c & 1) * 2 * BM + ins * 64;
-        if (p.fm_w_bf16) {
-          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const bf16_t*>(p.fm_w) + id) : (const void*)g_rmx_zero16;
+        if (!S3 && p.fm_w_bf16) {  // (kPrecS3 models have fp32 tables: launch_tower_s3 checks)
+          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const bf16_t*>(p.fm_w) + id) : (const void*)zero16;
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 2, 0, 0);
         } else {
-          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + id) : (const void*)g_rmx_zero16;
+          // (kPrecS3 issues this unconditionally: zeros when the launch fuses no first order)
+          const bool ok = id >= 0 && (!S3 || wfuse);
+          const void* src = ok ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + id) : (const void*)zero16;
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 4, 0, 0);
         }
       }
@@ -714,8 +798,153 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     if constexpr (WRING)
       if (wfuse)
 #pragma unroll
-        for (int q = 0; q < kQW; ++q) issue_w(0, q);
+        for (int q = 0; q < kQW; ++q) issue_w(0, q, [&] { return w_id(0, q); });
     for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
+    int pend_id = -1;  // kPrecS3: the ring id of the next DMA, read one MFMA group ahead
+    if constexpr (S3 && T::STAG) {
+      // Staggered split-GEMM loop (two barriers per K step).  Waves w and w + NW/2 share a SIMD's
+      // matrix pipe.  In the plain loop both reach the step barrier together and then both read
+      // and split their A fragments (VALU + LDS latency) while the pipe idles.  Here the second
+      // half (Y) runs its column tiles [NT1, NTW) one step late:
+      //   phase 1 (bar0(c) .. bar1(c)):  X: prep(c), tiles [0, NT1) of step c
+      //                                  Y: tiles [NT1, NTW) of step c - 1 (B of step c - 1)
+      //   phase 2 (bar1(c) .. bar0(c+1)): X: tiles [NT1, NTW) of step c
+      //                                  Y: prep(c), tiles [0, NT1) of step c
+      // so each wave's prep overlaps its partner's MFMAs, and each phase carries one step's worth
+      // of MFMAs per SIMD.  Y's split A of step c - 1 is still in its registers in phase 1 (no extra
+      // registers: the accumulator of a tile is the same across steps).  The A rows, ids and
+      // first-order weights of step c + 1 (their LDS slots were last read before bar0(c)) are
+      // issued in phase 1; the B planes of step c + 1 go into the buffer Y reads in phase 1, so
+      // they are issued after bar1(c) and have phase 2 to land (weights: L2 hits).
+      static_assert(RING == 2 && BKC == 1, "the staggered loop runs on the 2-deep ring");
+      constexpr int NT1 = (NTW + 1) / 2;
+      constexpr int AINS = AROWS / 16;
+      static_assert(AINS % NW == 0, "every wave issues the same number of A-region DMAs");
+      constexpr int QA = AINS / NW;              // this wave's A-region DMAs: q in [0, QA)
+      constexpr int NP1 = kQID + kQW + QA;       // phase-1 DMAs per wave
+      constexpr int NP2 = IPW - QA;              // phase-2 (B-plane) DMAs per wave
+      const bool late = wid >= NW / 2;
+      bf16x8 ah[MT], am[MT], al[MT];
+      auto dma1 = [&](int c, int q) {
+        if (q < kQID) {
+          if constexpr (IDRING) issue_id(c + 2, q);
+        } else if (q < kQID + kQW) {
+          if constexpr (WRING) issue_w(c + 1, q - kQID, [&] { return w_id(c + 1, q - kQID); });
+        } else {
+          const int cs = c + 1 < nchunks ? c + 1 : nchunks - 1;
+          issue_s3(cs, (c + 1) & 1, q - kQID - kQW, [&] { return a_id(cs, q - kQID - kQW); });
+        }
+      };
+      auto dma2 = [&](int c, int q) {
+        const int cs = c + 1 < nchunks ? c + 1 : nchunks - 1;
+        issue_s3(cs, (c + 1) & 1, QA + q, [&] { return a_id(cs, QA + q); });
+      };
+      // A fragments of step c (LDS, or the CIN outer product), FM sums / first-order weights, split
+      auto prep = [&](const float* cur, int c) {
+        f32x4 a0[MT], a1[MT];
+        if constexpr (A_LDS) {
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const int o = arow[i] * 16 + swz_slot(arow[i], g) * 4;
+            a0[i] = *reinterpret_cast<const f32x4*>(cur + o);
+            a1[i] = *reinterpret_cast<const f32x4*>(cur + BM * 16 + o);
+          }
+          if constexpr (FMS)
+#pragma unroll
+            for (int i = 0; i < MT; ++i) fm_accum(a0[i], a1[i], fm_s[i], fm_q[i]);
+          if constexpr (WRING) wsum(c);
+        } else {
+          if (c == 0) {
+            cin_x0(0, x0q[0]);
+            cin_x0(1, x0q[1]);
+          }
+          cin_a_x(0, 2 * c, x0q[0], a0);
+          cin_a_x(1, 2 * c + 1, x0q[1], a1);
+          cin_x0(2 * c + 2, x0q[0]);
+          cin_x0(2 * c + 3, x0q[1]);
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
+      };
+      // the six split MFMAs of column tiles [t0, t1) (compile-time after inlining) from the B
+      // planes of stage buffer `buf`; dma(q) for q < ndma rides one per tile
+      auto tiles = [&](const float* buf, auto T0, auto T1, auto ND, auto&& dma) {
+        constexpr int t0 = decltype(T0)::value, t1 = decltype(T1)::value, ndma = decltype(ND)::value;
+        const float* Bt = buf + AROWS * 16;
+        auto ldb = [&](int t, f32x4* b) {
+          const int row = (bt0 + t) * 16 + r16;
+          const int o = row * 16 + swz_slot(row, g) * 4;
+          b[0] = *reinterpret_cast<const f32x4*>(Bt + o);
+          b[1] = *reinterpret_cast<const f32x4*>(Bt + BN * 16 + o);
+          b[2] = *reinterpret_cast<const f32x4*>(Bt + 2 * BN * 16 + o);
+        };
+        constexpr int PF = RMX_STAG_PF;
+        f32x4 bq[PF + 1][3];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+          if (t >= t0 && t < t0 + PF && t < t1) ldb(t, bq[(t - t0) % (PF + 1)]);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          if (t < t0 || t >= t1) continue;
+          if (t + PF < t1) ldb(t + PF, bq[(t - t0 + PF) % (PF + 1)]);
+          if (t - t0 < ndma) dma(t - t0);
+          __builtin_amdgcn_sched_barrier(0);
+          const f32x4* b = bq[(t - t0) % (PF + 1)];
+          const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
+          const bf16x8 bm = __builtin_bit_cast(bf16x8, b[1]);
+          const bf16x8 bl = __builtin_bit_cast(bf16x8, b[2]);
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            f32x4 d = acc[i][t];
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bm, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[i], bh, d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bm, d, 0, 0, 0);
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, d, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NTW; ++q)
+          if (q >= t1 - t0 && q < ndma) dma(q);
+      };
+      // the two halves run separate copies of the loop (LATE is a compile-time flag), so the
+      // register allocator sees one straight schedule per copy
+      auto run = [&](auto LATE) {
+        constexpr bool kLate = decltype(LATE)::value != 0;
+        for (int c = 0; c < nchunks; ++c) {
+          // bar0(c): this wave's DMAs (A / w / ids of step c by phase 1 of step c - 1, B of step c
+          // by phase 2) have landed; after the barrier, every wave's have
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          const float* cur = smem + (c & 1) * STAGE;
+          if constexpr (!kLate) {
+            prep(cur, c);
+            tiles(cur, IC<0>{}, IC<NT1>{}, IC<NP1>{}, [&](int q) { dma1(c, q); });
+            __builtin_amdgcn_s_barrier();  // bar1(c): Y has read the B planes of step c - 1
+            tiles(cur, IC<NT1>{}, IC<NTW>{}, IC<NP2>{}, [&](int q) { dma2(c, q); });
+          } else {
+            if (c > 0) {
+              tiles(smem + ((c - 1) & 1) * STAGE, IC<NT1>{}, IC<NTW>{}, IC<NP1>{}, [&](int q) { dma1(c, q); });
+            } else {
+#pragma unroll
+              for (int q = 0; q < NP1; ++q) dma1(c, q);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its B reads of step c - 1 are done
+            __builtin_amdgcn_s_barrier();                        // bar1(c)
+            prep(cur, c);
+            tiles(cur, IC<0>{}, IC<NT1>{}, IC<NP2>{}, [&](int q) { dma2(c, q); });
+          }
+        }
+        if constexpr (kLate)
+          if (nchunks > 0) tiles(smem + ((nchunks - 1) & 1) * STAGE, IC<NT1>{}, IC<NTW>{}, IC<0>{}, [&](int) {});
+      };
+      if (late)
+        run(IC<1>{});
+      else
+        run(IC<0>{});
+    } else
     for (int c = 0; c < nchunks; ++c) {
       const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
       RMX_TMARK(6);  // 6: MFMA issue tail of the previous step (+ prologue)
@@ -729,23 +958,43 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       compute_chunk(smem + (c % RING) * STAGE, 0, c, [&](int q) {
         if (q < kQID) {
           // ids of step c + 2 into the slot of step c (its last reader, the issue of stage c,
-          // ran before this step's barrier)
-          if constexpr (IDRING)
-            if (c + 2 < nchunks) issue_id(c + 2, q);
+          // ran before this step's barrier); past the last step every id is -1 (fields >= F)
+          if constexpr (IDRING) {
+            if constexpr (S3)
+              issue_id(c + 2, q);
+            else if (c + 2 < nchunks)
+              issue_id(c + 2, q);
+          }
         } else if (q < kQID + kQW) {
           // weights of stage c + 1 into the w slot of step c - 1 (read before this step's barrier)
-          if constexpr (WRING)
-            if (wfuse && cn < nchunks) issue_w(cn, q - kQID);
+          if constexpr (WRING) {
+            if constexpr (S3) {
+              issue_w(cn, q - kQID, [&] { return pend_id; });
+            } else if (wfuse && cn < nchunks) {
+              issue_w(cn, q - kQID, [&] { return w_id(cn, q - kQID); });
+            }
+          }
+        } else if constexpr (S3) {
+          // past the last step: re-read the last step's sources into the free slot (never read)
+          issue_s3(cn < nchunks ? cn : nchunks - 1, cn % RING, q - kQID - kQW, [&] { return pend_id; });
         } else if (cn < nchunks) {
           issue_one(cn, q - kQID - kQW);
+        }
+      }, [&](int q) {
+        if constexpr (S3 && WRING) {
+          if (q >= kQID && q < kQID + kQW) pend_id = w_id(cn, q - kQID);
+        }
+        if constexpr (S3 && IDRING) {
+          constexpr int QA_ = AINS_ / NW;
+          if (q >= kQID + kQW && q < kQID + kQW + QA_) pend_id = a_id(cn < nchunks ? cn : nchunks - 1, q - kQID - kQW);
         }
       });
     }
     RMX_TMARK(6);
 #if RMX_GEMM_DIAG & 8
-    if (dmark && lane == 0 && nchunks > 100) {  // (DIAG & 16: CIN layers 2+, K = F * 208)
-      for (int k = 0; k < 7; ++k) g_rmx_diag_t[k] = dsum[k];
-      g_rmx_diag_t[7] = nchunks;
+    if (dmark && lane == 0 && (nchunks > 100 || (RMX_GEMM_DIAG & (64 | 128)))) {  // (DIAG & 16: CIN layers 2+)
+      for (int k = 0; k < 7; ++k) g_rmx_diag_t[(wid ? 8 : 0) + k] = dsum[k];
+      g_rmx_diag_t[(wid ? 8 : 0) + 7] = nchunks;
     }
 #endif
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -778,7 +1027,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       for (int q = lane; q < RW * nf4; q += 64) {
         const int rr = q / nf4, c4 = q - rr * nf4;
         const int m = m0 + wm * RW + rr;
-        if (m < M) {
+        if (m < M && !(RMX_GEMM_DIAG & 32)) {
           f32x4 v = *reinterpret_cast<const f32x4*>(wbuf + rr * LD + c4 * 4);
           const int64_t o = (int64_t)m * ldd + n0 + (bt0 + j0) * 16 + c4 * 4;
           if (p.mask) {

@@ -153,11 +153,22 @@ static bool s3_mt2(int M, int Npad, int amode, bool ids) {
 }
 
 int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
+  if (p.fm_w && p.fm_w_bf16) {
+    set_error("split GEMM: fp32 layers take an fp32 table");
+    return RMX_E_INVALID;
+  }
   const int var = tuning_get("s3_tower", 1);
   p.prio = tuning_get("gemm_prio", 0);
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
-  if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr))
+  if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr)) {
+    // knob "s3_stagger": 1 (default) staggered loop on every tower layer, 2 also on the CIN, 0 off
+    // (DeepFM 400^3 at B = 65,536: layers 0.1753 / 0.1110 / 0.0961 ms -> 0.1746 / 0.1082 / 0.0928;
+    // the CIN runs slower staggered: 3.06 -> 3.16 ms per layer, its B planes then get half a step
+    // of DMA lead)
+    if (tuning_get("s3_stagger", 1) != 0)
+      return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2, 1>, kPrecS3>(s, p, amode, epi);
     return launch_epi<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
+  }
   return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
 }
 
@@ -170,7 +181,11 @@ int launch_cin_s3(hipStream_t s, GemmArgs& p) {
   const int var = tuning_get("s3_cin", 2);
   p.prio = tuning_get("gemm_prio", 0);
   if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
-  if (var == 2) return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+  if (var == 2) {
+    if (tuning_get("s3_stagger", 1) == 2)
+      return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2, 1>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+    return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+  }
   if (var == 3) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
 }
@@ -179,8 +194,8 @@ int launch_cin_s3(hipStream_t s, GemmArgs& p) {
 
 #if RMX_GEMM_DIAG & 8
 // diagnostic builds only: the per-phase cycle sums of the last split-GEMM launch
-extern "C" int rmx_diag_phases(unsigned long long* out8) {
-  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 8) == hipSuccess
+extern "C" int rmx_diag_phases(unsigned long long* out16) {
+  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 16) == hipSuccess
              ? 0
              : -5;
 }

@@ -17,8 +17,12 @@ NAMES = ["dma_wait", "barrier", "dma_issue", "a_frag", "split", "mfma_section", 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="xdeepfm")
 ap.add_argument("--batch", type=int, default=0)
+ap.add_argument("--set", default="", help="knobs k=v,k=v")
 a = ap.parse_args()
 F, K, V = 39, 16, 1_000_000
+for kv in filter(None, a.set.split(",")):
+    k_, v_ = kv.split("=")
+    rmx.set_tuning(k_, int(v_))
 ctx = rmx.default_context()
 if a.workload == "xdeepfm":
     m, B = rmx.XDeepFM(V, F, K, [400, 400, 400], [200, 200, 200]), a.batch or 16384
@@ -34,11 +38,12 @@ out = rmx.DeviceArray(ctx, B, np.float32)
 for _ in range(3):
     m.forward_ids(t, B, ids, out)
 ctx.sync()
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 assert rmx._lib.lib.rmx_diag_phases(buf) == 0
-v = list(buf)
-steps = v[7]
-tot = sum(v[:7])
-print("last split-GEMM launch (%s): %d K steps, block 0 wave 0" % (a.workload, steps))
-for n, x in zip(NAMES, v[:7]):
-    print("  %-20s %12d cycles  %6.0f /step  %5.1f %%" % (n, x, x / max(steps, 1), 100.0 * x / max(tot, 1)))
+for w in (0, 1):
+    v = list(buf)[8 * w:8 * w + 8]
+    steps = v[7]
+    tot = sum(v[:7])
+    print("last recorded split-GEMM launch (%s): %d K steps, block 0 wave %s" % (a.workload, steps, "0" if w == 0 else "NW/2"))
+    for n, x in zip(NAMES, v[:7]):
+        print("  %-20s %12d cycles  %6.0f /step  %5.1f %%" % (n, x, x / max(steps, 1), 100.0 * x / max(tot, 1)))

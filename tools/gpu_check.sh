@@ -35,25 +35,29 @@ for s in $STEPS; do
     benchb) run bench_dcn_bf16 400 python bench.py --workload dcn_bf16 --no-cpu-baseline &&
             run bench_pnn_bf16 400 python bench.py --workload pnn_bf16 --no-cpu-baseline ;;
     prof) run prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o deepfm -- \
-            python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+            python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --settle-ms 0 ;;
     profx) run profx 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx" -o xdeepfm -- \
-            python3 bench.py --workload xdeepfm --steps 5 --warmup 2 --no-cpu-baseline ;;
+            python3 bench.py --workload xdeepfm --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 ;;
     sq) run pmc_sq 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_sq" -o sq -- \
-            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 &&
         run pmc_grbm 400 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmc_grbm" -o grbm -- \
-            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 ;;
     pmc) run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o fetch -- \
-            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 &&
          run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
-            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+            python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 ;;
     pmc:*) wl=${s#pmc:}
          run pmc_${wl}_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$wl/fetch" -o fetch -- \
-            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline &&
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 &&
          run pmc_${wl}_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_$wl/write" -o write -- \
-            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline ;;
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 ;;
     prof:*) wl=${s#prof:}
          run prof_$wl 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o $wl -- \
-            python3 bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline ;;
+            python3 bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline --settle-ms 0 ;;
+    settle) for ms in 0 100 400 1000; do
+              run settle_$ms 200 python bench.py --steps 20 --warmup 5 --no-companion --no-cpu-baseline --settle-ms $ms
+            done ;;
+    list) run list 120 rocprofv3 -L ;;
     bench:*) wl=${s#bench:}
          run bench_$wl 400 python bench.py --workload $wl ;;
   esac
