@@ -195,7 +195,16 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
     p.fm_y = fm->y;
   }
   const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
-  if (L.W16) return launch_tower_bf16(s, p, nt, amode, epi);
+  if (L.W16) {
+    const bool sliced = epi == Epi::kOutput && bf16_tower_sliced(L.Npad, epi, L.K, M, amode);
+    if (sliced && !p.oa.part) {
+      set_error("gemm: a sliced output layer needs the partial-logit buffer");
+      return RMX_E_INVALID;
+    }
+    int st = launch_tower_bf16(s, p, nt, amode, epi);
+    if (st == RMX_OK && sliced) st = launch_out_finish(s, M, L.Npad / kS3BN, *oa);
+    return st;
+  }
   if (use_s3(L) && (epi != Epi::kOutput || L.Npad == kS3BN || oa->part)) {
     // fp32 layer on the bf16 matrix cores through the exact 3-way split (k_gemm_s3.hip)
     p.Wp = reinterpret_cast<const float*>(L.W3);

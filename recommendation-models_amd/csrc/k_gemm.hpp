@@ -85,6 +85,9 @@ __device__ unsigned long long g_rmx_diag_t[16];  // waves 0 and NW/2 of block 0
 #ifndef RMX_STAG_PF
 #define RMX_STAG_PF 2
 #endif
+#ifndef RMX_BF_PF
+#define RMX_BF_PF 3  // bf16 fast tiles: B fragments read this many column tiles ahead
+#endif
 
 enum AMode : int { kDenseA = 0, kGatherK16 = 1, kGatherAny = 2, kCinOuter = 3 };
 enum EpiMode : int { kEpiRelu = 0, kEpiOutput = 1, kEpiCin = 2 };
@@ -148,13 +151,16 @@ __device__ __forceinline__ void fm_accum(const f32x4& a0, const f32x4& a1, f32x4
 // Block tiling: WM x WN waves; a wave owns MT*16 rows x NTW*16 columns (MT*NTW accumulator
 // tiles); the block spans BM = WM*MT*16 rows and BN = WN*NTW*16 columns.  BKC 16-wide K chunks per
 // LDS stage.  OCC = minimum waves per SIMD the register allocation must allow (launch bounds).
-template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_, int RING_ = 0, int STAG_ = 0>
+template <int MT_, int NTW_, int WM_, int WN_, int BKC_, int OCC_, int RING_ = 0, int STAG_ = 0, int FAST_ = 0>
 struct Tile {
   // RING > 0: LDS-DMA (global_load_lds_dwordx4) ring of RING one-chunk stages, RING - 1 chunks in
   // flight, counted vmcnt + one raw barrier per chunk (needs BKC == 1); 0: register-staged double buffer
   // STAG (kPrecS3, RING == 2): the two waves of each SIMD run half a K step apart (staggered loop below)
   static constexpr int MT = MT_, NTW = NTW_, WM = WM_, WN = WN_, BKC = BKC_, OCC = OCC_, RING = RING_;
   static constexpr int STAG = STAG_;
+  // FAST (kPrecBF16 ring tiles): the branch-free DMA issue and MFMA step of the split GEMM, applied
+  // to bf16 operands (kPrecS3 tiles always run it)
+  static constexpr int FAST = FAST_;
   static constexpr int NBUF = RING > 0 ? RING : 2;  // stage buffers in LDS
   static constexpr int NW = WM * WN, NTHR = NW * 64, NT = NTW * WN;
   static constexpr int BM = WM * MT * 16, BN = NT * 16;
@@ -179,7 +185,10 @@ constexpr bool kIdRing = AMODE == kGatherK16 && PREC == kPrecS3 && T::RING == 2 
 // 2-deep ring kernels of k = 16 gathers in 32-wide K steps (two fields per step): the first-order
 // weights of each step's (row, field) pairs can ride the ring ([2 slots][2 fields][BM] elements)
 template <class T, int AMODE, int PREC>
-constexpr bool kWRing = AMODE == kGatherK16 && (PREC == kPrecS3 || PREC == kPrecBF16) && T::RING == 2;
+constexpr bool kWRing = AMODE == kGatherK16 && (PREC == kPrecS3 || (PREC == kPrecBF16 && !T::FAST)) && T::RING == 2;
+// the branch-free ring path (padded stages, every wave the same DMA instructions every step)
+template <class T, int PREC>
+constexpr bool kFastRing = T::RING > 0 && (PREC == kPrecS3 || (PREC == kPrecBF16 && T::FAST));
 
 template <class T, int AMODE, int PREC = kPrecF32>
 struct StageGeom {
@@ -190,7 +199,7 @@ struct StageGeom {
   // kPrecS3 ring stages are padded to whole DMA instructions per wave (16 rows each), so every wave
   // issues the same instructions every step with no per-wave branch (the padding rows take zeros)
   static constexpr int NINS = ROWS / 16;
-  static constexpr int PADROWS = (PREC == kPrecS3 && T::RING > 0) ? 16 * (((NINS + T::NW - 1) / T::NW) * T::NW - NINS) : 0;
+  static constexpr int PADROWS = kFastRing<T, PREC> ? 16 * (((NINS + T::NW - 1) / T::NW) * T::NW - NINS) : 0;
   static constexpr int FLOATS = (ROWS + PADROWS) * 16;
 };
 
@@ -277,6 +286,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   const int F = p.ga.F;
 
   constexpr bool IDRING = kIdRing<T, AMODE, PREC>;
+  constexpr bool FAST = kFastRing<T, PREC>;
   int* idring = reinterpret_cast<int*>(extra);  // IDRING: [2 slots][2 fields][BM] ids
   // WRING + fused first order: the first-order weights of each step's (row, field) pairs ride the
   // DMA ring ([2 slots][2 fields][BM] table elements after the ids), summed per step in field order
@@ -571,12 +581,44 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     RMX_TMARK(5);  // 5: MFMA section (issue)
   };
 
+  // kPrecBF16 fast tiles: one 32-wide K step c -- one bf16 A fragment per row tile (LDS), the B
+  // fragment of each column tile read PF tiles ahead, one MFMA per (row tile, column tile); the
+  // next stages' DMAs ride one per MFMA group (same structure as compute_step_s3, 1/6 the MFMAs)
+  auto compute_step_bf16 = [&](const float* cur, int c, auto&& dma) {
+    bf16x8 a[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+      a[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const f32x4*>(cur + arow[i] * 16 + swz_slot(arow[i], g) * 4));
+    const float* Bt = cur + AROWS * 16;
+    auto ldb = [&](int t) -> f32x4 {
+      const int row = (bt0 + t) * 16 + r16;
+      return *reinterpret_cast<const f32x4*>(Bt + row * 16 + swz_slot(row, g) * 4);
+    };
+    constexpr int PF = RMX_BF_PF < NTW ? RMX_BF_PF : NTW;
+    f32x4 bq[PF + 1];
+#pragma unroll
+    for (int t = 0; t < PF && t < NTW; ++t) bq[t] = ldb(t);
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      if (t + PF < NTW) bq[(t + PF) % (PF + 1)] = ldb(t + PF);
+      if (t < kIPW) dma(t);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 b = __builtin_bit_cast(bf16x8, bq[t % (PF + 1)]);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc[i][t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = NTW; q < kIPW; ++q) dma(q);
+  };
+
   // one K chunk c of the stage image at `cur` (chunk slot cc inside the stage)
   // dma(q): issue this wave's q-th DMA instruction of the next stage (ring kernels), spread over the
   // MFMA groups so its issue stall overlaps MFMAs (a no-op for the register-staged pipeline)
   auto compute_chunk = [&](const float* cur, int cc, int c, auto&& dma, auto&& dpre) {
     if constexpr (S3) {
       compute_step_s3(cur, c, dma, dpre);
+    } else if constexpr (FAST) {
+      compute_step_bf16(cur, c, dma);
     } else {
       const float* Bt = cur + AROWS * 16 + cc * BN * 16;
       f32x4 a[MT];
@@ -653,7 +695,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     constexpr int NINS = ROWS / 16;
     constexpr int IPW = (NINS + NW - 1) / NW;
     // DMAs this wave issues per chunk (kPrecS3: every wave IPW, padding included)
-    const int my_n = S3 ? IPW : (wid < NINS ? (NINS - 1 - wid) / NW + 1 : 0);
+    const int my_n = FAST ? IPW : (wid < NINS ? (NINS - 1 - wid) / NW + 1 : 0);
     // A wave's instructions are the same every step (ins is wave-uniform), so the A / B region
     // and the chunk / plane of an instruction are scalar; dense A and B sources are a 32-bit
     // per-lane element offset plus a per-step stride (launch_cfg checks M * lda < 2^32).
@@ -721,7 +763,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     };
     // get_id(): the ring id of an IDRING A instruction (read here, or one MFMA group earlier)
     auto issue_s3 = [&](int cs, int slot, int q, auto&& get_id) {
-      if constexpr (S3) {
+      if constexpr (FAST) {
         float* buf = smem + slot * STAGE;
         const int ins = wid + q * NW;
         const int row = ins * 16 + (lane >> 2), ps = lane & 3;
@@ -732,7 +774,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
           if constexpr (AMODE == kDenseA) {
             const int m = m0 + r, kk = cs * KC + cc * KCA + g * KSA;
             const uint32_t o = (uint32_t)m * (uint32_t)p.lda + (uint32_t)kk;
-            src = (m < M && kk < p.K) ? (const void*)(p.A + o) : (const void*)zero16;
+            src = (m < M && kk < p.K) ? (BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + o) : (const void*)(p.A + o))
+                                      : (const void*)zero16;
           } else if constexpr (IDRING) {
             const int id = get_id();
             src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)zero16;
@@ -743,7 +786,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         } else {
           const int cc = (ins * 16 - AROWS) / BN;
           const int n = row - AROWS - cc * BN, g = swz_slot(n, ps);
-          src = reinterpret_cast<const bf16_t*>(p.Wp) + ((uint32_t)((cs * 3 + cc) * p.Npad + n0 + n) * 32u + (uint32_t)(g * 8));
+          // kPrecS3: plane cc of step cs (W3 [steps][3][Npad][32]); bf16: W16 [chunks][Npad][32]
+          src = reinterpret_cast<const bf16_t*>(p.Wp) +
+                ((uint32_t)((cs * (S3 ? 3 : 1) + cc) * p.Npad + n0 + n) * 32u + (uint32_t)(g * 8));
           if ((q + 1) * NW > NINS) src = ins < NINS ? src : (const void*)zero16;  // padding instruction
         }
         __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
@@ -752,7 +797,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     auto issue = [&](int c) {
 #pragma unroll
       for (int q = 0; q < IPW; ++q) {
-        if constexpr (S3)
+        if constexpr (FAST)
           issue_s3(c, c % RING, q, [&] { return a_id(c, q); });
         else
           issue_one(c, q);
@@ -946,7 +991,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         run(IC<0>{});
     } else
     for (int c = 0; c < nchunks; ++c) {
-      const int younger = (RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
+      // (fast rings issue every step's DMAs, past the end too: always RING - 2 younger stages)
+      const int younger = (FAST || RING - 2 < nchunks - 1 - c) ? RING - 2 : nchunks - 1 - c;
       RMX_TMARK(6);  // 6: MFMA issue tail of the previous step (+ prologue)
       vm_wait(younger * my_n);                             // this wave's DMAs of chunk c have landed
       RMX_TMARK(0);  // 0: DMA wait
@@ -974,7 +1020,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
               issue_w(cn, q - kQID, [&] { return w_id(cn, q - kQID); });
             }
           }
-        } else if constexpr (S3) {
+        } else if constexpr (FAST) {
           // past the last step: re-read the last step's sources into the free slot (never read)
           issue_s3(cn < nchunks ? cn : nchunks - 1, cn % RING, q - kQID - kQW, [&] { return pend_id; });
         } else if (cn < nchunks) {
@@ -1254,6 +1300,12 @@ inline int tower_variant_for(int NT, Epi epi, bool bf16, int K) {
   return tuning_get("tower_variant", def);
 }
 
+// a bf16 tower layer of Npad columns runs in 208-column slices (tower variant 6): an output layer
+// then writes partial logits and out_finish_kernel combines them
+inline bool bf16_tower_sliced(int Npad, Epi epi, int K, int M, int amode) {
+  return Npad == 416 && M >= 65536 && amode != kGatherAny && tower_variant_for(26, epi, true, K) == 6;
+}
+
 template <int NT, int PREC>
 int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // Large batches (M >= 65536, >= 2 blocks of 128 rows per CU).  Knob "tower_variant":
@@ -1281,6 +1333,10 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
       if constexpr (NT == 26) {
         if (var == 4) return launch_epi<Tile<1, NT / 2, 4, 2, 1, 4, 2>, PREC>(s, p, amode, epi);
         if (var == 5) return launch_epi<Tile<2, NT / 2, 4, 2, 1, 2, 2>, PREC>(s, p, amode, epi);
+        // 6 (bf16): the fast ring tile -- 8 waves of 32 rows x 208 columns (two column slices,
+        // XCD-paired), 3-deep branch-free LDS-DMA ring, 1 block / CU
+        if constexpr (PREC == kPrecBF16)
+          if (var == 6 && amode != kGatherAny) return launch_epi<Tile<2, NT / 2, 8, 1, 1, 2, 3, 0, 1>, PREC>(s, p, amode, epi);
       }
     }
     if (var == 1) return launch_epi<Tile<1, NT, 8, 1, 1, 1, 4>, PREC>(s, p, amode, epi);

@@ -19,3 +19,16 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _env_tuning():
+    """RMX_TEST_TUNING="k=v,k=v": run the suite with kernel knobs set (A/B of a kernel variant under
+    the same parity tests); applied before every test, after any test-local knob reset."""
+    spec = os.environ.get("RMX_TEST_TUNING", "")
+    if spec:
+        import rmx
+        for kv in filter(None, spec.split(",")):
+            k, v = kv.split("=")
+            rmx.set_tuning(k, int(v))
+    yield

@@ -26,11 +26,14 @@ for kv in filter(None, a.set.split(",")):
 ctx = rmx.default_context()
 if a.workload == "xdeepfm":
     m, B = rmx.XDeepFM(V, F, K, [400, 400, 400], [200, 200, 200]), a.batch or 16384
+elif a.workload == "dcn_bf16":
+    m, B = rmx.DCN(V, F, K, 3, [400, 400, 400]), a.batch or 65536
+    m.setPrecision(rmx.DTYPE_BF16)
 else:
     m, B = rmx.DeepFM(V, F, K, [400, 400, 400]), a.batch or 65536
 m.setMats(m.initMats(0x3A75))
 m.setBias(0.01)
-t = rmx.EmbeddingTable(ctx, V, K)
+t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16 if a.workload.endswith("bf16") else rmx.DTYPE_F32)
 t.fill_synthetic(0x7AB1E)
 ids = rmx.DeviceArray(ctx, B * F, np.int32)
 rmx.gen_ids(ctx, 0x5EED2026, 0, B, F, V, ids)
@@ -39,7 +42,8 @@ for _ in range(3):
     m.forward_ids(t, B, ids, out)
 ctx.sync()
 buf = (ctypes.c_ulonglong * 16)()
-assert rmx._lib.lib.rmx_diag_phases(buf) == 0
+fn = rmx._lib.lib.rmx_diag_phases_bf16 if a.workload.endswith("bf16") else rmx._lib.lib.rmx_diag_phases
+assert fn(buf) == 0
 for w in (0, 1):
     v = list(buf)[8 * w:8 * w + 8]
     steps = v[7]
