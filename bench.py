@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="Zipf exponent of the ids within a field (SURVEY.md §8d secondary; 0 = uniform)")
     ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step (default: auto)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="deepfm_sharded: exchange and forward on one stream (default: batch i + 1's exchange "
+                         "on a second stream beside batch i's forward)")
     ap.add_argument("--settle-ms", type=float, default=400.0,
                     help="untimed steps run back to back for this long before the W warm-up steps, so the GPU "
                          "leaves its idle clock state first (0 = off)")
@@ -414,10 +417,35 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         g_loss = rmx.DeviceArray(ctx, 1, np.float32)
         tviews = [tgt.view(s * B, B) for s in range(nb)]
 
+    # deepfm_sharded, overlapped (default): rmx_shard_pull of batch j + 1 into the other pull slot on
+    # a second stream while rmx_forward_pulled runs batch j; every step still does one exchange and
+    # one forward (the first batch's pull happens in the step before it)
+    overlap = sharded and not args.no_overlap
+    pipe = {"j": 0, "pulled": False}
+    ctx_x = rmx.Context(ctx.device) if overlap else None
+
+    def step_overlap():
+        j = pipe["j"]
+        if not pipe["pulled"]:
+            table.pull(views[j % nb][0], B * F, j % 2, ctx_x.stream)
+        table.pull(views[(j + 1) % nb][0], B * F, (j + 1) % 2, ctx_x.stream)
+        model.forward_pulled(table, B, j % 2, views[j % nb][1], stream)
+        pipe["j"], pipe["pulled"] = j + 1, True
+
+    def drain():
+        if overlap and pipe["pulled"]:
+            j = pipe["j"]
+            model.forward_pulled(table, B, j % 2, views[j % nb][1], stream)
+            pipe["j"], pipe["pulled"] = j + 1, False
+            ctx.sync()
+            ctx_x.sync()
+
     def step(i):
         ids_v, out_v = views[i % nb]
         if train:
             model.backward_ids(table, B, ids_v, tviews[i % nb], g_b, g_w, g_e, g_m, g_loss, stream)
+        elif overlap:
+            step_overlap()
         elif sharded:
             model.forward_ids_sharded(table, B, ids_v, out_v, stream)
         else:
@@ -451,6 +479,8 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         step(warmup + i)
     rmx._lib.lib.rmx_event_record(ev1, stream)
     ctx.sync()
+    if overlap:
+        ctx_x.sync()
     wall = time.perf_counter() - t0
     if dist:
         dist.barrier()
@@ -459,14 +489,20 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     t_rank = max_over_ranks(dist, max(wall, ms.value / 1e3))
     value = world * B * steps / t_rank
 
+    drain()  # (overlap) the pull of the batch after the last timed one
     # ---- roofline of the dominant kernel: per-stage HIP events on the launch stream ----
+    # (deepfm_sharded: measured on the one-stream path, exchange and forward in sequence)
     model.set_timing(True)
+    if overlap:
+        overlap, saved = False, overlap
     nt = max(5, min(steps, 20))
     for i in range(nt):
         step(i)
     ctx.sync()
     stages, calls = model.get_timing()
     model.set_timing(False)
+    if sharded and not args.no_overlap:
+        overlap = saved
     split = not bf16 and rmx.get_tuning("f32_split", 1) != 0
 
     def peak_of(stage):
@@ -527,7 +563,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         pa = {"rows": nrows, "predict_ms": round((t1 - t0) * 1e3, 3), "auc_ms": round((t2 - t1) * 1e3, 3),
               "auc": round(a, 6), "labels": "Bernoulli(0.25), independent of the scores (AUC ~ 0.5)"}
     elif sharded:
-        step(0)  # rows [0, B) of this rank again, for the parity check below
+        model.forward_ids_sharded(table, B, views[0][0], views[0][1], stream)  # rows [0, B) again, for parity
         ctx.sync()
     res = {"value": value, "ms_per_step": t_rank * 1e3 / steps, "B": B, "Vw": Vw, "nrows": nrows,
            "roofline": roof, "stages": per_stage, "stage_sum_ms": round(stage_sum, 4), "predict_auc": pa,
@@ -535,7 +571,10 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
            "out": out.numpy()[:512], "bf16": bf16, "split": split}
     if sharded:
         res["exchange"] = {"dedupe": "off" if args.no_dedupe else "auto", "ids_sent_last_step": table.last_sent(),
-                           "nnz_per_step": B * F}
+                           "nnz_per_step": B * F,
+                           "overlap": ("batch i + 1's exchange (rmx_shard_pull) on a second stream beside batch i's "
+                                       "forward (rmx_forward_pulled)") if not args.no_overlap else "none (one stream)",
+                           "table_rows": "[emb 16 | w | pad] fp32, 128 B: one memory line per id"}
     return res
 
 

@@ -268,9 +268,18 @@ int rmx_group_create(int nranks, rmx_group** out);
 int rmx_group_destroy(rmx_group* g);
 int rmx_shard_create_group(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, rmx_group* group, int rank,
                            rmx_shard** out);
-/* Collective: L-B forward of this rank's batch (d_ids [batch * nFields]) over the sharded table. */
+/* Collective: L-B forward of this rank's batch (d_ids [batch * nFields]) over the sharded table
+ * (exchange + forward on one stream, through pull slot 0). */
 int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t batch, const int32_t* d_ids,
                             float* d_out, void* stream);
+/* The same split in two, so batch i + 1's exchange overlaps batch i's forward (the reference's pull*
+ * then forward, ParRecModel.scala:165-199 / :279-306):
+ *   rmx_shard_pull     (collective) exchange n ids into pull slot 0 or 1 on `stream`;
+ *   rmx_forward_pulled forward of the batch in that slot on `stream` (typically another stream: it
+ *                      waits for the pull on the device, and the slot's next pull waits for it).
+ * A slot holds one pull until its forward consumes it (a second pull into it fails RMX_E_INVALID). */
+int rmx_shard_pull(rmx_shard* sh, int64_t n, const int32_t* d_ids, int slot, void* stream);
+int rmx_forward_pulled(rmx_model* m, rmx_shard* sh, int32_t batch, int slot, float* d_out, void* stream);
 
 /* ---- samples: native LIBSVM / LIBFFM parser (host, multi-threaded) ----
  * Replaces SampleParser.parse (yr/data/SampleParser.scala:14-85) for text in memory (one sample per

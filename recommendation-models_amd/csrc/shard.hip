@@ -90,18 +90,28 @@ struct rmx_shard {
   rmx_group* group = nullptr;           // in-process exchange group (or null)
   std::unique_ptr<rmx::Transport> tr;   // RCCL or group transport (null: loopback)
   int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
-  std::vector<float*> emb, w;           // partitions held here: [rows_per][k], [rows_per] (loopback: N)
+  int rs = 0;                           // row stride in floats: [emb k | w | pad], one 128-B line at k < 32
+  std::vector<float*> part;             // partitions held here: [rows_per][rs] (loopback: N)
   // per-batch buffers (grow only)
   int64_t cap_send = 0, cap_recv = 0;
   int32_t* counts = nullptr;            // [4N]: send counts, recv counts, cursors, scratch
   int32_t* h_counts = nullptr;          // pinned host [2N]
   int32_t* send_ids = nullptr;          // [nnz] local rows, bucketed by owner
-  int32_t* perm = nullptr;              // [nnz] slot of id n
   int32_t* recv_ids = nullptr;          // [recv] local rows requested by the PEERS (own bucket excluded)
   float* send_emb = nullptr;            // [recv][k] rows gathered for them
   float* send_w = nullptr;              // [recv]
+  // the exchange's output, the forward's input: two pull slots (rmx_shard_pull / rmx_forward_pulled
+  // overlap batch i + 1's exchange with batch i's forward); perm / recv_* point at the active slot
+  int32_t* perm = nullptr;              // [nnz] slot of id n
   float* recv_emb = nullptr;            // [nnz][k] rows for this rank's batch (bucket order)
   float* recv_w = nullptr;              // [nnz]
+  int32_t* perm_s[2] = {nullptr, nullptr};
+  float* recv_emb_s[2] = {nullptr, nullptr};
+  float* recv_w_s[2] = {nullptr, nullptr};
+  hipEvent_t ready[2] = {nullptr, nullptr};     // slot filled (recorded on the pull's stream)
+  hipEvent_t consumed[2] = {nullptr, nullptr};  // slot read by its forward (on the forward's stream)
+  bool consumed_rec[2] = {false, false};
+  int64_t slot_nnz[2] = {-1, -1};               // ids pulled into the slot, -1 = none pending
   // dedupe (step 0): 0 off, 1 on, 2 auto -- on for one batch, then off for the next kAutoSkip
   // batches when it removed under 10 % of the ids (uniform ids over a large V: the hash pass costs
   // more than the rows it saves), re-probed after them
@@ -233,28 +243,34 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nn
   }
 }
 
-// rows for requested local ids: 4 lanes per row at k = 16 (one float4 each), generic otherwise.
+// rows for requested local ids out of a partition of [emb k | w | pad] rows (stride rs floats).
+// k = 16, rs = 32: 8 lanes per row, one float4 each from the row's single 128-B line -- lanes 0-3
+// the embedding, lane 4 the first-order weight (+ padding), lanes 5-7 idle -- so one id costs one
+// memory line (a [V][k] table plus a separate [V] weight array costs two); generic otherwise.
 // dcount (nullable): the row count lives on the device (the one-rank exchange, no host sync); n is
 // then the grid's upper bound.
-__global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, const int32_t* __restrict__ dcount, int k,
+__global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, const int32_t* __restrict__ dcount, int k, int rs,
                                                           const int32_t* __restrict__ rows,
-                                                          const float* __restrict__ emb, const float* __restrict__ w,
+                                                          const float* __restrict__ part,
                                                           float* __restrict__ out_emb, float* __restrict__ out_w) {
   if (dcount) n = min(n, (int64_t)*dcount);
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k == 16) {
-    const int64_t i = t >> 2;
-    const int c = (int)(t & 3);
-    if (i >= n) return;
+  if (k == 16 && rs == 32) {
+    const int64_t i = t >> 3;
+    const int c = (int)(t & 7);
+    if (i >= n || c > 4) return;
     const int r = rows[i];
-    reinterpret_cast<float4*>(out_emb)[i * 4 + c] = reinterpret_cast<const float4*>(emb)[(int64_t)r * 4 + c];
-    if (c == 0) out_w[i] = w[r];
+    const float4 v = reinterpret_cast<const float4*>(part)[(int64_t)r * 8 + c];
+    if (c < 4)
+      reinterpret_cast<float4*>(out_emb)[i * 4 + c] = v;
+    else
+      out_w[i] = v.x;
     return;
   }
   if (t >= n) return;
-  const int r = rows[t];
-  for (int j = 0; j < k; ++j) out_emb[t * k + j] = emb[(int64_t)r * k + j];
-  out_w[t] = w[r];
+  const float* row = part + (int64_t)rows[t] * rs;
+  for (int j = 0; j < k; ++j) out_emb[t * k + j] = row[j];
+  out_w[t] = row[k];
 }
 
 // step 0: insert ids[n] into the hash set; hslot[n] = its slot (first inserter claims an empty one)
@@ -298,20 +314,19 @@ __device__ __forceinline__ uint64_t splitmix64_d(uint64_t x) {
 
 // owned rows of partition `part`: global id = l*N + part, values of the global generator
 // (oracle orc_gen_table / fill_table_kernel): bit-identical to the replicated table's rows
-__global__ void shard_fill_kernel(uint64_t seed, int64_t V, int64_t rows_per, int N, int part, int k,
-                                  float scale, float* __restrict__ emb, float* __restrict__ w) {
+__global__ void shard_fill_kernel(uint64_t seed, int64_t V, int64_t rows_per, int N, int part, int k, int rs,
+                                  float scale, float* __restrict__ rowsbuf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rows_per * (k + 1)) return;
-  const int64_t l = i / (k + 1);
-  const int j = (int)(i - l * (k + 1));
+  if (i >= rows_per * rs) return;
+  const int64_t l = i / rs;
+  const int j = (int)(i - l * rs);
   const int64_t id = l * N + part;
   float v = 0.f;
-  if (id < V) {
+  if (id < V && j <= k) {  // j == k: the first-order weight; j > k: padding
     const uint64_t h = splitmix64_d(seed ^ (uint64_t)(id * (k + 1) + j));
     v = (float)((int32_t)(h >> 40) - 8388608) * scale;
   }
-  if (j < k) emb[l * k + j] = v;
-  else w[l] = v;
+  rowsbuf[i] = v;
 }
 
 }  // namespace
@@ -336,10 +351,13 @@ int ensure_batch(rmx_shard& sh, int64_t nnz) {
   int st;
   int64_t hc = 1024;
   while (hc < 2 * nnz) hc <<= 1;
-  if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.perm, nnz)) ||
-      (st = realloc_dev(&sh.recv_emb, nnz * sh.k)) || (st = realloc_dev(&sh.recv_w, nnz)) ||
-      (st = realloc_dev(&sh.hslot, nnz)) || (st = realloc_dev(&sh.hkeys, hc)) || (st = realloc_dev(&sh.hvals, hc)))
+  if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.hslot, nnz)) || (st = realloc_dev(&sh.hkeys, hc)) ||
+      (st = realloc_dev(&sh.hvals, hc)))
     return st;
+  for (int q = 0; q < 2; ++q)
+    if ((st = realloc_dev(&sh.perm_s[q], nnz)) || (st = realloc_dev(&sh.recv_emb_s[q], nnz * sh.k)) ||
+        (st = realloc_dev(&sh.recv_w_s[q], nnz)))
+      return st;
   sh.cap_send = nnz;
   sh.cap_hash = hc;
   return RMX_OK;
@@ -369,14 +387,34 @@ int ensure_recv(rmx_shard& sh, int64_t n) {
 // the shard's lock + cross-stream order of its per-batch buffers (see rmx::StreamUse)
 typedef StreamUse<rmx_shard> ShardUse;
 
-int launch_owner_gather(hipStream_t s, int64_t n, int k, const int32_t* rows, const float* emb, const float* w,
+int launch_owner_gather(hipStream_t s, int64_t n, int k, int rs, const int32_t* rows, const float* part,
                         float* out_emb, float* out_w, const int32_t* dcount = nullptr) {
   if (n <= 0) return RMX_OK;
-  const int64_t threads = k == 16 ? n * 4 : n;
-  hipLaunchKernelGGL(owner_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, dcount, k,
-                     rows, emb, w, out_emb, out_w);
+  const int64_t threads = (k == 16 && rs == 32) ? n * 8 : n;
+  hipLaunchKernelGGL(owner_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, dcount, k, rs,
+                     rows, part, out_emb, out_w);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
+}
+
+// the un-permute of rmx_shard_gather: d_emb[i] = recv_emb[perm[i]] (dense [nnz][k] rows + weights)
+__global__ __launch_bounds__(256) void unpermute_kernel(int64_t n, int k, const int32_t* __restrict__ perm,
+                                                       const float* __restrict__ emb, const float* __restrict__ w,
+                                                       float* __restrict__ out_emb, float* __restrict__ out_w) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 16) {  // 4 lanes per row, one float4 each
+    const int64_t i = t >> 2;
+    const int c = (int)(t & 3);
+    if (i >= n) return;
+    const int64_t r = perm[i];
+    reinterpret_cast<float4*>(out_emb)[i * 4 + c] = reinterpret_cast<const float4*>(emb)[r * 4 + c];
+    if (c == 0) out_w[i] = w[r];
+    return;
+  }
+  if (t >= n) return;
+  const int64_t r = perm[t];
+  for (int j = 0; j < k; ++j) out_emb[t * k + j] = emb[r * k + j];
+  out_w[t] = w[r];
 }
 
 }  // namespace
@@ -547,21 +585,16 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
   sh->rank = rank;
   sh->loopback = unique_id == nullptr && group == nullptr;
   sh->rows_per = (V + N - 1) / N;
+  sh->rs = (k + 1 + 31) / 32 * 32;  // [emb | w | pad]: a 128-B line per row for k < 32
   const int parts = sh->loopback ? N : 1;
   for (int p = 0; p < parts; ++p) {
-    float *e = nullptr, *w = nullptr;
-    if (hipMalloc(&e, sizeof(float) * sh->rows_per * k) != hipSuccess ||
-        hipMalloc(&w, sizeof(float) * sh->rows_per) != hipSuccess) {
-      if (e) (void)hipFree(e);
-      for (size_t i = 0; i < sh->emb.size(); ++i) {
-        (void)hipFree(sh->emb[i]);
-        (void)hipFree(sh->w[i]);
-      }
+    float* r = nullptr;
+    if (hipMalloc(&r, sizeof(float) * sh->rows_per * sh->rs) != hipSuccess) {
+      for (float* q : sh->part) (void)hipFree(q);
       set_error("rmx_shard_create: out of device memory for the partition");
       return RMX_E_NOMEM;
     }
-    sh->emb.push_back(e);
-    sh->w.push_back(w);
+    sh->part.push_back(r);
   }
   RMX_HIP(hipMalloc(&sh->counts, sizeof(int32_t) * 4 * N));
   RMX_HIP(hipHostMalloc(&sh->h_counts, sizeof(int32_t) * 2 * N));
@@ -599,14 +632,16 @@ int shard_destroy(rmx_shard* sh) {
     }
     group_unref(sh->group);
   }
-  for (size_t i = 0; i < sh->emb.size(); ++i) {
-    (void)hipFree(sh->emb[i]);
-    (void)hipFree(sh->w[i]);
-  }
-  for (void* p : {(void*)sh->counts, (void*)sh->send_ids, (void*)sh->perm, (void*)sh->recv_ids,
-                  (void*)sh->send_emb, (void*)sh->send_w, (void*)sh->recv_emb, (void*)sh->recv_w,
+  for (float* q : sh->part) (void)hipFree(q);
+  for (void* p : {(void*)sh->counts, (void*)sh->send_ids, (void*)sh->recv_ids, (void*)sh->send_emb, (void*)sh->send_w,
                   (void*)sh->hkeys, (void*)sh->hvals, (void*)sh->hslot, (void*)sh->bcnt})
     if (p) (void)hipFree(p);
+  for (int q = 0; q < 2; ++q) {
+    for (void* p : {(void*)sh->perm_s[q], (void*)sh->recv_emb_s[q], (void*)sh->recv_w_s[q]})
+      if (p) (void)hipFree(p);
+    if (sh->ready[q]) (void)hipEventDestroy(sh->ready[q]);
+    if (sh->consumed[q]) (void)hipEventDestroy(sh->consumed[q]);
+  }
   if (sh->h_counts) (void)hipHostFree(sh->h_counts);
   delete sh;
   return RMX_OK;
@@ -616,11 +651,11 @@ int shard_fill_synthetic(rmx_shard& sh, uint64_t seed) {
   RMX_HIP(hipSetDevice(sh.ctx->device));
   hipStream_t s = sh.ctx->stream;
   const float scale = 0.05f * (1.0f / 8388608.0f);
-  const int64_t tot = sh.rows_per * (sh.k + 1);
-  for (size_t p = 0; p < sh.emb.size(); ++p) {
+  const int64_t tot = sh.rows_per * sh.rs;
+  for (size_t p = 0; p < sh.part.size(); ++p) {
     const int part = sh.loopback ? (int)p : sh.rank;
     hipLaunchKernelGGL(shard_fill_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, sh.V,
-                       sh.rows_per, sh.N, part, sh.k, scale, sh.emb[p], sh.w[p]);
+                       sh.rows_per, sh.N, part, sh.k, sh.rs, scale, sh.part[p]);
     RMX_HIP(hipGetLastError());
   }
   RMX_HIP(hipStreamSynchronize(s));
@@ -638,11 +673,15 @@ void dedupe_auto(rmx_shard& sh, bool dd, int64_t nnz) {
     --sh.dedupe_skip;
 }
 
-// Steps 1-5 of the exchange: fills sh.perm / sh.recv_emb / sh.recv_w for this rank's batch.
-int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids) {
+// Steps 1-5 of the exchange: fills pull slot `slot` (sh.perm / sh.recv_emb / sh.recv_w) for this
+// rank's batch.
+int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot = 0) {
   const int N = sh.N, k = sh.k;
   int st;
   if ((st = ensure_batch(sh, nnz))) return st;
+  sh.perm = sh.perm_s[slot];
+  sh.recv_emb = sh.recv_emb_s[slot];
+  sh.recv_w = sh.recv_w_s[slot];
   int32_t* cnt = sh.counts;           // [N] send counts
   int32_t* rcnt = sh.counts + N;      // [N] recv counts
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
@@ -689,7 +728,7 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     dedupe_auto(sh, dd, nnz);
     for (int o = 0; o < N; ++o) {
       const int64_t c = sh.h_counts[o];
-      if ((st = launch_owner_gather(s, c, k, sh.send_ids + off, sh.emb[o], sh.w[o], sh.recv_emb + off * k,
+      if ((st = launch_owner_gather(s, c, k, sh.rs, sh.send_ids + off, sh.part[o], sh.recv_emb + off * k,
                                     sh.recv_w + off)))
         return st;
       off += c;
@@ -702,7 +741,7 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     sh.last_sent = nnz;
     sh.last_sent_dev = dd;
     dedupe_auto(sh, dd, nnz);
-    return launch_owner_gather(s, nnz, k, sh.send_ids, sh.emb[0], sh.w[0], sh.recv_emb, sh.recv_w,
+    return launch_owner_gather(s, nnz, k, sh.rs, sh.send_ids, sh.part[0], sh.recv_emb, sh.recv_w,
                                dd ? cnt : nullptr);
   }
   Transport& tr = *sh.tr;
@@ -742,8 +781,8 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   }
   if ((st = tr.end(s))) return st;
   // 4. owner gather: every peer's request in one launch, then the own bucket
-  if ((st = launch_owner_gather(s, npeer, k, sh.recv_ids, sh.emb[0], sh.w[0], sh.send_emb, sh.send_w))) return st;
-  if ((st = launch_owner_gather(s, hc[me], k, sh.send_ids + so_me, sh.emb[0], sh.w[0], sh.recv_emb + so_me * k,
+  if ((st = launch_owner_gather(s, npeer, k, sh.rs, sh.recv_ids, sh.part[0], sh.send_emb, sh.send_w))) return st;
+  if ((st = launch_owner_gather(s, hc[me], k, sh.rs, sh.send_ids + so_me, sh.part[0], sh.recv_emb + so_me * k,
                                 sh.recv_w + so_me)))
     return st;
   // 5. rows back, into the requester's bucket order
@@ -868,10 +907,109 @@ extern "C" int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, 
   hipStream_t s = stream ? (hipStream_t)stream : sh->ctx->stream;
   ShardUse use(*sh, s);
   if (use.st) return use.st;
-  int st = shard_exchange(*sh, s, n, d_ids);
+  if (sh->slot_nnz[0] >= 0) {
+    set_error("rmx_shard_gather: pull slot 0 holds a pull no rmx_forward_pulled has consumed yet");
+    return RMX_E_INVALID;
+  }
+  if (sh->consumed_rec[0]) RMX_HIP(hipStreamWaitEvent(s, sh->consumed[0], 0));
+  int st = shard_exchange(*sh, s, n, d_ids, 0);
   if (st) return st;
   // un-permute into id order: d_emb[i] = recv_emb[perm[i]]
-  return launch_owner_gather(s, n, sh->k, sh->perm, sh->recv_emb, sh->recv_w, d_emb, d_w);
+  if (n <= 0) return RMX_OK;
+  const int64_t threads = sh->k == 16 ? n * 4 : n;
+  hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, sh->k, sh->perm,
+                     sh->recv_emb, sh->recv_w, d_emb, d_w);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// Pull (exchange) a batch into slot `slot` on `stream`, then let rmx_forward_pulled consume it on
+// another stream: batch i + 1's exchange runs beside batch i's forward (ParRecModel's pull* and the
+// model forward are separate calls in the reference too: ParRecModel.scala:165-199 then :279-306).
+extern "C" int rmx_shard_pull(rmx_shard* sh, int64_t n, const int32_t* d_ids, int slot, void* stream) {
+  if (!sh || n < 0 || (!d_ids && n > 0) || slot < 0 || slot > 1) {
+    set_error("rmx_shard_pull: bad args (slot must be 0 or 1)");
+    return RMX_E_INVALID;
+  }
+  RMX_HIP(hipSetDevice(sh->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : sh->ctx->stream;
+  ShardUse use(*sh, s);  // the exchange's internal buffers: one pull at a time
+  if (use.st) return use.st;
+  if (sh->slot_nnz[slot] >= 0) {
+    set_error("rmx_shard_pull: slot " + std::to_string(slot) + " holds a pull no forward has consumed yet");
+    return RMX_E_INVALID;
+  }
+  for (int q = 0; q < 2; ++q)
+    if (!sh->ready[q]) {
+      RMX_HIP(hipEventCreateWithFlags(&sh->ready[q], hipEventDisableTiming));
+      RMX_HIP(hipEventCreateWithFlags(&sh->consumed[q], hipEventDisableTiming));
+    }
+  // the slot's previous forward must have read it before the exchange overwrites it
+  if (sh->consumed_rec[slot]) RMX_HIP(hipStreamWaitEvent(s, sh->consumed[slot], 0));
+  int st = shard_exchange(*sh, s, n, d_ids, slot);
+  if (st) return st;
+  RMX_HIP(hipEventRecord(sh->ready[slot], s));
+  sh->slot_nnz[slot] = n;
+  return RMX_OK;
+}
+
+extern "C" int rmx_forward_pulled(rmx_model* m, rmx_shard* sh, int32_t B, int slot, float* d_out, void* stream) {
+  if (!m || !sh || !d_out || B < 0 || slot < 0 || slot > 1 || !m->ctx) {
+    set_error("rmx_forward_pulled: bad args (slot must be 0 or 1)");
+    return RMX_E_INVALID;
+  }
+  if (!m->params_ready && m->mats_len > 0) {
+    set_error("rmx_forward_pulled: call rmx_model_set_mats first");
+    return RMX_E_INVALID;
+  }
+  if (!m->beta_set) {
+    set_error("rmx_forward_pulled: call rmx_model_set_bias first");
+    return RMX_E_INVALID;
+  }
+  if (m->precision != RMX_DTYPE_F32) {
+    set_error("rmx_forward_pulled: sharded tables are fp32 (model precision must be RMX_DTYPE_F32)");
+    return RMX_E_INVALID;
+  }
+  if (m->type != RMX_MODEL_LR && sh->k != m->k) {
+    set_error("rmx_forward_pulled: table embedding_dim differs from the model's");
+    return RMX_E_SHAPE;
+  }
+  RMX_HIP(hipSetDevice(m->ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
+  int32_t* perm;
+  float *emb, *w;
+  {
+    std::lock_guard<std::mutex> lk(sh->mu);
+    if (sh->slot_nnz[slot] != (int64_t)B * m->F) {
+      set_error(sh->slot_nnz[slot] < 0 ? "rmx_forward_pulled: nothing pulled into slot " + std::to_string(slot)
+                                       : "rmx_forward_pulled: the slot holds " + std::to_string(sh->slot_nnz[slot]) +
+                                             " ids, not batch * nFields");
+      return sh->slot_nnz[slot] < 0 ? RMX_E_INVALID : RMX_E_SHAPE;
+    }
+    RMX_HIP(hipStreamWaitEvent(s, sh->ready[slot], 0));
+    perm = sh->perm_s[slot];
+    emb = sh->recv_emb_s[slot];
+    w = sh->recv_w_s[slot];
+  }
+  int st;
+  {
+    ModelUse use(*m, s);
+    if (use.st) return use.st;
+    FwdInputs in;
+    in.B = B;
+    in.ids = perm;
+    in.table = emb;
+    in.wtab = w;
+    in.dtype = kF32;
+    in.beta = m->beta;
+    in.out = d_out;
+    st = model_forward(*m, s, in);
+  }
+  std::lock_guard<std::mutex> lk(sh->mu);
+  RMX_HIP(hipEventRecord(sh->consumed[slot], s));
+  sh->consumed_rec[slot] = true;
+  sh->slot_nnz[slot] = -1;
+  return st;
 }
 
 extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, const int32_t* d_ids, float* d_out,
@@ -902,10 +1040,15 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
   if (suse.st) return suse.st;
   ModelUse use(*m, s);
   if (use.st) return use.st;
+  if (sh->slot_nnz[0] >= 0) {
+    set_error("rmx_forward_ids_sharded: pull slot 0 holds a pull no rmx_forward_pulled has consumed yet");
+    return RMX_E_INVALID;
+  }
+  if (sh->consumed_rec[0]) RMX_HIP(hipStreamWaitEvent(s, sh->consumed[0], 0));
   int st;
   {
     StageTimer t(*m, s, "shard_exchange");
-    st = shard_exchange(*sh, s, (int64_t)B * m->F, d_ids);
+    st = shard_exchange(*sh, s, (int64_t)B * m->F, d_ids, 0);
   }
   if (st) return st;
   if (m->timing) ++m->timed_calls;  // model_forward counts it again; undone below

@@ -297,6 +297,11 @@ class ShardedTable:
         """Ids this rank sent to owners in its last exchange."""
         return int(_lib.lib.rmx_shard_last_sent(self.handle))
 
+    def pull(self, ids_dev, n, slot, stream=None):
+        """Collective: exchange n ids into pull slot 0 / 1 (ParRecModel.pull*); a model's
+        forward_pulled consumes the slot, possibly on another stream."""
+        check(_lib.lib.rmx_shard_pull(self.handle, int(n), ids_dev.ptr, int(slot), stream))
+
     def gather(self, ids_dev, n, w_out, emb_out, stream=None):
         """Collective: rows of ids_dev from their owners (bit-exact copies)."""
         check(_lib.lib.rmx_shard_gather(self.handle, int(n), ids_dev.ptr, w_out.ptr, emb_out.ptr, stream))
@@ -499,6 +504,10 @@ class RecModel:
         """Collective L-B forward over a ShardedTable (every rank calls it with its own batch)."""
         check(_lib.lib.rmx_forward_ids_sharded(self._device(), shard.handle, int(batch), ids_dev.ptr, out_dev.ptr,
                                                stream))
+
+    def forward_pulled(self, shard, batch, slot, out_dev, stream=None):
+        """Forward over the rows ShardedTable.pull put in `slot` (waits for that pull on the device)."""
+        check(_lib.lib.rmx_forward_pulled(self._device(), shard.handle, int(batch), int(slot), out_dev.ptr, stream))
 
     def encoder_ids(self, table, batch, ids_dev, y_dev, stream=None):
         check(_lib.lib.rmx_encoder_ids(self._device(), table.handle, int(batch), ids_dev.ptr, y_dev.ptr, stream))

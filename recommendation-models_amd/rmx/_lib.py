@@ -111,6 +111,8 @@ SIGNATURES = [
     ("rmx_samples_ids", c_int, [c_vp, c_i32, c_vp, c_i64]),
     ("rmx_shard_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_forward_ids_sharded", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
+    ("rmx_shard_pull", c_int, [c_vp, c_i64, c_vp, c_int, c_vp]),
+    ("rmx_forward_pulled", c_int, [c_vp, c_vp, c_i32, c_int, c_vp, c_vp]),
 ]
 
 for _name, _res, _args in SIGNATURES:

@@ -385,3 +385,114 @@ def test_group_exchange_100m_rows_vs_fp64_oracle():
             ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 1)
             err = float(np.abs(got[rows] - ref).max())
             assert err <= 1e-5, err
+
+
+# ------------------------------------------- pull / forward_pulled (exchange beside forward) ----
+def _pipelined(m, sh, ids_all, B, nb, ctx, ctx_x):
+    """Batches 0..nb-1: pull(i + 1) on the exchange stream beside forward_pulled(i) on the main one."""
+    import rmx
+    outs = [rmx.DeviceArray(ctx, B, np.float32) for _ in range(nb)]
+    sh.pull(ids_all.view(0, B * F), B * F, 0, ctx_x.stream)
+    for i in range(nb):
+        if i + 1 < nb:
+            sh.pull(ids_all.view((i + 1) * B * F, B * F), B * F, (i + 1) % 2, ctx_x.stream)
+        m.forward_pulled(sh, B, i % 2, outs[i], ctx.stream)
+    ctx.sync()
+    ctx_x.sync()
+    return [o.numpy() for o in outs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 4])
+def test_pull_pipeline_bitwise_equals_replicated(N):
+    """rmx_shard_pull into alternating slots on a second stream while rmx_forward_pulled runs the
+    previous batch: every batch's output is bitwise the replicated table's (loopback N = 4, one-rank
+    RCCL N = 1)."""
+    import rmx
+    ctx, ctx_x = rmx.default_context(), rmx.Context(0)
+    V, B, nb = 100_003, 1000, 5
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 5, nb * B, F, V, ids)
+    m = rmx.DeepFM(V, F, K, [400, 400, 400])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, N, 0, rmx.comm_unique_id() if N == 1 else None)
+    sh.fill_synthetic(SEED_TAB)
+    ctx.sync()
+    got = _pipelined(m, sh, ids, B, nb, ctx, ctx_x)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    for i in range(nb):
+        m.forward_ids(table, B, ids.view(i * B * F, B * F), ref)
+        ctx.sync()
+        assert np.array_equal(got[i], ref.numpy()), i
+    # the one-stream path still works after pipelined use (slot 0 ordered behind its last forward)
+    m.forward_ids_sharded(sh, B, ids.view(0, B * F), ref)
+    ctx.sync()
+    assert np.array_equal(ref.numpy(), got[0])
+
+
+@pytest.mark.gpu
+def test_pull_slot_misuse_raises():
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 10_007, 64
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids)
+    m = rmx.DeepFM(V, F, K, [32])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, 2)
+    sh.fill_synthetic(SEED_TAB)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    with pytest.raises(rmx.RmxError):
+        m.forward_pulled(sh, B, 1, out)  # nothing pulled
+    sh.pull(ids, B * F, 1)
+    with pytest.raises(rmx.RmxError):
+        sh.pull(ids, B * F, 1)  # slot still holds an unconsumed pull
+    with pytest.raises(rmx.RmxError):
+        m.forward_pulled(sh, B - 1, 1, out)  # batch * nFields differs from the pull
+    m.forward_pulled(sh, B, 1, out)
+    with pytest.raises(rmx.RmxError):
+        sh.pull(ids, B * F, 2)
+    ctx.sync()
+
+
+@pytest.mark.gpu
+def test_group_pull_pipeline(N=2):
+    """The pipelined calls through the N > 1 group schedule: each rank pulls on its exchange stream."""
+    import rmx
+    V, B, nb = 100_003, 500, 3
+    g = rmx.ExchangeGroup(N)
+
+    def rank(r):
+        ctx, ctx_x = rmx.Context(0), rmx.Context(0)
+        sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+        sh.fill_synthetic(SEED_TAB)
+        ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
+        rmx.gen_ids(ctx, SEED_IDS, 100 + r * nb * B, nb * B, F, V, ids)
+        m = _models_v(V)["deepfm"]()
+        m.setMats(m.initMats(SEED_MATS))
+        m.setBias(0.01)
+        ctx.sync()
+        got = _pipelined(m, sh, ids, B, nb, ctx, ctx_x)
+        out = (got, ids.numpy())
+        sh.close()
+        return out
+
+    outs = _run_ranks(N, rank)
+    ctx = rmx.default_context()
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    m = _models_v(V)["deepfm"]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    for got, h_ids in outs:
+        ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
+        ids.upload(h_ids)
+        ref = rmx.DeviceArray(ctx, B, np.float32)
+        for i in range(nb):
+            m.forward_ids(table, B, ids.view(i * B * F, B * F), ref)
+            ctx.sync()
+            assert np.array_equal(got[i], ref.numpy()), i
