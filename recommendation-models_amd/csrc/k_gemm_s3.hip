@@ -78,6 +78,39 @@ int launch_pack_linear_t(hipStream_t s, const float* mats_dev, DenseLayer& L) {
   return launch_pack_split3(s, L.WT, L.KTpad / 16, L.NTpad, L.WT3);
 }
 
+// C_l^T of a CIN layer (C_l: H x F*Hp at c.w_off) packed like a Linear's W^T: element (col j, k h) =
+// C_l[h][j], [KTpad/16][NTpad][16], then split into the three bf16 planes
+int launch_pack_cin_t(hipStream_t s, const float* mats_dev, int F, CinLayer& c) {
+  const int64_t tot = (int64_t)c.KTpad * c.NTpad;
+  hipLaunchKernelGGL(pack_linear_t_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats_dev, c.w_off,
+                     c.H, F * c.Hp, c.KTpad, c.NTpad, c.WT);
+  RMX_HIP(hipGetLastError());
+  return launch_pack_split3(s, c.WT, c.KTpad / 16, c.NTpad, c.WT3);
+}
+
+// dz[r][j] = sum_h gpre[r][h] C_l[h][j] for rows r of a chunk, on the split GEMM (raw store, no bias);
+// dz has row stride ldz >= c.NTpad (columns past F*Hp come out zero)
+int launch_cin_dz_s3(hipStream_t s, const CinLayer& c, int rows, const float* gpre, int ldg, float* dz, int ldz) {
+  if (!c.WT3 || ldz < c.NTpad) {
+    set_error("cin backward: no split-GEMM C^T planes for this layer");
+    return RMX_E_INVALID;
+  }
+  if (rows <= 0) return RMX_OK;
+  GemmArgs p{};
+  p.M = rows;
+  p.K = c.H;
+  p.Kpad = (c.KTpad / 16 + 1) / 2 * 32;
+  p.Npad = c.NTpad;
+  p.A = gpre;
+  p.lda = ldg;
+  p.Wp = reinterpret_cast<const float*>(c.WT3);
+  p.bias = nullptr;
+  p.C = dz;
+  p.ldc = ldz;
+  p.raw = 1;
+  return launch_tower_s3(s, p, kDenseA, Epi::kReluStore);
+}
+
 bool dx_s3_usable(const DenseLayer& L, int ldx) {
   return L.WT3 && f32_split_enabled() && L.NTpad % kS3BN == 0 && L.NTpad <= ldx;
 }

@@ -336,6 +336,10 @@ int model_build(rmx_model& m) {
   for (auto& c : m.cin_layers) {
     if ((st = dev_alloc(&c.W, (size_t)c.Hp_pad * m.F * c.Npad))) return st;
     if ((st = dev_alloc_bf16(&c.W3, split3_elems(c.Hp_pad / kChunk * m.F, c.Npad)))) return st;
+    c.KTpad = round_up(c.H, kChunk);
+    c.NTpad = round_up(m.F * c.Hp, 208);
+    if ((st = dev_alloc(&c.WT, (size_t)c.KTpad * c.NTpad))) return st;
+    if ((st = dev_alloc_bf16(&c.WT3, split3_elems(c.KTpad / kChunk, c.NTpad)))) return st;
     if ((st = dev_alloc(&c.b, c.Npad))) return st;
     if ((st = dev_alloc(&c.wo, c.Npad))) return st;
   }
@@ -424,6 +428,8 @@ void model_release(rmx_model& m) {
   for (auto& c : m.cin_layers) {
     dev_free(c.W);
     dev_free(c.W3);
+    dev_free(c.WT);
+    dev_free(c.WT3);
     dev_free(c.b);
     dev_free(c.wo);
   }
@@ -519,6 +525,7 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   for (auto& c : m.cin_layers) {
     if ((st = launch_pack_cin(s, m.mats_dev, m.F, c))) return st;
     if (c.W3 && (st = launch_pack_split3(s, c.W, c.Hp_pad / kChunk * m.F, c.Npad, c.W3))) return st;
+    if (c.WT3 && (st = launch_pack_cin_t(s, m.mats_dev, m.F, c))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.b_off, c.H, c.Npad, c.b))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.wo_off, c.H, c.Npad, c.wo))) return st;
   }

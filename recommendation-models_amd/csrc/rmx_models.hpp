@@ -55,6 +55,10 @@ struct CinLayer {
   float* b = nullptr;
   float* wo = nullptr;  // [Npad] slice of the output Linear for this layer's pooled maps
   bf16_t* W3 = nullptr;  // kPrecS3 planes of W (k_gemm_s3.hip)
+  // backward dL/dz = gpre C_l on the split GEMM: C_l^T packed [KTpad/16][NTpad][16] (K = H, N = F Hp)
+  float* WT = nullptr;
+  bf16_t* WT3 = nullptr;
+  int KTpad = 0, NTpad = 0;
 };
 
 }  // namespace rmx
@@ -208,6 +212,8 @@ int shard_destroy(rmx_shard* sh);
 
 // kernels specific to the interaction encoders
 int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L);
+int launch_pack_cin_t(hipStream_t s, const float* mats_dev, int F, CinLayer& c);
+int launch_cin_dz_s3(hipStream_t s, const CinLayer& c, int rows, const float* gpre, int ldg, float* dz, int ldz);
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
                      const int32_t* ids, const float* table, const float* u_prev, float* u_out,
                      float* rowdot);

@@ -12,32 +12,21 @@
 //             is stored (ReLU-store epilogue), the tower input x = Reshape(E) is materialised,
 //             and the logit head runs over the stored last hidden layer;
 //   loss      bce_kernel: p -> dL/dz per row + per-block partial sums (deterministic tree);
-//   tower     per layer, from the top: dW = dPre^T x_in and dx_in = dPre W are plain fp32 GEMMs
-//             (rocBLAS: the library path for plain GEMMs), db = dPre^T 1 (GEMV); the ReLU mask
-//             of the layer below is applied by a streaming kernel;
+//   tower     per layer, from the top: dW = dPre^T x_in (wgrad_s3_kernel, split GEMM) and dx_in =
+//             dPre W (the forward's split GEMM on W^T planes, ReLU mask of the layer below fused;
+//             gemm_f32_kernel for layers without W^T planes), db = dPre^T 1 (GEMV);
+//   CIN       dC_l = gpre^T z (wgrad), dL/dz = gpre C_l (split GEMM on C_l^T planes), contracted
+//             into dL/dx0 and dL/du_{l-1}; DCN cross GEMMs on gemm_f32_kernel (no library GEMM);
 //   encoders  emb_grad_kernel: dL/dE = dx (tower) + FM term dz (s_j - e_fj) / k; dL/dw[n] =
 //             dz[index[n]] (Scatter backward).
-#include <rocblas/rocblas.h>
-
 #include <algorithm>
 #include <vector>
 
 #include "rmx_models.hpp"
 
-#define RMX_BLAS(expr)                                                                      \
-  do {                                                                                      \
-    rocblas_status _s = (expr);                                                             \
-    if (_s != rocblas_status_success) {                                                     \
-      ::rmx::set_error(std::string("rocBLAS error ") + rocblas_status_to_string(_s) + " at " \
-                       __FILE__ ":" + std::to_string(__LINE__) + ": " #expr);              \
-      return RMX_E_HIP;                                                                     \
-    }                                                                                       \
-  } while (0)
-
 namespace rmx {
 
 struct TrainState {
-  rocblas_handle blas = nullptr;
   int B = 0;
   int ldx = 0;                  // row stride of x / dx
   float* x = nullptr;           // [B][ldx] tower input (Reshape(B, F*k) of the gathered rows)
@@ -313,13 +302,13 @@ __global__ void cin_z_kernel(int64_t rows, int F, int Hp, const float* __restric
 // gx0[r][f] += sum_h gz[r][f*Hp + h] * up[r][h]: one block per row, wave w takes f = w, w + 4, ...,
 // lanes stride h (coalesced 256-B reads of gz), shuffle reduction per f (fixed order).
 __global__ __launch_bounds__(256) void cin_back_x0_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
-                                                          const float* __restrict__ up, int ldu,
+                                                          int ldz, const float* __restrict__ up, int ldu,
                                                           float* __restrict__ gx0) {
   const int64_t r = blockIdx.x;
   if (r >= rows) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float* uu = up + r * ldu;
-  const float* g = gz + r * (int64_t)F * Hp;
+  const float* g = gz + r * (int64_t)ldz;
   for (int f = w; f < F; f += 4) {
     float acc = 0.f;
     for (int h = lane; h < Hp; h += 64) acc += g[(int64_t)f * Hp + h] * uu[h];
@@ -330,18 +319,106 @@ __global__ __launch_bounds__(256) void cin_back_x0_kernel(int64_t rows, int F, i
 }
 
 // out[r][h] (=, or += when accum) sum_f gz[r][f*Hp + h] * x0[r][f]
-__global__ void cin_back_u_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
+__global__ void cin_back_u_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz, int ldz,
                                   const float* __restrict__ x0, float* __restrict__ out, int ldo, int accum) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * Hp) return;
   const int64_t r = i / Hp;
   const int h = (int)(i - r * Hp);
-  const float* g = gz + r * (int64_t)F * Hp + h;
+  const float* g = gz + r * (int64_t)ldz + h;
   const float* xr = x0 + r * F;
   float acc = 0.f;
   for (int f = 0; f < F; ++f) acc += g[(int64_t)f * Hp] * xr[f];
   if (accum) out[r * ldo + h] += acc;
   else out[r * ldo + h] = acc;
+}
+
+// ---- small / irregular fp32 GEMMs of the backward (replaces the library sgemm) ----
+// C[m][n] (= or += when ACC) sum_k A[m][k] * B(k, n), B(k, n) = B[k * ldb + n] (row-major K x N) or,
+// with BT, B[n * ldb + k] (row-major N x K).  64 x 64 block tiles, 4 waves of 32 x 32 (2 x 2 tiles of
+// v_mfma_f32_16x16x4_f32: an exact fp32 FMA chain), K in 16-wide LDS chunks, zero-filled edges.
+// Used for the tower dX of layers without split-GEMM W^T planes and the DCN cross GEMMs (K or N of
+// the cross width L + 1).
+template <bool BT, bool ACC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
+                                                      const float* __restrict__ B, int ldb, float* __restrict__ C,
+                                                      int ldc) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ float As[64][17];  // [row][k]
+  __shared__ float Bs[16][65];  // [k][col]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int wr = (wid >> 1) * 32, wc = (wid & 1) * 32;
+  const int g = lane >> 4, r16 = lane & 15;
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // A: 64 x 16, consecutive threads along k
+      const int e = tid + q * 256, r = e >> 4, c = e & 15;
+      const int m = m0 + r, k = k0 + c;
+      As[r][c] = (m < M && k < K) ? A[(int64_t)m * lda + k] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // B: 16 x 64
+      const int e = tid + q * 256;
+      int kk, nn;
+      if (BT) {
+        nn = e >> 4;
+        kk = e & 15;
+      } else {
+        kk = e >> 6;
+        nn = e & 63;
+      }
+      const int k = k0 + kk, n = n0 + nn;
+      Bs[kk][nn] = (k < K && n < N) ? (BT ? B[(int64_t)n * ldb + k] : B[(int64_t)k * ldb + n]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int kk = s4 * 4 + g;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float a = As[wr + i * 16 + r16][kk];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[kk][wc + j * 16 + r16], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr + i * 16 + g * 4 + r, n = n0 + wc + j * 16 + r16;
+        if (m < M && n < N) {
+          float* c = C + (int64_t)m * ldc + n;
+          *c = ACC ? *c + acc[i][j][r] : acc[i][j][r];
+        }
+      }
+}
+
+int launch_gemm_f32(hipStream_t s, bool bt, bool accumulate, int M, int N, int K, const float* A, int lda,
+                    const float* B, int ldb, float* C, int ldc) {
+  if (M <= 0 || N <= 0) return RMX_OK;
+  dim3 grid((M + 63) / 64, (N + 63) / 64);
+#define RMX_G(bt_, acc_) hipLaunchKernelGGL((gemm_f32_kernel<bt_, acc_>), grid, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc)
+  if (bt) {
+    if (accumulate) RMX_G(true, true);
+    else RMX_G(true, false);
+  } else {
+    if (accumulate) RMX_G(false, true);
+    else RMX_G(false, false);
+  }
+#undef RMX_G
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
 }
 
 // ---- weight gradients: dW[n][k] = sum_r A[r][n] X[r][k] (reduction over the batch rows) ----
@@ -693,10 +770,6 @@ inline int eff_n(const DenseLayer& L) { return L.N1 >= 0 ? L.N1 : L.N; }
 int ensure_train(rmx_model& m, int B) {
   if (!m.train) m.train = new TrainState();
   TrainState& T = *m.train;
-  if (!T.blas) {
-    RMX_BLAS(rocblas_create_handle(&T.blas));
-    RMX_BLAS(rocblas_set_pointer_mode(T.blas, rocblas_pointer_mode_host));
-  }
   if (B <= T.B) return RMX_OK;
   RMX_HIP(hipDeviceSynchronize());
   tfree(T.x);
@@ -747,7 +820,7 @@ int ensure_train(rmx_model& m, int B) {
     int maxH = 16, maxFH = 16;
     for (auto& c : m.cin_layers) {
       maxH = std::max(maxH, c.Npad);
-      maxFH = std::max(maxFH, m.F * c.Hp);
+      maxFH = std::max(maxFH, std::max(m.F * c.Hp, c.NTpad));  // dz rows are NTpad wide (split GEMM)
     }
     for (auto& c : m.cin_layers) {
       T.u.push_back(nullptr);
@@ -810,7 +883,6 @@ void train_release(rmx_model& m) {
   tfree(T.onesR);
   tfree(T.part2);
   if (T.part) (void)hipFree(T.part);
-  if (T.blas) rocblas_destroy_handle(T.blas);
   delete m.train;
   m.train = nullptr;
 }
@@ -832,9 +904,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   if ((st = ensure_train(m, B))) return st;
   if (m.timing) ++m.timed_calls;
   TrainState& T = *m.train;
-  RMX_BLAS(rocblas_set_stream(T.blas, s));
   const int F = m.F, k = m.k, D = F * k, Lc = m.cross_depth;
-  const float one = 1.f, zero = 0.f;
 
   // ---- forward with stored activations ----
   if (t == RMX_MODEL_LR) {
@@ -897,9 +967,8 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       // wc = [w_0 .. w_{L-1}; W_out[0:D]]; the unfused case gets u / v from one GEMM
       RMX_HIP(hipMemcpyAsync(T.wc, m.cross_w, sizeof(float) * Lc * D, hipMemcpyDeviceToDevice, s));
       RMX_HIP(hipMemcpyAsync(T.wc + (int64_t)Lc * D, m.wo_x, sizeof(float) * D, hipMemcpyDeviceToDevice, s));
-      if (!m.dcn_fused)
-        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_transpose, rocblas_operation_none, Lc + 1, B, D, &one, T.wc,
-                               D, T.x, T.ldx, &zero, T.xcol, Lc + 1));
+      if (!m.dcn_fused && (st = launch_gemm_f32(s, true, false, B, Lc + 1, D, T.x, T.ldx, T.wc, D, T.xcol, Lc + 1)))
+        return st;
       if ((st = launch_cross_finish(s, B, Lc, T.xcol, m.cross_scalars, m.pre2))) return st;
       oa.pre2 = m.pre2;
     }
@@ -966,7 +1035,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       nb = 2;
     }
     // dX on the split GEMM (W^T planes) when the layer has them, with the ReLU backward of the layer
-    // below fused as a mask; otherwise the library GEMM + relu_back_kernel
+    // below fused as a mask; otherwise gemm_f32_kernel + relu_back_kernel
     const float* mask = l > 0 ? T.h[l - 1] : nullptr;
     const int ldmask = l > 0 ? m.layers[l - 1].Npad : 0;
     bool masked = false;
@@ -979,8 +1048,9 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
         if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, dxin + bk.c0, ldin, mask, ldmask))) return st;
         masked = mask != nullptr;
       } else {
-        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, bk.K, B, N, &one,
-                               m.mats_dev + bk.w, bk.K, dpre, L.Npad, &zero, dxin + bk.c0, ldin));
+        if ((st = launch_gemm_f32(s, false, false, B, bk.K, N, dpre, L.Npad, m.mats_dev + bk.w, bk.K, dxin + bk.c0,
+                                  ldin)))
+          return st;
       }
     }
     if (o.g_mats && L.bias_mode == 1 && (st = colsum(T, s, B, N, dpre, L.Npad, nullptr, o.g_mats + L.b_off, false)))
@@ -1008,8 +1078,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
                        T.coef, T.cst);
     RMX_HIP(hipGetLastError());
     // dX += coef [B][L+1] . wc [L+1][D]
-    RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, D, B, Lc + 1, &one, T.wc, D,
-                           T.coef, Lc + 1, &one, dX, T.ldx));
+    if ((st = launch_gemm_f32(s, false, true, B, D, Lc + 1, T.coef, Lc + 1, T.wc, D, dX, T.ldx))) return st;
     if (o.g_mats) {
       // gwc = coef^T x0 ; + the per-row constants summed over the batch ; beta_l sums
       if ((st = wgrad(T, s, B, Lc + 1, D, T.coef, Lc + 1, T.x, T.ldx, T.gwc, false))) return st;
@@ -1055,16 +1124,16 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
           RMX_HIP(hipGetLastError());
           if ((st = wgrad(T, s, rows, H, FH, gp, ldu, T.zb, FH, o.g_mats + c.w_off, r0 > 0))) return st;
         }
-        // dL/dz for this chunk: gpre . C_l  [rows][F*Hp]
-        RMX_BLAS(rocblas_sgemm(T.blas, rocblas_operation_none, rocblas_operation_none, FH, rows, H, &one,
-                               m.mats_dev + c.w_off, FH, gp, ldu, &zero, T.zb, FH));
-        hipLaunchKernelGGL(cin_back_x0_kernel, dim3(rows), dim3(256), 0, s, (int64_t)rows, F, Hp, T.zb,
+        // dL/dz for this chunk: gpre . C_l  [rows][F*Hp], on the split GEMM (C_l^T planes, row stride NTpad)
+        if ((st = launch_cin_dz_s3(s, c, rows, gp, ldu, T.zb, c.NTpad))) return st;
+        const int ldz = c.NTpad;
+        hipLaunchKernelGGL(cin_back_x0_kernel, dim3(rows), dim3(256), 0, s, (int64_t)rows, F, Hp, T.zb, ldz,
                            up + r0 * ldup, ldup, T.gx0 + r0 * F);
         RMX_HIP(hipGetLastError());
         // through u_{l-1} (layer 0: u_0 = x0, so into gx0 as well)
         float* gout = l == 0 ? T.gx0 + r0 * F : T.gu[gcur ^ 1] + r0 * m.cin_layers[l - 1].Npad;
         hipLaunchKernelGGL(cin_back_u_kernel, dim3(nblk((int64_t)rows * Hp)), dim3(256), 0, s, (int64_t)rows, F, Hp,
-                           T.zb, T.x0 + r0 * F, gout, l == 0 ? F : m.cin_layers[l - 1].Npad, l == 0 ? 1 : 0);
+                           T.zb, ldz, T.x0 + r0 * F, gout, l == 0 ? F : m.cin_layers[l - 1].Npad, l == 0 ? 1 : 0);
         RMX_HIP(hipGetLastError());
       }
       gcur ^= 1;

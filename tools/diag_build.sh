@@ -16,5 +16,5 @@ wait
 for d in "$@"; do
   out=../../build/diag$d
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/librmx.so $OBJS $out/k_gemm_s3.o $out/k_gemm_bf16.o \
-    -L/opt/rocm/lib -lrccl -lrocblas -lpthread -Wl,-rpath,/opt/rocm/lib
+    -L/opt/rocm/lib -lrccl -lpthread -Wl,-rpath,/opt/rocm/lib
 done

@@ -13,5 +13,5 @@ while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc $FL $flags -c -o $out/k_gemm_bf16.o k_gemm_bf16.hip &
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out/librmx.so $OBJS $out/k_gemm_s3.o $out/k_gemm_bf16.o \
-    -L/opt/rocm/lib -lrccl -lrocblas -lpthread -Wl,-rpath,/opt/rocm/lib
+    -L/opt/rocm/lib -lrccl -lpthread -Wl,-rpath,/opt/rocm/lib
 done
