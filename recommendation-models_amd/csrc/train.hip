@@ -540,14 +540,22 @@ __device__ __forceinline__ void wg_split(const float* v, wg_bf16x8& hi, wg_bf16x
   }
 }
 
+// GZ: the X operand is the CIN outer product z[r][f * Hp + h] = x0[r][f] * up[r][h] (CINEncoder.scala:152),
+// generated while staged (the same fp32 product cin_z_kernel stores) instead of read from memory
+struct WgZ {
+  const float* x0 = nullptr;  // [rows][F]
+  const float* up = nullptr;  // [rows][ldup]
+  int F = 0, Hp = 0, ldup = 0;
+};
+
 // TT x TT output tile per block (TT = 64: 2 x 2 waves of 32 x 32; TT = 128: 2 x 4 waves of 64 x 32,
 // halving the L2 reads and LDS fragment reads per output), LDS [buf][A | X][plane][col][32 rows] bf16
-template <int TT>
+template <int TT, bool GZ = false>
 __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows, int N, int K,
                                                                         const float* __restrict__ A, int lda,
                                                                         const float* __restrict__ X, int ldx,
                                                                         int rows_per_slice, int tiles,
-                                                                        float* __restrict__ part) {
+                                                                        float* __restrict__ part, WgZ zg) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   constexpr int WJ = TT == 64 ? 2 : 4, TI = TT == 64 ? 2 : 4, TJ = 2;  // waves along k; tiles per wave
   extern __shared__ __attribute__((aligned(16))) wg_bf16x8 wlds[];
@@ -563,6 +571,7 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows
   // staging item: column tid % TT, row octet h = tid / TT (rows 8h..8h+7 of the chunk)
   const int col = tid % TT, h = tid / TT;
   const bool a_ok = n0 + col < N, x_ok = k0 + col < K;
+  const int zf = GZ ? (k0 + col) / zg.Hp : 0, zh = GZ ? k0 + col - zf * zg.Hp : 0;  // (f, h) of column k
   // two register sets: the loads of chunk c + 2 are in flight while chunk c computes and chunk c + 1
   // (loaded two steps earlier) is split into LDS
   float a0[8], x0[8], a1[8], x1[8];
@@ -573,7 +582,10 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows
       const int r = r0 + q;
       const bool ok = r < r_end;
       va[q] = (ok && a_ok) ? A[(int64_t)r * lda + n0 + col] : 0.f;
-      vx[q] = (ok && x_ok) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
+      if constexpr (GZ)
+        vx[q] = (ok && x_ok) ? zg.x0[(int64_t)r * zg.F + zf] * zg.up[(int64_t)r * zg.ldup + zh] : 0.f;
+      else
+        vx[q] = (ok && x_ok) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
     }
   };
   auto sstore = [&](int buf, const float* va, const float* vx) {
@@ -708,12 +720,20 @@ int ensure_part(TrainState& T, int64_t n) {
   return RMX_OK;
 }
 
-// out (N x K row-major) (= or +=) A[rows][lda](N columns)^T . X[rows][ldx](K columns)
+// out (N x K row-major) (= or +=) A[rows][lda](N columns)^T . X[rows][ldx](K columns); zg (split GEMM
+// only, wgrad_z_ok): X is the CIN outer product generated from x0 / up instead of read
+bool wgrad_z_ok() { return f32_split_enabled() && tuning_get("wgrad_s3", 1) != 0; }
+
 int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, int lda, const float* X, int ldx,
-          float* out, bool accum) {
+          float* out, bool accum, const WgZ* zg = nullptr) {
   if (rows <= 0 || N <= 0 || K <= 0) return RMX_OK;
   // knob "wgrad_s3": 0 = the f32 MFMA kernel, 1 = split GEMM with 64 x 64 tiles, 2 = 128 x 128 tiles
   const int var = f32_split_enabled() ? tuning_get("wgrad_s3", 1) : 0;
+  if (zg && !var) {
+    set_error("wgrad: the generated CIN operand needs the split GEMM");
+    return RMX_E_INVALID;
+  }
+  const WgZ z = zg ? *zg : WgZ{};
   const int TT = var == 2 ? 128 : kWgT;
   const int tiles = ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
   // slices of ~1024 rows (one slice of both operands, (N + K) * 4 KiB, stays in an XCD's 4 MiB L2),
@@ -727,15 +747,26 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * 128 * 4;
     static bool attr = false;
     if (!attr) {
-      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_s3_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_s3_kernel<128, false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_s3_kernel<128, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       attr = true;
     }
-    hipLaunchKernelGGL(wgrad_s3_kernel<128>, dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx, rps,
-                       tiles, T.part2);
+    if (zg)
+      hipLaunchKernelGGL((wgrad_s3_kernel<128, true>), dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx,
+                         rps, tiles, T.part2, z);
+    else
+      hipLaunchKernelGGL((wgrad_s3_kernel<128, false>), dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X,
+                         ldx, rps, tiles, T.part2, z);
   } else if (var) {
-    hipLaunchKernelGGL(wgrad_s3_kernel<64>, dim3(tiles * S), dim3(256), sizeof(wg_bf16x8) * 2 * 2 * 3 * 64 * 4, s,
-                       rows, N, K, A, lda, X, ldx, rps, tiles, T.part2);
+    const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * 64 * 4;
+    if (zg)
+      hipLaunchKernelGGL((wgrad_s3_kernel<64, true>), dim3(tiles * S), dim3(256), lds, s, rows, N, K, A, lda, X, ldx,
+                         rps, tiles, T.part2, z);
+    else
+      hipLaunchKernelGGL((wgrad_s3_kernel<64, false>), dim3(tiles * S), dim3(256), lds, s, rows, N, K, A, lda, X,
+                         ldx, rps, tiles, T.part2, z);
   } else {
     hipLaunchKernelGGL(wgrad_kernel, dim3(tiles * S), dim3(256), 0, s, rows, N, K, A, lda, X, ldx, rps, tiles,
                        T.part2);
@@ -1115,10 +1146,21 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
         if ((st = colsum(T, s, (int)R, H, T.u[l], ldu, T.dzr, o.g_mats + c.wo_off, false))) return st;
         if ((st = colsum(T, s, (int)R, H, T.gpre, ldu, nullptr, o.g_mats + c.b_off, false))) return st;
       }
+      // dC_l = gpre^T z over all rows, z = x0 (x) u_{l-1} generated inside the split wgrad (never stored)
+      const bool genz = wgrad_z_ok();
+      if (o.g_mats && genz) {
+        WgZ zg;
+        zg.x0 = T.x0;
+        zg.up = up;
+        zg.F = F;
+        zg.Hp = Hp;
+        zg.ldup = ldup;
+        if ((st = wgrad(T, s, (int)R, H, FH, T.gpre, ldu, nullptr, 0, o.g_mats + c.w_off, false, &zg))) return st;
+      }
       for (int64_t r0 = 0; r0 < R; r0 += T.rc) {
         const int rows = (int)std::min<int64_t>(T.rc, R - r0);
         const float* gp = T.gpre + r0 * ldu;
-        if (o.g_mats) {
+        if (o.g_mats && !genz) {  // f32 MFMA wgrad: z materialised per chunk
           hipLaunchKernelGGL(cin_z_kernel, dim3(nblk((int64_t)rows * FH)), dim3(256), 0, s, (int64_t)rows, F, Hp,
                              T.x0 + r0 * F, up + r0 * ldup, ldup, T.zb);
           RMX_HIP(hipGetLastError());
