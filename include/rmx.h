@@ -246,6 +246,12 @@ int rmx_shard_destroy(rmx_shard* sh);
 /* Owned rows from the same generator as rmx_table_fill_synthetic (bit-identical rows). */
 int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);
 int64_t rmx_shard_local_rows(const rmx_shard* sh);
+/* Owner function (before rmx_shard_fill_synthetic; every rank the same key): key 0 = id mod nranks
+ * (default); else owner = p(id) mod nranks, local row = p(id) div nranks with p a keyed pseudo-random
+ * permutation of [0, num_rows) (4-round Feistel, cycle-walked), so strided or clustered id spaces
+ * spread evenly.  rmx_shard_owner_of: the rank owning id (-1 if out of range). */
+int rmx_shard_set_owner_hash(rmx_shard* sh, uint64_t key);
+int64_t rmx_shard_owner_of(const rmx_shard* sh, int64_t id);
 /* Step 0 of the exchange: send each DISTINCT id of the batch once, as
  * ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull; results are identical.
  * on: 0 off, 1 on, 2 auto (default: off at one rank; else on for a batch, then off for the next 63

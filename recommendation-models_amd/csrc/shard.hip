@@ -4,8 +4,11 @@
 // (ParRecModel.scala:74-105 ColumnRangePartitioner, pull :165-199, make* :279-306) for tables
 // that are sharded over GPUs (BASELINE.json configs[3]: V = 100M over 8 x MI355X).
 //
-// Partitioning: owner(id) = id mod N, local row = id div N (Criteo ids are feature hashes, so
-// modulo partitioning balances; it is a bijection [0, V) -> [N] x [ceil(V/N)]).
+// Partitioning: owner(id) = p(id) mod N, local row = p(id) div N, a bijection [0, V) -> [N] x [ceil(V/N)].
+// p = identity by default (Criteo ids are feature hashes, so modulo partitioning balances), or
+// (rmx_shard_set_owner_hash) a keyed pseudo-random permutation of [0, V): a 4-round Feistel network
+// on the smallest even-width bit domain >= V, cycle-walked back into [0, V) -- strided or clustered
+// real id spaces then spread evenly over the owners, with no lookup table.
 // One exchange step per batch on the caller's stream:
 //   0. dedupe  : (rmx_shard_set_dedupe: off / on / auto, default auto) the batch's distinct ids, as
 //                ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull: an
@@ -90,6 +93,8 @@ struct rmx_shard {
   rmx_group* group = nullptr;           // in-process exchange group (or null)
   std::unique_ptr<rmx::Transport> tr;   // RCCL or group transport (null: loopback)
   int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
+  uint64_t owner_key = 0;               // 0: owner = id mod N; else the Feistel key of p (set_owner_hash)
+  bool filled = false;                  // rows written (the owner function is then fixed)
   int rs = 0;                           // row stride in floats: [emb k | w | pad], one 128-B line at k < 32
   std::vector<float*> part;             // partitions held here: [rows_per][rs] (loopback: N)
   // per-batch buffers (grow only)
@@ -161,24 +166,75 @@ __device__ __forceinline__ int wave_reserve(int o, int* h) {
 // Routing = count -> scan -> scatter with no global atomics: block b histograms its tile of
 // kRouteTile ids by owner into bcnt[o][b] (wave-aggregated LDS counters), one block per owner scans
 // its column into the tile's start offset, and the scatter pass recomputes the in-tile ranks.
-__device__ __forceinline__ int route_owner(const int32_t* ids, int64_t n, int64_t nnz, int N, int* loc) {
+// The keyed permutation p of [0, V) (OwnerPerm.key == 0: identity).  Feistel rounds over 2h bits
+// (2^(2h) >= V, h >= 1), the round function a splitmix64 finaliser of (half, round, key); inverse = the
+// rounds backwards; cycle-walking keeps it a bijection on [0, V) (every cycle re-enters [0, V)).
+struct OwnerPerm {
+  uint64_t key = 0;
+  int h = 1;
+  int64_t V = 0;
+};
+__device__ __host__ __forceinline__ uint32_t feistel_f(uint32_t x, int r, uint64_t key, uint32_t mask) {
+  uint64_t z = ((uint64_t)x << 8) ^ (uint64_t)r ^ key;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return (uint32_t)(z ^ (z >> 31)) & mask;
+}
+__device__ __host__ __forceinline__ int64_t feistel_once(int64_t x, const OwnerPerm& op, bool inverse) {
+  const uint32_t mask = (1u << op.h) - 1u;
+  uint32_t L = (uint32_t)(x >> op.h) & mask, R = (uint32_t)x & mask;
+  if (!inverse) {
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t t = L ^ feistel_f(R, r, op.key, mask);
+      L = R;
+      R = t;
+    }
+  } else {
+    for (int r = 3; r >= 0; --r) {
+      const uint32_t t = R ^ feistel_f(L, r, op.key, mask);
+      R = L;
+      L = t;
+    }
+  }
+  return ((int64_t)L << op.h) | R;
+}
+__device__ __host__ __forceinline__ int64_t owner_perm(int64_t id, const OwnerPerm& op, bool inverse) {
+  if (!op.key) return id;
+  int64_t y = feistel_once(id, op, inverse);
+  while (y >= op.V) y = feistel_once(y, op, inverse);
+  return y;
+}
+
+OwnerPerm owner_perm_of(const rmx_shard& sh) {
+  OwnerPerm op;
+  op.key = sh.owner_key;
+  op.V = sh.V;
+  int b = 1;
+  while ((int64_t(1) << b) < sh.V) ++b;
+  op.h = std::max(1, (b + 1) / 2);
+  return op;
+}
+
+__device__ __forceinline__ int route_owner(const int32_t* ids, int64_t n, int64_t nnz, int N, int* loc,
+                                           const OwnerPerm& op) {
   if (n >= nnz) return -1;
   const int id = ids[n];
   if (id < 0) return -1;  // an empty hash-set slot (dedupe)
-  *loc = id / N;
-  return id % N;
+  const int64_t p = owner_perm(id, op, false);
+  *loc = (int)(p / N);
+  return (int)(p % N);
 }
 
 __global__ __launch_bounds__(kRouteThreads) void route_count_kernel(int64_t nnz, int N, int nb,
                                                                    const int32_t* __restrict__ ids,
-                                                                   int32_t* __restrict__ bcnt) {
+                                                                   int32_t* __restrict__ bcnt, OwnerPerm op) {
   __shared__ int h[kMaxRanks];
   for (int i = threadIdx.x; i < N; i += blockDim.x) h[i] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kRouteTile;
   int own[kRoutePer], loc;
 #pragma unroll
-  for (int u = 0; u < kRoutePer; ++u) own[u] = route_owner(ids, base + u * kRouteThreads + threadIdx.x, nnz, N, &loc);
+  for (int u = 0; u < kRoutePer; ++u) own[u] = route_owner(ids, base + u * kRouteThreads + threadIdx.x, nnz, N, &loc, op);
 #pragma unroll
   for (int u = 0; u < kRoutePer; ++u) (void)wave_reserve(own[u], h);
   __syncthreads();
@@ -217,7 +273,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nn
                                                                      const int32_t* __restrict__ counts,
                                                                      const int32_t* __restrict__ bstart,
                                                                      int32_t* __restrict__ send_ids,
-                                                                     int32_t* __restrict__ perm) {
+                                                                     int32_t* __restrict__ perm, OwnerPerm op) {
   __shared__ int h[kMaxRanks], start[kMaxRanks];
   if (threadIdx.x == 0) {
     int s = 0;
@@ -231,7 +287,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nn
   const int64_t base = (int64_t)blockIdx.x * kRouteTile;
   int own[kRoutePer], loc[kRoutePer];
 #pragma unroll
-  for (int u = 0; u < kRoutePer; ++u) own[u] = route_owner(ids, base + u * kRouteThreads + threadIdx.x, nnz, N, &loc[u]);
+  for (int u = 0; u < kRoutePer; ++u)
+    own[u] = route_owner(ids, base + u * kRouteThreads + threadIdx.x, nnz, N, &loc[u], op);
 #pragma unroll
   for (int u = 0; u < kRoutePer; ++u) {
     const int rk = wave_reserve(own[u], h);
@@ -315,12 +372,13 @@ __device__ __forceinline__ uint64_t splitmix64_d(uint64_t x) {
 // owned rows of partition `part`: global id = l*N + part, values of the global generator
 // (oracle orc_gen_table / fill_table_kernel): bit-identical to the replicated table's rows
 __global__ void shard_fill_kernel(uint64_t seed, int64_t V, int64_t rows_per, int N, int part, int k, int rs,
-                                  float scale, float* __restrict__ rowsbuf) {
+                                  float scale, float* __restrict__ rowsbuf, OwnerPerm op) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows_per * rs) return;
   const int64_t l = i / rs;
   const int j = (int)(i - l * rs);
-  const int64_t id = l * N + part;
+  const int64_t pid = l * N + part;                              // position in p's image
+  const int64_t id = pid < V ? owner_perm(pid, op, true) : V;    // the global id stored there
   float v = 0.f;
   if (id < V && j <= k) {  // j == k: the first-order weight; j > k: padding
     const uint64_t h = splitmix64_d(seed ^ (uint64_t)(id * (k + 1) + j));
@@ -649,13 +707,14 @@ int shard_destroy(rmx_shard* sh) {
 
 int shard_fill_synthetic(rmx_shard& sh, uint64_t seed) {
   RMX_HIP(hipSetDevice(sh.ctx->device));
+  sh.filled = true;
   hipStream_t s = sh.ctx->stream;
   const float scale = 0.05f * (1.0f / 8388608.0f);
   const int64_t tot = sh.rows_per * sh.rs;
   for (size_t p = 0; p < sh.part.size(); ++p) {
     const int part = sh.loopback ? (int)p : sh.rank;
     hipLaunchKernelGGL(shard_fill_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, sh.V,
-                       sh.rows_per, sh.N, part, sh.k, sh.rs, scale, sh.part[p]);
+                       sh.rows_per, sh.N, part, sh.k, sh.rs, scale, sh.part[p], owner_perm_of(sh));
     RMX_HIP(hipGetLastError());
   }
   RMX_HIP(hipStreamSynchronize(s));
@@ -704,12 +763,13 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     }
     const int nb = (int)((rn + kRouteTile - 1) / kRouteTile);
     if ((st = ensure_tiles(sh, nb))) return st;
-    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, sh.bcnt);
+    const OwnerPerm op = owner_perm_of(sh);
+    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, sh.bcnt, op);
     RMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(route_scan_kernel, dim3(N), dim3(1024), 0, s, nb, sh.bcnt, cnt);
     RMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, cnt, sh.bcnt,
-                       sh.send_ids, rslot);
+                       sh.send_ids, rslot, op);
     RMX_HIP(hipGetLastError());
     if (dd) {
       hipLaunchKernelGGL(dedupe_perm_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, sh.hslot,
@@ -868,6 +928,25 @@ extern "C" int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed) {
 }
 
 extern "C" int64_t rmx_shard_local_rows(const rmx_shard* sh) { return sh ? sh->rows_per : -1; }
+
+extern "C" int rmx_shard_set_owner_hash(rmx_shard* sh, uint64_t key) {
+  if (!sh) {
+    set_error("rmx_shard_set_owner_hash: NULL shard");
+    return RMX_E_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(sh->mu);
+  if (sh->filled) {
+    set_error("rmx_shard_set_owner_hash: set the owner function before the rows are filled");
+    return RMX_E_INVALID;
+  }
+  sh->owner_key = key;
+  return RMX_OK;
+}
+
+extern "C" int64_t rmx_shard_owner_of(const rmx_shard* sh, int64_t id) {
+  if (!sh || id < 0 || id >= sh->V) return -1;
+  return owner_perm(id, owner_perm_of(*sh), false) % sh->N;
+}
 
 extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
   if (!sh) {

@@ -281,6 +281,13 @@ class ShardedTable:
     def local_rows(self):
         return int(_lib.lib.rmx_shard_local_rows(self.handle))
 
+    def set_owner_hash(self, key):
+        """Owner = keyed permutation of the id mod nranks (before fill_synthetic; 0 = id mod nranks)."""
+        check(_lib.lib.rmx_shard_set_owner_hash(self.handle, int(key)))
+
+    def owner_of(self, gid):
+        return int(_lib.lib.rmx_shard_owner_of(self.handle, int(gid)))
+
     def set_dedupe(self, on):
         """Send each distinct id of a batch once (ParRecModel.distinctIntIndices): True, False or
         "auto" (the default: off at one rank, else on, then off for 63 batches when it removed < 10 %

@@ -95,6 +95,8 @@ SIGNATURES = [
     ("rmx_shard_create_group", c_int, [c_vp, c_i64, c_int, c_vp, c_int, P(c_vp)]),
     ("rmx_shard_fill_synthetic", c_int, [c_vp, c_u64]),
     ("rmx_shard_local_rows", c_i64, [c_vp]),
+    ("rmx_shard_set_owner_hash", c_int, [c_vp, c_u64]),
+    ("rmx_shard_owner_of", c_i64, [c_vp, c_i64]),
     ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),
     ("rmx_shard_last_sent", c_i64, [c_vp]),
     ("rmx_predict_ids", c_int, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -496,3 +496,82 @@ def test_group_pull_pipeline(N=2):
             m.forward_ids(table, B, ids.view(i * B * F, B * F), ref)
             ctx.sync()
             assert np.array_equal(got[i], ref.numpy()), i
+
+
+# ------------------------------------------------- keyed owner permutation (set_owner_hash) ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [3, 8])
+def test_owner_hash_balances_strided_ids_and_stays_bitwise(N):
+    """Ids that are all multiples of N land on one owner under id mod N; the keyed Feistel permutation
+    spreads them within +-15 %, and the sharded forward (loopback) stays bitwise the replicated one."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 100_003, 1000
+    sh = rmx.ShardedTable(ctx, V, K, N)
+    sh.set_owner_hash(0x1234ABCD)
+    strided = range(0, V, N)
+    cnt = np.bincount([sh.owner_of(i) for i in strided], minlength=N)
+    assert cnt.min() > 0.85 * len(strided) / N and cnt.max() < 1.15 * len(strided) / N
+    plain = rmx.ShardedTable(ctx, V, K, N)
+    assert all(plain.owner_of(i) == 0 for i in range(0, 3000, N))
+    sh.fill_synthetic(SEED_TAB)
+    with pytest.raises(rmx.RmxError):
+        sh.set_owner_hash(7)  # fixed once the rows are filled
+    table, ids = _setup(ctx, V, B, seed_row=21)
+    m = rmx.DeepFM(V, F, K, [400, 400, 400])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    got = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids, ref)
+    m.forward_ids_sharded(sh, B, ids, got)
+    ctx.sync()
+    assert np.array_equal(got.numpy(), ref.numpy())
+    n = 500
+    w = rmx.DeviceArray(ctx, n, np.float32)
+    e = rmx.DeviceArray(ctx, n * K, np.float32)
+    sh.gather(ids, n, w, e)
+    ctx.sync()
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    w_ref, e_ref = oc.gather(wt, et, 1, ids.numpy()[:n].astype(np.int64))
+    assert np.array_equal(w.numpy(), w_ref) and np.array_equal(e.numpy(), e_ref)
+
+
+@pytest.mark.gpu
+def test_group_exchange_owner_hash(N=4):
+    """The N > 1 group schedule with the keyed owner permutation: bitwise the replicated forward."""
+    import rmx
+    V, B = 100_003, 800
+    g = rmx.ExchangeGroup(N)
+
+    def rank(r):
+        ctx = rmx.Context(0)
+        sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+        sh.set_owner_hash(99)
+        sh.fill_synthetic(SEED_TAB)
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        rmx.gen_ids(ctx, SEED_IDS, 7 + r * B, B, F, V, ids)
+        m = _models_v(V)["deepfm"]()
+        m.setMats(m.initMats(SEED_MATS))
+        m.setBias(0.01)
+        got = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids_sharded(sh, B, ids, got, ctx.stream)
+        ctx.sync()
+        out = (got.numpy(), ids.numpy())
+        sh.close()
+        return out
+
+    outs = _run_ranks(N, rank)
+    ctx = rmx.default_context()
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    m = _models_v(V)["deepfm"]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    for got, h_ids in outs:
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        ids.upload(h_ids)
+        ref = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(table, B, ids, ref)
+        ctx.sync()
+        assert np.array_equal(got, ref.numpy())
