@@ -11,7 +11,7 @@
  *   L-B (HBM-resident table, replaces pull + make*):  createContext, createTable, uploadTable,
  *        fillTableSynthetic, setMats, setBias, setPrecision, forwardIds, backwardIds, predictIds, auc
  *   sharded table (RCCL, one rank per GPU):            commUniqueId, createShard, fillShardSynthetic,
- *        forwardIdsSharded
+ *        forwardIdsSharded, setShardOwnerHash
  *
  * A model handle is a `jmodel`: the rmx_model plus device staging for the L-B calls (ids, outputs,
  * targets, gradients), grown on demand and guarded by a mutex, so host int[] ids reach the device
@@ -470,6 +470,13 @@ JNIEXPORT void JNICALL JFN(destroyShard)(JNIEnv* env, jclass cls, jlong sh) {
 JNIEXPORT void JNICALL JFN(fillShardSynthetic)(JNIEnv* env, jclass cls, jlong sh, jlong seed) {
   (void)cls;
   const int st = rmx_shard_fill_synthetic((rmx_shard*)(intptr_t)sh, (uint64_t)seed);
+  if (st) throw_status(env, st);
+}
+
+/* void setShardOwnerHash(long shard, long key) -- before fillShardSynthetic, the same key on every rank */
+JNIEXPORT void JNICALL JFN(setShardOwnerHash)(JNIEnv* env, jclass cls, jlong sh, jlong key) {
+  (void)cls;
+  const int st = rmx_shard_set_owner_hash((rmx_shard*)(intptr_t)sh, (uint64_t)key);
   if (st) throw_status(env, st);
 }
 

@@ -23,7 +23,7 @@ JNI_ABORT = 2
 NATIVES = ["createContext", "destroyContext", "createModel", "destroyModel", "getMatsSize", "forward0", "backward0",
            "setMats", "setBias", "setPrecision", "createTable", "destroyTable", "uploadTable", "fillTableSynthetic",
            "forwardIds", "predictIds", "backwardIds", "auc", "commUniqueId", "createShard", "destroyShard",
-           "fillShardSynthetic", "forwardIdsSharded"]
+           "fillShardSynthetic", "setShardOwnerHash", "forwardIdsSharded"]
 PFX = "Java_io_yaochi_recommendation_model_gpu_GpuRecModel_"
 INT, LONG, FLOAT, BYTE = 1, 2, 3, 4
 
