@@ -139,7 +139,9 @@ def cpu_baseline(workload, budget_s, threads):
     if workload == "lr_plumbing":
         return cpu_baseline_plumbing(oc, budget_s, threads)
     om = _oracle_model(oc, workload)
-    B = 16 if workload == "xdeepfm" else 4096
+    # the oracle parallelises over 8-row blocks (oracle/rmx_oracle.c RB): xDeepFM (~45 rows/s per thread)
+    # takes 8 rows per thread per batch so every thread has a block
+    B = 8 * max(threads, 1) if workload == "xdeepfm" else 4096
     mats = oc.init_mats(om, SEED_MATS)
     done, t_tot, row0 = 0, 0.0, 0
     wt, et = oc.gen_table(SEED_TAB, V, K)
@@ -544,6 +546,10 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         if ent and ent.get("batch") == B:
             roof["traffic"] = ent["hbm_bytes"]
             roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
+            if "mfma_util" in ent:  # measured matrix-pipe occupancy of the same kernel (profiled run)
+                roof["mfma_util_pmc"] = ent["mfma_util"]
+                roof["mfma_util_source"] = ("rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), "
+                                            "profiles/r02/pmc_%s_summary.txt" % workload)
     roof["kernel"] = dom
     roof["algorithmic_per_launch"] = work
 

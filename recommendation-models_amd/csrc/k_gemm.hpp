@@ -846,7 +846,20 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         for (int q = 0; q < kQW; ++q) issue_w(0, q, [&] { return w_id(0, q); });
     for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
     int pend_id = -1;  // kPrecS3: the ring id of the next DMA, read one MFMA group ahead
-    if constexpr (S3 && T::STAG) {
+    if constexpr (RING == 1) {
+      // Single-buffered stage, two (or more) blocks per CU: each block loads a step, computes it,
+      // and only then loads the next, so its own DMA latency and epilogue are exposed -- and covered
+      // by the other resident block's MFMAs instead of by a second LDS stage (kPrecS3 only).
+      static_assert(S3, "the single-stage loop is a split-GEMM tile");
+      for (int c = 0; c < nchunks; ++c) {
+        issue(c);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's DMAs of step c have landed
+        compute_chunk(smem, 0, c, [](int) {}, [](int) {});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave has read step c: the next issue may overwrite it
+      }
+    } else if constexpr (S3 && T::STAG) {
       // Staggered split-GEMM loop (two barriers per K step).  Waves w and w + NW/2 share a SIMD's
       // matrix pipe.  In the plain loop both reach the step barrier together and then both read
       // and split their A fragments (VALU + LDS latency) while the pipe idles.  Here the second

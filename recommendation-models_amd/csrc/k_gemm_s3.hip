@@ -193,6 +193,8 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   const int var = tuning_get("s3_tower", 1);
   p.prio = tuning_get("gemm_prio", 0);
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
+  // 3: 16-row waves, a single-buffered 57 KiB stage, two blocks per CU (4 waves / SIMD)
+  if (var == 3) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 4, 1>, kPrecS3>(s, p, amode, epi);
   if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr)) {
     // knob "s3_stagger": 1 (default) staggered loop on every tower layer, 2 also on the CIN, 0 off
     // (DeepFM 400^3 at B = 65,536: layers 0.1753 / 0.1110 / 0.0961 ms -> 0.1746 / 0.1082 / 0.0928;

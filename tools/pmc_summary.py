@@ -61,10 +61,11 @@ def stage_of(kernel):
         if amode in (1, 2):
             return "tower_layer1"
         return "tower_layer3" if epi == 1 else "tower_layer2"
+    kernel = re.sub(r"^\(anonymous namespace\)::", "", kernel)
     for pat, st in (("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
                     ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
                     ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
-                    ("route_", "shard_exchange"), ("owner_gather", "shard_exchange")):
+                    ("owner_gather", "shard_exchange")):
         if kernel.startswith(pat):
             return st
     return None
@@ -94,6 +95,10 @@ def main():
             e["clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8 / t
         if "SQ_VALU_MFMA_BUSY_CYCLES" in v and "SQ_BUSY_CYCLES" in v and v["SQ_BUSY_CYCLES"] > 0:
             e["mfma_busy_per_sq_busy"] = v["SQ_VALU_MFMA_BUSY_CYCLES"] / v["SQ_BUSY_CYCLES"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in v and v.get("GRBM_GUI_ACTIVE", 0) > 0:
+            # MfmaUtil (rocprofv3 -L): MFMA-busy cycles summed over the 1,024 SIMDs / (per-XCD GPU-active
+            # cycles x 1,024); GRBM_GUI_ACTIVE sums the 8 XCDs (MI355X_MICROARCH.md DVFS recipe)
+            e["mfma_util"] = v["SQ_VALU_MFMA_BUSY_CYCLES"] / (v["GRBM_GUI_ACTIVE"] / 8 * 1024)
         out[k] = e
     for k, e in out.items():
         parts = [k[:70]]
@@ -114,6 +119,8 @@ def main():
             parts.append("lds_conf %.3g" % c["SQ_LDS_BANK_CONFLICT"])
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             parts.append("mfma_busy %.3g" % c["SQ_VALU_MFMA_BUSY_CYCLES"])
+        if "mfma_util" in e:
+            parts.append("MFMA util %.1f %%" % (100 * e["mfma_util"]))
         print(" | ".join(parts))
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
@@ -127,6 +134,8 @@ def main():
             if name and "hbm_bytes" in e:
                 st[name] = {"hbm_bytes": round(e["hbm_bytes"]), "fetch_bytes_x2": round(e["fetch_bytes_x2"]),
                             "write_bytes": round(e["write_bytes"]), "kernel": k, "batch": a.batch}
+                if "mfma_util" in e:
+                    st[name]["mfma_util"] = round(e["mfma_util"], 4)
         db[wl] = st
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         json.dump(db, open(path, "w"), indent=1, sort_keys=True)
