@@ -286,3 +286,46 @@ def test_backward_unsupported_raises():
     with pytest.raises(rmx.RmxError):
         d.backward(2, (np.repeat(np.arange(2), 4), np.arange(8)), np.zeros(1, np.float32), np.zeros(8, np.float32),
                    np.zeros(8 * 16, np.float32), 16, d.initMats(1), d.getMatsSize(), np.ones(2, np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "dcn", "pnn", "xdeepfm"])
+def test_backward_unfiltered_batch_only_ties_differ(kind):
+    """The full batch, no row filtering: every row whose embedding gradient misses the element-wise
+    bar must be a ReLU-tie row (a pre-activation within 1e-4 of the layer's mean magnitude, where fp32
+    and fp64 may take different ReLU branches); the weight gradients meet the array-wide bar."""
+    import rmx
+    ctx = rmx.default_context()
+    B, V, F, K, fc = 512, 20_000, 39, 16, (400, 400, 400)
+    m = _gpu_model(rmx, kind, V, F, K, fc)
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 777, B, F, V, ids)
+    tg = (np.random.default_rng(9).random(B) > 0.7).astype(np.float32)
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload(tg)
+    ml = len(mats)
+    g_b = rmx.DeviceArray(ctx, 1, np.float32)
+    g_w = rmx.DeviceArray(ctx, B * F, np.float32)
+    g_e = rmx.DeviceArray(ctx, B * F * K, np.float32)
+    g_m = rmx.DeviceArray(ctx, ml, np.float32)
+    loss = rmx.DeviceArray(ctx, 1, np.float32)
+    m.backward_ids(t, B, ids, targets, g_b, g_w, g_e, g_m, loss)
+    ctx.sync()
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    h_ids = ids.numpy().astype(np.int64)
+    w, e = oc.gather(wt, et, 1, h_ids)
+    index = np.repeat(np.arange(B), F).astype(np.int64)
+    ref = oc.backward(_orc_model(kind, F, K, fc), B, index, np.array([0.01], np.float32), w, e, mats, tg)
+    assert abs(loss.numpy()[0] - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    assert _close(g_b.numpy(), ref["bias"]) and _close(g_m.numpy(), ref["mats"])
+    ge, re_ = g_e.numpy().reshape(B, F * K).astype(np.float64), ref["embedding"].reshape(B, F * K)
+    mx = np.abs(re_).max()
+    bad_rows = np.where((np.abs(ge - re_) > 1e-3 * np.maximum(np.abs(re_), 1e-3 * mx)).any(axis=1))[0]
+    ties = set(range(B)) - set(_tie_free(kind, et[h_ids.reshape(B, F)].astype(np.float64), mats, fc, rel=1e-4))
+    print("%s: %d rows off the element-wise bar, %d ReLU-tie rows" % (kind, len(bad_rows), len(ties)))
+    assert set(bad_rows.tolist()) <= ties
