@@ -427,11 +427,13 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     ctx_x = rmx.Context(ctx.device) if overlap else None
 
     def step_overlap():
+        # forward j is enqueued first, so the host-side part of pull j + 1 (at N > 1 the counts round
+        # trip and its stream sync) runs while the GPU computes batch j
         j = pipe["j"]
         if not pipe["pulled"]:
             table.pull(views[j % nb][0], B * F, j % 2, ctx_x.stream)
-        table.pull(views[(j + 1) % nb][0], B * F, (j + 1) % 2, ctx_x.stream)
         model.forward_pulled(table, B, j % 2, views[j % nb][1], stream)
+        table.pull(views[(j + 1) % nb][0], B * F, (j + 1) % 2, ctx_x.stream)
         pipe["j"], pipe["pulled"] = j + 1, True
 
     def drain():
