@@ -69,7 +69,12 @@ __device__ __forceinline__ void vm_wait(int n) {
 
 #if RMX_GEMM_DIAG & 8
 // per-phase cycle sums of one wave (block 0, wave 0) of the last split-GEMM launch (tools/diag_phases.py)
-__device__ unsigned long long g_rmx_diag_t[16];  // waves 0 and NW/2 of block 0
+// [0, 16): waves 0 and NW/2 of block 0; [16], [17]: s_memtime and s_memrealtime (100 MHz) spans of wave 0
+__device__ unsigned long long g_rmx_diag_t[18];
+#if RMX_GEMM_DIAG & 256
+// per-block timeline of the last selected launch: s_memrealtime at entry / exit, __smid() | XCC id << 16
+__device__ unsigned long long g_rmx_blk[4096][3];
+#endif
 #define RMX_TMARK(k)                                                             \
   do {                                                                           \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                  \
@@ -84,6 +89,9 @@ __device__ unsigned long long g_rmx_diag_t[16];  // waves 0 and NW/2 of block 0
 
 #ifndef RMX_STAG_PF
 #define RMX_STAG_PF 2
+#endif
+#ifndef RMX_DIAG_NOB
+#define RMX_DIAG_NOB 0  // timing probe only (wrong results): split tiles read B fragments for the first tiles only
 #endif
 #ifndef RMX_BF_PF
 #define RMX_BF_PF 3  // bf16 fast tiles: B fragments read this many column tiles ahead
@@ -256,6 +264,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   const int* neg1 = g_rmx_neg1;
   asm volatile("" : "+s"(zero16));
   asm volatile("" : "+s"(neg1));
+#if RMX_GEMM_DIAG & 256
+  const unsigned long long blk_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   constexpr int RING = T::RING;
   static_assert(RING == 0 || BKC == 1, "the LDS-DMA ring stages one K chunk at a time");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -349,6 +360,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                                                     : (!(RMX_GEMM_DIAG & 16) || AMODE == kCinOuter);
   const bool dmark = blockIdx.x == 0 && blockIdx.y == 0 && (wid == 0 || wid == T::NW / 2) && kDiagSel;
   unsigned long long dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dlast = __builtin_amdgcn_s_memtime();
+  const unsigned long long dt0 = dlast, drt0 = __builtin_amdgcn_s_memrealtime();
 #endif
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -542,7 +554,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     for (int t = 0; t < PF && t < NTW; ++t) ldb(t, bq[t]);
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
-      if (t + PF < NTW) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
+      if (t + PF < NTW && !RMX_DIAG_NOB) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
       // one of the next stage's DMA instructions per tile: a DMA issue can stall the wave for ~200
       // cycles (vector-memory queue), which here overlaps the partner wave's MFMAs instead of
       // idling the SIMD in a separate post-barrier phase
@@ -944,7 +956,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int t = 0; t < NTW; ++t) {
           if (t < t0 || t >= t1) continue;
-          if (t + PF < t1) ldb(t + PF, bq[(t - t0 + PF) % (PF + 1)]);
+          if (t + PF < t1 && !RMX_DIAG_NOB) ldb(t + PF, bq[(t - t0 + PF) % (PF + 1)]);
           if (t - t0 < ndma) dma(t - t0);
           __builtin_amdgcn_sched_barrier(0);
           const f32x4* b = bq[(t - t0) % (PF + 1)];
@@ -1054,6 +1066,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     if (dmark && lane == 0 && (nchunks > 100 || (RMX_GEMM_DIAG & (64 | 128)))) {  // (DIAG & 16: CIN layers 2+)
       for (int k = 0; k < 7; ++k) g_rmx_diag_t[(wid ? 8 : 0) + k] = dsum[k];
       g_rmx_diag_t[(wid ? 8 : 0) + 7] = nchunks;
+      if (wid == 0) {
+        g_rmx_diag_t[16] = __builtin_amdgcn_s_memtime() - dt0;
+        g_rmx_diag_t[17] = __builtin_amdgcn_s_memrealtime() - drt0;
+      }
     }
 #endif
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -1240,6 +1256,16 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       }
     }
   }
+#if RMX_GEMM_DIAG & 256
+  if (kDiagSel && threadIdx.x == 0) {
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    if (bid < 4096) {
+      g_rmx_blk[bid][0] = blk_t0;
+      g_rmx_blk[bid][1] = __builtin_amdgcn_s_memrealtime();
+      g_rmx_blk[bid][2] = __smid() | ((unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 16);  // | XCC_ID << 16
+    }
+  }
+#endif
 }
 
 

@@ -23,7 +23,7 @@ int launch_tower_bf16(hipStream_t s, GemmArgs& p, int nt, int amode, Epi epi) {
 // diagnostic builds only: the per-phase cycle sums of the last recorded bf16 GEMM launch (this
 // translation unit's own copy of g_rmx_diag_t)
 extern "C" int rmx_diag_phases_bf16(unsigned long long* out16) {
-  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 16) == hipSuccess
+  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 18) == hipSuccess
              ? 0
              : -5;
 }

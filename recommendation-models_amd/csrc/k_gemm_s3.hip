@@ -195,7 +195,15 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
   // 3: 16-row waves, a single-buffered 57 KiB stage, two blocks per CU (4 waves / SIMD)
   if (var == 3) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 4, 1>, kPrecS3>(s, p, amode, epi);
+  // 4: 32-row waves, 4-wave blocks on a single-buffered 55 KiB stage, two blocks per CU (the partner
+  // wave on a SIMD belongs to the other block, so one block's DMA wait / epilogue meets the other's MFMAs)
+  if (var == 4) return launch_epi<Tile<2, kS3NT, 4, 1, 1, 2, 1>, kPrecS3>(s, p, amode, epi);
   if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr)) {
+    // knob "s3_dense_store": 4 (default) runs the dense stored layers on variant 4 (DeepFM layer 2 at
+    // B = 65,536: 0.1075 vs 0.1114 ms staggered; the output-dot layer ties and the gathered layer 1
+    // loses, 0.215 vs 0.181: single-buffered, it waits out every random-row gather), 1 staggered
+    if (amode == kDenseA && epi == Epi::kReluStore && tuning_get("s3_dense_store", 4) == 4)
+      return launch_epi<Tile<2, kS3NT, 4, 1, 1, 2, 1>, kPrecS3>(s, p, amode, epi);
     // knob "s3_stagger": 1 (default) staggered loop on every tower layer, 2 also on the CIN, 0 off
     // (DeepFM 400^3 at B = 65,536: layers 0.1753 / 0.1110 / 0.0961 ms -> 0.1746 / 0.1082 / 0.0928;
     // the CIN runs slower staggered: 3.06 -> 3.16 ms per layer, its B planes then get half a step
@@ -230,7 +238,16 @@ int launch_cin_s3(hipStream_t s, GemmArgs& p) {
 #if RMX_GEMM_DIAG & 8
 // diagnostic builds only: the per-phase cycle sums of the last split-GEMM launch
 extern "C" int rmx_diag_phases(unsigned long long* out16) {
-  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 16) == hipSuccess
+  return hipMemcpyFromSymbol(out16, HIP_SYMBOL(rmx::g_rmx_diag_t), sizeof(unsigned long long) * 18) == hipSuccess
+             ? 0
+             : -5;
+}
+#endif
+
+#if RMX_GEMM_DIAG & 256
+// diagnostic builds only: the per-block timeline of the last selected split-GEMM launch
+extern "C" int rmx_diag_blocks(unsigned long long* out, int nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rmx::g_rmx_blk), sizeof(unsigned long long) * 3 * nblocks) == hipSuccess
              ? 0
              : -5;
 }

@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense_store": 4, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
         rmx.set_tuning(k, v)
 
 
@@ -96,7 +96,7 @@ def test_split_matches_oracle_and_f32_engine(ctx, kind, B):
     assert np.array_equal(run(), p_s3)
 
 
-@pytest.mark.parametrize("knob,values", [("s3_tower", [0, 1, 2]), ("s3_cin", [0, 1, 2, 3])])
+@pytest.mark.parametrize("knob,values", [("s3_tower", [0, 1, 2, 3, 4]), ("s3_cin", [0, 1, 2, 3])])
 def test_split_variants(ctx, knob, values):
     kind = "xdeepfm" if knob == "s3_cin" else "dnn"
     run, ref64 = _case(ctx, kind, 300, row0=999)
@@ -105,6 +105,36 @@ def test_split_variants(ctx, knob, values):
         err = float(np.abs(run() - ref64).max())
         print("%s=%d: max|p - p_fp64| = %.3g" % (knob, v, err))
         assert err <= TOL
+
+
+def test_dense_store_variant_bitwise(ctx):
+    """s3_dense_store = 4 (4-wave blocks, two per CU, single-buffered) and 1 (the staggered 8-wave
+    tile) accumulate each output element in the same K order: identical bits, at a batch large
+    enough (M >= 32,513) for the 32-row-wave tiles; head rows against the fp64 oracle."""
+    B, V = 40000, 50000
+    m = _model("dnn", V)
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids_dev = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_dev)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    res = []
+    for v in (1, 4):
+        rmx.set_tuning("s3_dense_store", v)
+        m.forward_ids(table, B, ids_dev, out)
+        ctx.sync()
+        res.append(out.numpy().copy())
+    assert np.array_equal(res[0], res[1])
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    n = 512
+    ids = oc.gen_ids(SEED_IDS, 0, n, F, V).astype(np.int64)
+    w, e = oc.gather(wt, et, 1, ids)
+    index = np.repeat(np.arange(n, dtype=np.int64), F)
+    ref = oc.forward(oc.make_model(oc.DNN, F, K, fc=(400, 400)), n, index, np.array([0.01], np.float32), w, e, mats, 1)
+    assert np.abs(res[1][:n] - ref).max() <= TOL
 
 
 def test_split_headline_deepfm_full_batch(ctx):

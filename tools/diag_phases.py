@@ -17,6 +17,7 @@ NAMES = ["dma_wait", "barrier", "dma_issue", "a_frag", "split", "mfma_section", 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="xdeepfm")
 ap.add_argument("--batch", type=int, default=0)
+ap.add_argument("--warm-s", type=float, default=2.5)
 ap.add_argument("--set", default="", help="knobs k=v,k=v")
 a = ap.parse_args()
 F, K, V = 39, 16, 1_000_000
@@ -38,10 +39,14 @@ t.fill_synthetic(0x7AB1E)
 ids = rmx.DeviceArray(ctx, B * F, np.int32)
 rmx.gen_ids(ctx, 0x5EED2026, 0, B, F, V, ids)
 out = rmx.DeviceArray(ctx, B, np.float32)
-for _ in range(3):
+import time
+t_end = time.time() + a.warm_s  # >= 2 s of back-to-back launches first (MI355X_MICROARCH.md DVFS item 6)
+while True:
     m.forward_ids(t, B, ids, out)
-ctx.sync()
-buf = (ctypes.c_ulonglong * 16)()
+    ctx.sync()
+    if time.time() >= t_end:
+        break
+buf = (ctypes.c_ulonglong * 18)()
 fn = rmx._lib.lib.rmx_diag_phases_bf16 if a.workload.endswith("bf16") else rmx._lib.lib.rmx_diag_phases
 assert fn(buf) == 0
 for w in (0, 1):
@@ -51,3 +56,6 @@ for w in (0, 1):
     print("last recorded split-GEMM launch (%s): %d K steps, block 0 wave %s" % (a.workload, steps, "0" if w == 0 else "NW/2"))
     for n, x in zip(NAMES, v[:7]):
         print("  %-20s %12d cycles  %6.0f /step  %5.1f %%" % (n, x, x / max(steps, 1), 100.0 * x / max(tot, 1)))
+v = list(buf)
+if v[17]:
+    print("wave 0 of block 0: %d cycles in %.1f us -> in-kernel clock %.2f GHz" % (v[16], v[17] / 100.0, v[16] / v[17] * 0.1))
