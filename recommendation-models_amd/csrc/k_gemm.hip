@@ -246,6 +246,10 @@ int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, in
   p.ldc = L.Npad;
   p.wo = L.wo;
   p.rowdot = rowdot;
+  if (p.K / 16 + 8 >= 65536 || F >= 65536) {  // the kernel's exact c16 / F (k_gemm.hpp div_f)
+    set_error("cin: F * H_prev must stay below 1,048,448");
+    return RMX_E_INVALID;
+  }
   if (first && L.Hp_pad > p.XS - 4) {
     set_error("cin: first layer Hp_pad mismatch");
     return RMX_E_INVALID;

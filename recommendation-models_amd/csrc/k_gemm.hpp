@@ -93,6 +93,9 @@ __device__ unsigned long long g_rmx_blk[4096][3];
 #ifndef RMX_DIAG_NOB
 #define RMX_DIAG_NOB 0  // timing probe only (wrong results): split tiles read B fragments for the first tiles only
 #endif
+#ifndef RMX_DIAG_NODMA
+#define RMX_DIAG_NODMA 0  // timing probe only (wrong results): the plain split loop issues no DMAs after its prologue
+#endif
 #ifndef RMX_BF_PF
 #define RMX_BF_PF 3  // bf16 fast tiles: B fragments read this many column tiles ahead
 #endif
@@ -470,8 +473,17 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
     cur_hc[h] = hc;
   };
   // CIN A fragment of 16-wide chunk c16 (= hc * F + f): a = x0[row][f] * u[row][16 hc + 4 g ..]
+  // c16 / F for the (wave-uniform) chunk index: q = floor(c16 * ceil(2^32 / F) / 2^32) is exact for
+  // c16, F < 2^16 -- two scalar multiplies instead of the generic division's VALU sequence
+  const uint64_t fmagic = ((1ull << 32) + (uint64_t)F - 1) / (uint64_t)(F > 0 ? F : 1);
+#ifndef RMX_CIN_DIVF
+#define RMX_CIN_DIVF 1  // (0: the generic division, timing A/B only)
+#endif
+  auto div_f = [&](int c16) -> int {
+    return RMX_CIN_DIVF ? (int)(((uint64_t)(uint32_t)c16 * fmagic) >> 32) : c16 / F;
+  };
   auto cin_x0 = [&](int c16, float* xv) {  // the x0 scalars of chunk c16 (LDS)
-    const int f = c16 - (c16 / F) * F;
+    const int f = c16 - div_f(c16) * F;
 #pragma unroll
     for (int i = 0; i < MT; ++i) xv[i] = c16 * 16 < p.K ? extra[arow[i] * p.XS + f] : 0.f;
   };
@@ -481,7 +493,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       for (int i = 0; i < MT; ++i) a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       return;
     }
-    const int hc = c16 / F;
+    const int hc = div_f(c16);
     if (hc != cur_hc[h]) load_u(h, hc);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -558,7 +570,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       // one of the next stage's DMA instructions per tile: a DMA issue can stall the wave for ~200
       // cycles (vector-memory queue), which here overlaps the partner wave's MFMAs instead of
       // idling the SIMD in a separate post-barrier phase
-      if (t < kIPW) dma(t);
+      if (t < kIPW && !RMX_DIAG_NODMA) dma(t);
       // the LDS-held operand (a ring id) of the next DMA is read one MFMA group ahead of its use
       if (t + 1 < kIPW) dpre(t + 1);
       if constexpr (!A_LDS)
@@ -589,7 +601,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       }
     }
 #pragma unroll
-    for (int q = NTW; q < kIPW; ++q) dma(q);
+    for (int q = NTW; q < kIPW; ++q)
+      if (!RMX_DIAG_NODMA) dma(q);
     RMX_TMARK(5);  // 5: MFMA section (issue)
   };
 
@@ -985,15 +998,22 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         for (int c = 0; c < nchunks; ++c) {
           // bar0(c): this wave's DMAs (A / w / ids of step c by phase 1 of step c - 1, B of step c
           // by phase 2) have landed; after the barrier, every wave's have
+          RMX_TMARK(6);  // (diagnostic phases of the staggered loop: 6 tail of phase 2 + this wait)
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          RMX_TMARK(0);  // 0: DMA / LDS wait before bar0
           __builtin_amdgcn_s_barrier();
+          RMX_TMARK(1);  // 1: bar0
           const float* cur = smem + (c & 1) * STAGE;
           if constexpr (!kLate) {
             prep(cur, c);
+            RMX_TMARK(2);  // 2: prep (X)
             tiles(cur, IC<0>{}, IC<NT1>{}, IC<NP1>{}, [&](int q) { dma1(c, q); });
+            RMX_TMARK(3);  // 3: phase-1 tiles
             __builtin_amdgcn_s_barrier();  // bar1(c): Y has read the B planes of step c - 1
+            RMX_TMARK(4);  // 4: bar1
             tiles(cur, IC<NT1>{}, IC<NTW>{}, IC<NP2>{}, [&](int q) { dma2(c, q); });
+            RMX_TMARK(5);  // 5: phase-2 tiles
           } else {
             if (c > 0) {
               tiles(smem + ((c - 1) & 1) * STAGE, IC<NT1>{}, IC<NTW>{}, IC<NP1>{}, [&](int q) { dma1(c, q); });
@@ -1001,10 +1021,14 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
 #pragma unroll
               for (int q = 0; q < NP1; ++q) dma1(c, q);
             }
+            RMX_TMARK(3);  // 3: phase-1 tiles
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // its B reads of step c - 1 are done
             __builtin_amdgcn_s_barrier();                        // bar1(c)
+            RMX_TMARK(4);  // 4: bar1
             prep(cur, c);
+            RMX_TMARK(2);  // 2: prep (Y)
             tiles(cur, IC<0>{}, IC<NT1>{}, IC<NP2>{}, [&](int q) { dma2(c, q); });
+            RMX_TMARK(5);  // 5: phase-2 tiles
           }
         }
         if constexpr (kLate)

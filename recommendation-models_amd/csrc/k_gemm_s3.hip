@@ -217,11 +217,13 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 
 // CIN layer, kPrecS3 (H <= 208): only the B planes go through LDS (39 KiB per K step); the A
 // operand x0[f] * u[h] is formed in fp32 registers and split there.  Knob "s3_cin":
-//   0  MT = 1, 2-deep LDS-DMA ring;  1  MT = 1, 3-deep ring;  2  MT = 2, 2-deep ring (default:
-//   CIN 200^3 at B = 16,384, layer 2: 3.73 ms vs 4.60 (MT = 1) and 6.69 on the f32 MFMA engine);
-//   3  MT = 1, register-staged double buffer.
+//   0  MT = 1, 2-deep LDS-DMA ring;  1  MT = 1, 3-deep ring;  2  MT = 2, 2-deep ring (CIN 200^3 at
+//   B = 16,384, layer 2: 3.73 ms vs 4.60 (MT = 1, 8 waves) and 6.69 on the f32 MFMA engine);
+//   3  MT = 1, register-staged double buffer;  4 (default) MT = 1, 16 waves (4 per SIMD), 2-deep ring:
+//   twice the B-fragment LDS reads of 2, hidden by the extra waves (B = 16,384: layer 1 0.827 ->
+//   0.795 ms, layers 2+ 3.037 -> 3.022 ms).
 int launch_cin_s3(hipStream_t s, GemmArgs& p) {
-  const int var = tuning_get("s3_cin", 2);
+  const int var = tuning_get("s3_cin", 4);
   p.prio = tuning_get("gemm_prio", 0);
   if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   if (var == 2) {
@@ -230,6 +232,7 @@ int launch_cin_s3(hipStream_t s, GemmArgs& p) {
     return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   }
   if (var == 3) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+  if (var == 4) return launch_cfg<Tile<1, kS3NT, 16, 1, 1, 4, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
 }
 

@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense_store": 4, "s3_cin": 2, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense_store": 4, "s3_cin": 4, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
         rmx.set_tuning(k, v)
 
 
@@ -96,7 +96,7 @@ def test_split_matches_oracle_and_f32_engine(ctx, kind, B):
     assert np.array_equal(run(), p_s3)
 
 
-@pytest.mark.parametrize("knob,values", [("s3_tower", [0, 1, 2, 3, 4]), ("s3_cin", [0, 1, 2, 3])])
+@pytest.mark.parametrize("knob,values", [("s3_tower", [0, 1, 2, 3, 4]), ("s3_cin", [0, 1, 2, 3, 4])])
 def test_split_variants(ctx, knob, values):
     kind = "xdeepfm" if knob == "s3_cin" else "dnn"
     run, ref64 = _case(ctx, kind, 300, row0=999)

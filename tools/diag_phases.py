@@ -18,8 +18,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="xdeepfm")
 ap.add_argument("--batch", type=int, default=0)
 ap.add_argument("--warm-s", type=float, default=2.5)
+ap.add_argument("--stag", action="store_true", help="name the staggered loop's phases")
 ap.add_argument("--set", default="", help="knobs k=v,k=v")
 a = ap.parse_args()
+if a.stag:
+    NAMES = ["wait_before_bar0", "bar0", "prep", "phase1_tiles", "bar1", "phase2_tiles", "tail+prologue"]
 F, K, V = 39, 16, 1_000_000
 for kv in filter(None, a.set.split(",")):
     k_, v_ = kv.split("=")
