@@ -79,7 +79,7 @@ const char* rmx_last_error(void);
 int rmx_abi_version(void);
 
 /* Process-wide tuning knobs (kernel variant selection for A/B timing in one process).
- * Known keys (README.md lists them): "f32_split", "s3_tower", "s3_cin", "tower_variant" (GEMM
+ * Known keys (README.md lists them): "f32_split", "s3_tower", "s3_dense", "s3_cin", "tower_variant" (GEMM
  * engine and tile variants, csrc/k_gemm.hpp, k_gemm_s3.hip), "fm_fuse", "fm_y1", "fo_fuse" (first
  * order / FM inside tower layer 1), "wgrad_s3" (training dW kernel, csrc/train.hip).  Unknown keys
  * are stored and ignored.  rmx_get_tuning returns def when the key was never set; setting

@@ -199,11 +199,17 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // wave on a SIMD belongs to the other block, so one block's DMA wait / epilogue meets the other's MFMAs)
   if (var == 4) return launch_epi<Tile<2, kS3NT, 4, 1, 1, 2, 1>, kPrecS3>(s, p, amode, epi);
   if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr)) {
-    // knob "s3_dense_store": 4 (default) runs the dense stored layers on variant 4 (DeepFM layer 2 at
-    // B = 65,536: 0.1075 vs 0.1114 ms staggered; the output-dot layer ties and the gathered layer 1
-    // loses, 0.215 vs 0.181: single-buffered, it waits out every random-row gather), 1 staggered
-    if (amode == kDenseA && epi == Epi::kReluStore && tuning_get("s3_dense_store", 4) == 4)
-      return launch_epi<Tile<2, kS3NT, 4, 1, 1, 2, 1>, kPrecS3>(s, p, amode, epi);
+    // knob "s3_dense" (dense-A layers at this size; all accumulate in the same K order: equal bits):
+    //   5 (default) 16 waves of 16 rows, 4 per SIMD, 2-deep ring (the CIN's s3_cin 4 shape; DeepFM at
+    //     B = 65,536: layer 2 0.1075, layer 3 0.0929 ms);
+    //   4 stored layers on 4-wave blocks of 32-row waves, two blocks per CU, single-buffered (layer 2
+    //     0.1075 vs 0.1114 ms staggered; the gathered layer 1 loses on it, 0.215 vs 0.181: it waits
+    //     out every random-row gather);  1 the staggered 8-wave tile (layer 3 0.0959 ms).
+    if (amode == kDenseA) {
+      const int dv = tuning_get("s3_dense", 5);
+      if (dv == 5) return launch_epi<Tile<1, kS3NT, 16, 1, 1, 4, 2>, kPrecS3>(s, p, amode, epi);
+      if (dv == 4 && epi == Epi::kReluStore) return launch_epi<Tile<2, kS3NT, 4, 1, 1, 2, 1>, kPrecS3>(s, p, amode, epi);
+    }
     // knob "s3_stagger": 1 (default) staggered loop on every tower layer, 2 also on the CIN, 0 off
     // (DeepFM 400^3 at B = 65,536: layers 0.1753 / 0.1110 / 0.0961 ms -> 0.1746 / 0.1082 / 0.0928;
     // the CIN runs slower staggered: 3.06 -> 3.16 ms per layer, its B planes then get half a step

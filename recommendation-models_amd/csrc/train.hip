@@ -728,7 +728,11 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
           float* out, bool accum, const WgZ* zg = nullptr) {
   if (rows <= 0 || N <= 0 || K <= 0) return RMX_OK;
   // knob "wgrad_s3": 0 = the f32 MFMA kernel, 1 = split GEMM with 64 x 64 tiles, 2 = 128 x 128 tiles
-  const int var = f32_split_enabled() ? tuning_get("wgrad_s3", 1) : 0;
+  int var = f32_split_enabled() ? tuning_get("wgrad_s3", 1) : 0;
+  // the generated CIN operand (N = H, K = F * Hp, rows = B * k) runs on the 128 x 128 tiles unless
+  // "wgrad_gz" = 64: xDeepFM training at B = 4,096: CIN backward 14.88 -> 14.00 ms (the tower's dW,
+  // K <= 624, stays faster on 64 x 64 tiles)
+  if (zg && var == 1 && tuning_get("wgrad_gz", 128) == 128) var = 2;
   if (zg && !var) {
     set_error("wgrad: the generated CIN operand needs the split GEMM");
     return RMX_E_INVALID;

@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense_store": 4, "s3_cin": 4, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense": 5, "s3_cin": 4, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
         rmx.set_tuning(k, v)
 
 
@@ -107,10 +107,11 @@ def test_split_variants(ctx, knob, values):
         assert err <= TOL
 
 
-def test_dense_store_variant_bitwise(ctx):
-    """s3_dense_store = 4 (4-wave blocks, two per CU, single-buffered) and 1 (the staggered 8-wave
-    tile) accumulate each output element in the same K order: identical bits, at a batch large
-    enough (M >= 32,513) for the 32-row-wave tiles; head rows against the fp64 oracle."""
+def test_dense_variants_bitwise(ctx):
+    """The dense-layer tiles (s3_dense 5: 16 waves of 16 rows; 4: 4-wave blocks of 32-row waves, two
+    per CU, single-buffered; 1: the staggered 8-wave tile) accumulate each output element in the same
+    K order: identical bits, at a batch large enough (M >= 32,513) for these tiles; head rows against
+    the fp64 oracle."""
     B, V = 40000, 50000
     m = _model("dnn", V)
     mats = m.initMats(SEED_MATS)
@@ -122,12 +123,13 @@ def test_dense_store_variant_bitwise(ctx):
     rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_dev)
     out = rmx.DeviceArray(ctx, B, np.float32)
     res = []
-    for v in (1, 4):
-        rmx.set_tuning("s3_dense_store", v)
+    for v in (1, 4, 5):
+        rmx.set_tuning("s3_dense", v)
         m.forward_ids(table, B, ids_dev, out)
         ctx.sync()
         res.append(out.numpy().copy())
     assert np.array_equal(res[0], res[1])
+    assert np.array_equal(res[0], res[2])
     wt, et = oc.gen_table(SEED_TAB, V, K)
     n = 512
     ids = oc.gen_ids(SEED_IDS, 0, n, F, V).astype(np.int64)

@@ -221,17 +221,20 @@ def test_backward_ids_matches_oracle(kind, B, fc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant,gz", [(0, 128), (1, 128), (1, 64), (2, 128)])
 @pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn"])
-def test_backward_weight_grad_variants(kind, variant):
-    """dW on the f32 MFMA kernel (0) and the split GEMM with 64 x 64 (1) / 128 x 128 (2) tiles: all
-    within the same oracle bar (tower, CIN and cross weight gradients)."""
+def test_backward_weight_grad_variants(kind, variant, gz):
+    """dW on the f32 MFMA kernel (0) and the split GEMM with 64 x 64 (1) / 128 x 128 (2) tiles, the
+    CIN's generated-operand dW on 128 x 128 (wgrad_gz 128, the default) or 64 x 64 tiles: all within
+    the same oracle bar (tower, CIN and cross weight gradients)."""
     import rmx
     rmx.set_tuning("wgrad_s3", variant)
+    rmx.set_tuning("wgrad_gz", gz)
     try:
         test_backward_ids_matches_oracle(kind, 512, (400, 400, 400))
     finally:
         rmx.set_tuning("wgrad_s3", None)
+        rmx.set_tuning("wgrad_gz", None)
 
 
 @pytest.mark.gpu
