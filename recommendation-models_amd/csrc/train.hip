@@ -333,6 +333,69 @@ __global__ void cin_back_u_kernel(int64_t rows, int F, int Hp, const float* __re
   else out[r * ldo + h] = acc;
 }
 
+// Both contractions of dL/dz in one pass over it (one block per row r; the two kernels above read
+// the 4 x F x Hp bytes of each row twice):
+//   gx0[r][f] += sum_h gz[r][f*Hp + h] * up[r][h]   (f-row partials of VEC columns per thread,
+//                                                     then summed over the row in h order)
+//   out[r][h] (=, or += when accum) sum_f gz[r][f*Hp + h] * x0[r][f]   (G interleaved f-groups,
+//                                                     each in ascending f, then the groups in order)
+// Thread t owns columns [VEC hw, VEC hw + VEC) (hw = t % HW, HW = Hp / VEC) of f-group fg = t / HW.
+// gx0 is updated before out (layer 0: both are the x0 gradient).  Fixed orders: deterministic.
+template <int VEC>
+__global__ __launch_bounds__(256) void cin_back_fused_kernel(int64_t rows, int F, int Hp, const float* __restrict__ gz,
+                                                             int ldz, const float* __restrict__ up, int ldup,
+                                                             const float* __restrict__ x0, float* gx0, float* out,
+                                                             int ldo, int accum) {
+  extern __shared__ float cbf_sm[];
+  const int64_t r = blockIdx.x;
+  if (r >= rows) return;
+  const int HW = Hp / VEC, G = 256 / HW;
+  const int t = threadIdx.x, hw = t % HW, fg = t / HW;
+  float* redx = cbf_sm;           // [F][HW]
+  float* redu = cbf_sm + F * HW;  // [G][Hp]
+  if (fg < G) {
+    float uv[VEC], gacc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      uv[e] = up[r * ldup + hw * VEC + e];
+      gacc[e] = 0.f;
+    }
+    const float* g = gz + r * (int64_t)ldz + hw * VEC;
+    for (int f = fg; f < F; f += G) {
+      float v[VEC];
+      if constexpr (VEC == 4) {
+        const float4 q = *reinterpret_cast<const float4*>(g + (int64_t)f * Hp);
+        v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+      } else {
+        v[0] = g[(int64_t)f * Hp];
+      }
+      const float xf = x0[r * F + f];
+      float pd = 0.f;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        gacc[e] += v[e] * xf;
+        pd += v[e] * uv[e];
+      }
+      redx[f * HW + hw] = pd;
+    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) redu[fg * Hp + hw * VEC + e] = gacc[e];
+  }
+  __syncthreads();
+  if (t < F) {
+    float sx = 0.f;
+    for (int i = 0; i < HW; ++i) sx += redx[t * HW + i];
+    gx0[r * F + t] += sx;
+  }
+  __syncthreads();
+  for (int h = t; h < Hp; h += 256) {
+    float su = 0.f;
+    for (int q = 0; q < G; ++q) su += redu[q * Hp + h];
+    if (accum) out[r * ldo + h] += su;
+    else out[r * ldo + h] = su;
+  }
+}
+
 // ---- small / irregular fp32 GEMMs of the backward (replaces the library sgemm) ----
 // C[m][n] (= or += when ACC) sum_k A[m][k] * B(k, n), B(k, n) = B[k * ldb + n] (row-major K x N) or,
 // with BT, B[n * ldb + k] (row-major N x K).  64 x 64 block tiles, 4 waves of 32 x 32 (2 x 2 tiles of
@@ -1173,14 +1236,28 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
         // dL/dz for this chunk: gpre . C_l  [rows][F*Hp], on the split GEMM (C_l^T planes, row stride NTpad)
         if ((st = launch_cin_dz_s3(s, c, rows, gp, ldu, T.zb, c.NTpad))) return st;
         const int ldz = c.NTpad;
-        hipLaunchKernelGGL(cin_back_x0_kernel, dim3(rows), dim3(256), 0, s, (int64_t)rows, F, Hp, T.zb, ldz,
-                           up + r0 * ldup, ldup, T.gx0 + r0 * F);
-        RMX_HIP(hipGetLastError());
         // through u_{l-1} (layer 0: u_0 = x0, so into gx0 as well)
         float* gout = l == 0 ? T.gx0 + r0 * F : T.gu[gcur ^ 1] + r0 * m.cin_layers[l - 1].Npad;
-        hipLaunchKernelGGL(cin_back_u_kernel, dim3(nblk((int64_t)rows * Hp)), dim3(256), 0, s, (int64_t)rows, F, Hp,
-                           T.zb, ldz, T.x0 + r0 * F, gout, l == 0 ? F : m.cin_layers[l - 1].Npad, l == 0 ? 1 : 0);
-        RMX_HIP(hipGetLastError());
+        const int ldo = l == 0 ? F : m.cin_layers[l - 1].Npad;
+        // knob "cin_back_fused" (default 1): both contractions in one pass over dL/dz
+        const int vec = Hp % 4 == 0 ? 4 : 1;
+        const size_t smem = sizeof(float) * ((size_t)F * (Hp / vec) + (size_t)(256 / std::max(1, Hp / vec)) * Hp);
+        if (tuning_get("cin_back_fused", 1) && Hp / vec <= 256 && smem <= 64 * 1024) {
+          if (vec == 4)
+            hipLaunchKernelGGL(cin_back_fused_kernel<4>, dim3(rows), dim3(256), smem, s, (int64_t)rows, F, Hp, T.zb,
+                               ldz, up + r0 * ldup, ldup, T.x0 + r0 * F, T.gx0 + r0 * F, gout, ldo, l == 0 ? 1 : 0);
+          else
+            hipLaunchKernelGGL(cin_back_fused_kernel<1>, dim3(rows), dim3(256), smem, s, (int64_t)rows, F, Hp, T.zb,
+                               ldz, up + r0 * ldup, ldup, T.x0 + r0 * F, T.gx0 + r0 * F, gout, ldo, l == 0 ? 1 : 0);
+          RMX_HIP(hipGetLastError());
+        } else {
+          hipLaunchKernelGGL(cin_back_x0_kernel, dim3(rows), dim3(256), 0, s, (int64_t)rows, F, Hp, T.zb, ldz,
+                             up + r0 * ldup, ldup, T.gx0 + r0 * F);
+          RMX_HIP(hipGetLastError());
+          hipLaunchKernelGGL(cin_back_u_kernel, dim3(nblk((int64_t)rows * Hp)), dim3(256), 0, s, (int64_t)rows, F,
+                             Hp, T.zb, ldz, T.x0 + r0 * F, gout, ldo, l == 0 ? 1 : 0);
+          RMX_HIP(hipGetLastError());
+        }
       }
       gcur ^= 1;
     }
