@@ -85,6 +85,58 @@ int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L) {
   return RMX_OK;
 }
 
+// The split CIN's K order (k_gemm.hpp cin_chunk).  Chunks run over h-chunks hc (16 maps each), and
+// inside one over the fields f.  tri (layer 1, u = x0): z[f][h] = x0[f] x0[h] = z[h][f], so only
+// h <= f is kept -- fields f >= 16 hc -- with C[f,h] + C[h,f] as the weight (CINEncoder.scala:152
+// multiplies every ordered pair; the sum is the same bilinear form in one fp32 rounding per weight).
+// pair: an h-chunk with <= 8 live maps (H = 200: maps 192..199) takes fields f0, f0 + 1 in one chunk
+// (lane groups 0-1 and 2-3), so no MFMA runs on the zero half.
+std::vector<int> cin_chunk_map(int F, int Hp, bool tri) {
+  std::vector<int> m;
+  const int nhc = (Hp + 15) / 16;
+  for (int hc = 0; hc < nhc; ++hc) {
+    const bool pair = Hp - 16 * hc <= 8;
+    for (int f = tri ? 16 * hc : 0; f < F; f += pair ? 2 : 1) m.push_back(f | hc << 16 | (pair ? 1 << 30 : 0));
+  }
+  return m;
+}
+
+// C_l (H x F*Hp) -> [ncm][Npad][16] in the chunk-map order; element 4 g + q of chunk c is lane
+// group g's K value q (plain: z[f0][16 hc + 4 g + q]; pair: z[f0 + g / 2][16 hc + 4 (g % 2) + q])
+__global__ void pack_cin_map_kernel(const float* __restrict__ C, int F, int Hp, int H, int Npad, int tri,
+                                    const int* __restrict__ cmap, int64_t tot, float* __restrict__ Wm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= tot) return;
+  const int e = (int)(i & 15), g = e >> 2, q = e & 3;
+  const int64_t rest = i >> 4;
+  const int n = (int)(rest % Npad);
+  const int c = (int)(rest / Npad);
+  const int ent = cmap[c];
+  const int pr = (ent >> 30) & 1, hc = (ent >> 16) & 0x3fff;
+  const int f = (ent & 0xffff) + (pr ? g >> 1 : 0);
+  const int h = 16 * hc + (pr ? (g & 1) * 4 : g * 4) + q;
+  float v = 0.f;
+  if (n < H && f < F && h < Hp) {
+    const float* Cn = C + (int64_t)n * F * Hp;
+    if (!tri)
+      v = Cn[(int64_t)f * Hp + h];
+    else if (h < f)
+      v = Cn[(int64_t)f * Hp + h] + Cn[(int64_t)h * Hp + f];
+    else if (h == f)
+      v = Cn[(int64_t)f * Hp + f];
+  }
+  Wm[i] = v;
+}
+
+int launch_pack_cin_map(hipStream_t s, const float* mats, int F, CinLayer& L) {
+  const int64_t tot = (int64_t)L.ncm * L.Npad * 16;
+  if (tot <= 0) return RMX_OK;
+  hipLaunchKernelGGL(pack_cin_map_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, mats + L.w_off, F,
+                     L.Hp, L.H, L.Npad, L.tri, L.cmap, tot, L.Wm);
+  RMX_HIP(hipGetLastError());
+  return launch_pack_split3(s, L.Wm, L.ncm, L.Npad, L.W3);
+}
+
 
 // Npad of a tower layer of width N: a multiple of one block width NT*16 (NT from kNTs), chosen
 // to minimise padding (ties: the wider block).
@@ -256,6 +308,11 @@ int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, in
   }
   if (L.W3 && f32_split_enabled() && L.Npad == kS3BN) {
     p.Wp = reinterpret_cast<const float*>(L.W3);
+    if (L.map_on) {  // W3 packed in the chunk-map order (cin_chunk_map)
+      p.cmap = L.cmap;
+      p.ncmap = L.ncm;
+      p.K = L.ncm * 16;
+    }
     p.Kpad = round_up(p.K, 32);
     return launch_cin_s3(s, p);
   }

@@ -111,6 +111,8 @@ struct GemmArgs {
   // kCinOuter
   const float* u_prev;  // [M][ldu] previous CIN maps, nullptr for the first layer (u = x0)
   int ldu, XS, cin_first;
+  const int* cmap;  // kPrecS3 chunk map (CinLayer::cmap, staged in LDS), nullptr: chunk c16 = hc * F + f
+  int ncmap;
   const float* Wp;     // [Kpad/16][Npad][16]
   const float* bias;   // [Npad]
   float* C;            // kEpiRelu / kEpiCin (u_out, may be null): [M][ldc]
@@ -335,6 +337,10 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       }
       extra[r * XS + f] = v;
     }
+    // the chunk map after the x0 tile (read wave-uniformly in the MFMA loop: an LDS broadcast, no
+    // vector-memory op among the counted DMAs)
+    if (S3 && p.cmap)
+      for (int i = tid; i < p.ncmap; i += NTHR) reinterpret_cast<int*>(extra + BM * XS)[i] = p.cmap[i];
     __syncthreads();
   }
 
@@ -459,18 +465,20 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   int cur_hc[NU];
 #pragma unroll
   for (int h = 0; h < NU; ++h) cur_hc[h] = -1;
-  auto load_u = [&](int h, int hc) {
+  // key = hc * 2 + pair (cin_chunk): lane group g's maps 16 hc + 4 g .. (pair: 16 hc + 4 (g & 1) ..)
+  auto load_u = [&](int h, int key) {
+    const int col = (key >> 1) * 16 + ((key & 1) ? (g & 1) * 4 : g * 4);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       if (p.cin_first) {
-        uf[h][i] = *reinterpret_cast<const float4*>(extra + arow[i] * p.XS + hc * 16 + g * 4);
+        uf[h][i] = *reinterpret_cast<const float4*>(extra + arow[i] * p.XS + col);
       } else {
         const int m = m0 + arow[i];
-        uf[h][i] = m < M ? *reinterpret_cast<const float4*>(p.u_prev + (int64_t)m * p.ldu + hc * 16 + g * 4)
+        uf[h][i] = m < M ? *reinterpret_cast<const float4*>(p.u_prev + (int64_t)m * p.ldu + col)
                          : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    cur_hc[h] = hc;
+    cur_hc[h] = key;
   };
   // CIN A fragment of 16-wide chunk c16 (= hc * F + f): a = x0[row][f] * u[row][16 hc + 4 g ..]
   // c16 / F for the (wave-uniform) chunk index: q = floor(c16 * ceil(2^32 / F) / 2^32) is exact for
@@ -482,8 +490,24 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   auto div_f = [&](int c16) -> int {
     return RMX_CIN_DIVF ? (int)(((uint64_t)(uint32_t)c16 * fmagic) >> 32) : c16 / F;
   };
+  // chunk c16 -> this lane's field f and the u-slice key hc * 2 + pair.  With a chunk map (kPrecS3)
+  // the wave-uniform entry comes from LDS; a pair entry gives lane groups 2-3 the next field
+  const int* lmap = reinterpret_cast<const int*>(extra + BM * p.XS);
+  auto cin_chunk = [&](int c16, int& f, int& key) {
+    if (S3 && p.cmap) {
+      const int e = __builtin_amdgcn_readfirstlane(c16 * 16 < p.K ? lmap[c16] : 0);
+      const int pr = (e >> 30) & 1;
+      f = (e & 0xffff) + (pr ? (g >> 1) : 0);
+      key = ((e >> 16) & 0x3fff) * 2 + pr;
+    } else {
+      const int hc = div_f(c16);
+      f = c16 - hc * F;
+      key = hc * 2;
+    }
+  };
   auto cin_x0 = [&](int c16, float* xv) {  // the x0 scalars of chunk c16 (LDS)
-    const int f = c16 - div_f(c16) * F;
+    int f, key;
+    cin_chunk(c16, f, key);
 #pragma unroll
     for (int i = 0; i < MT; ++i) xv[i] = c16 * 16 < p.K ? extra[arow[i] * p.XS + f] : 0.f;
   };
@@ -493,8 +517,9 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       for (int i = 0; i < MT; ++i) a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       return;
     }
-    const int hc = div_f(c16);
-    if (hc != cur_hc[h]) load_u(h, hc);
+    int f, key;
+    cin_chunk(c16, f, key);
+    if (key != cur_hc[h]) load_u(h, key);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
       a[i] = f32x4{xv[i] * uf[h][i].x, xv[i] * uf[h][i].y, xv[i] * uf[h][i].z, xv[i] * uf[h][i].w};
@@ -1313,7 +1338,11 @@ int launch_cfg(hipStream_t s, GemmArgs& p) {
     lds += sizeof(int) * T::BM * p.ga.F;
     if (kWRing<T, AMODE, PREC> && EPI == kEpiRelu) lds += sizeof(float) * 4 * T::BM;  // first-order weight ring
   }
-  if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS;
+  if (AMODE == kCinOuter) lds += sizeof(float) * T::BM * p.XS + (p.cmap ? sizeof(int) * p.ncmap : 0);
+  if (p.cmap && (AMODE != kCinOuter || PREC != kPrecS3)) {
+    set_error("gemm: a CIN chunk map needs the split CIN kernel");
+    return RMX_E_INVALID;
+  }
   if (EPI != kEpiOutput) lds = std::max(lds, sizeof(float) * EpiGeom<T, SG::FLOATS>::FLOATS);
   lds = std::max(lds, sizeof(float) * T::WN * T::BM);  // row-reduction partials
   if (lds > 160 * 1024) {

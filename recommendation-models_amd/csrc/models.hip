@@ -336,6 +336,17 @@ int model_build(rmx_model& m) {
   for (auto& c : m.cin_layers) {
     if ((st = dev_alloc(&c.W, (size_t)c.Hp_pad * m.F * c.Npad))) return st;
     if ((st = dev_alloc_bf16(&c.W3, split3_elems(c.Hp_pad / kChunk * m.F, c.Npad)))) return st;
+    {  // the split kernel's K order (k_gemm.hip cin_chunk_map): at most Hp_pad / 16 * F chunks
+      c.tri = &c == &m.cin_layers.front() ? 1 : 0;
+      const std::vector<int> map = cin_chunk_map(m.F, c.Hp, c.tri != 0);
+      c.ncm = (int)map.size();
+      if (hipMalloc(&c.cmap, sizeof(int) * std::max<size_t>(map.size(), 1)) != hipSuccess) {
+        set_error("out of device memory (CIN chunk map)");
+        return RMX_E_NOMEM;
+      }
+      RMX_HIP(hipMemcpy(c.cmap, map.data(), sizeof(int) * map.size(), hipMemcpyHostToDevice));
+      if ((st = dev_alloc(&c.Wm, (size_t)c.ncm * c.Npad * 16))) return st;
+    }
     c.KTpad = round_up(c.H, kChunk);
     c.NTpad = round_up(m.F * c.Hp, 208);
     if ((st = dev_alloc(&c.WT, (size_t)c.KTpad * c.NTpad))) return st;
@@ -428,6 +439,8 @@ void model_release(rmx_model& m) {
   for (auto& c : m.cin_layers) {
     dev_free(c.W);
     dev_free(c.W3);
+    dev_free(c.Wm);
+    dev_free(c.cmap);
     dev_free(c.WT);
     dev_free(c.WT3);
     dev_free(c.b);
@@ -524,7 +537,11 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
   }
   for (auto& c : m.cin_layers) {
     if ((st = launch_pack_cin(s, m.mats_dev, m.F, c))) return st;
-    if (c.W3 && (st = launch_pack_split3(s, c.W, c.Hp_pad / kChunk * m.F, c.Npad, c.W3))) return st;
+    // knob "cin_map" (default 1): the split planes in the chunk-map order (layer 1 folded to h <= f,
+    // paired fields on a half-live h-chunk); 0: the plain hc * F + f order of c.W
+    c.map_on = c.W3 && c.cmap && tuning_get("cin_map", 1) != 0 ? 1 : 0;
+    if (c.map_on && (st = launch_pack_cin_map(s, m.mats_dev, m.F, c))) return st;
+    if (c.W3 && !c.map_on && (st = launch_pack_split3(s, c.W, c.Hp_pad / kChunk * m.F, c.Npad, c.W3))) return st;
     if (c.WT3 && (st = launch_pack_cin_t(s, m.mats_dev, m.F, c))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.b_off, c.H, c.Npad, c.b))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.wo_off, c.H, c.Npad, c.wo))) return st;

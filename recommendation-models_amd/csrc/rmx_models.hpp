@@ -54,7 +54,14 @@ struct CinLayer {
   float* W = nullptr;
   float* b = nullptr;
   float* wo = nullptr;  // [Npad] slice of the output Linear for this layer's pooled maps
-  bf16_t* W3 = nullptr;  // kPrecS3 planes of W (k_gemm_s3.hip)
+  bf16_t* W3 = nullptr;  // kPrecS3 planes of W (k_gemm_s3.hip), in the chunk-map K order when map_on
+  // kPrecS3 K-chunk map (k_gemm.hpp cin_chunk): one entry f0 | hc << 16 | pair << 30 per 16-wide
+  // chunk.  Layer 1 keeps only the h <= f half of its symmetric z = x0 (x) x0 (folded weights
+  // C[f,h] + C[h,f]), and an h-chunk with <= 8 live maps carries two fields per chunk.
+  int* cmap = nullptr;
+  float* Wm = nullptr;  // fp32 [ncm][Npad][16] mapped weights (the split planes' source)
+  int ncm = 0, tri = 0;
+  int map_on = 0;       // W3 was packed in the mapped order (knob "cin_map" at set_mats)
   // backward dL/dz = gpre C_l on the split GEMM: C_l^T packed [KTpad/16][NTpad][16] (K = H, N = F Hp)
   float* WT = nullptr;
   bf16_t* WT3 = nullptr;
@@ -212,6 +219,8 @@ int shard_destroy(rmx_shard* sh);
 
 // kernels specific to the interaction encoders
 int launch_pack_cin(hipStream_t s, const float* mats, int F, CinLayer& L);
+std::vector<int> cin_chunk_map(int F, int Hp, bool tri);
+int launch_pack_cin_map(hipStream_t s, const float* mats, int F, CinLayer& L);
 int launch_pack_cin_t(hipStream_t s, const float* mats_dev, int F, CinLayer& c);
 int launch_cin_dz_s3(hipStream_t s, const CinLayer& c, int rows, const float* gpre, int ldg, float* dz, int ldz);
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,

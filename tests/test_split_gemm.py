@@ -35,7 +35,8 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense": 5, "s3_cin": 4, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None}.items():
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense": 5, "s3_cin": 4, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None,
+                 "cin_map": 1}.items():
         rmx.set_tuning(k, v)
 
 
@@ -197,6 +198,42 @@ def test_split_headline_xdeepfm_full_batch(ctx):
     m.forward_ids(table, B, ids_dev, out)
     ctx.sync()
     assert np.array_equal(out.numpy(), got)
+
+
+@pytest.mark.parametrize("Fm,cin", [(39, (200, 196, 208)), (24, (200, 200)), (17, (208,)), (40, (200,))])
+@pytest.mark.parametrize("B", [1, 300])
+def test_cin_chunk_map_matches_oracle_and_plain_order(ctx, Fm, cin, B):
+    """The split CIN's K order (k_gemm.hip cin_chunk_map, knob cin_map, packed at setMats): layer 1 on
+    the h <= f half of its symmetric z = x0 (x) x0 with folded weights C[f,h] + C[h,f], and an h-chunk
+    with <= 8 live maps (H_prev = 200, 196; F = 24, 40, 39 in layer 1) carrying two fields.  Same
+    bilinear forms (CINEncoder.scala:152-155), different fp32 rounding: both orders against the fp64
+    oracle at the north-star bar, and against each other."""
+    V = 50000
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    ids = oc.gen_ids(SEED_IDS, 7, B, Fm, V).astype(np.int64)
+    w, e = oc.gather(wt, et, 1, ids)
+    index = np.repeat(np.arange(B, dtype=np.int64), Fm)
+    res = {}
+    for on in (1, 0):
+        rmx.set_tuning("cin_map", on)
+        m = rmx.XDeepFM(V, Fm, K, [400, 400], list(cin))
+        mats = m.initMats(SEED_MATS)
+        m.setMats(mats)
+        m.setBias(0.01)
+        table = rmx.EmbeddingTable(ctx, V, K)
+        table.fill_synthetic(SEED_TAB)
+        ids_dev = rmx.DeviceArray(ctx, B * Fm, np.int32)
+        rmx.gen_ids(ctx, SEED_IDS, 7, B, Fm, V, ids_dev)
+        out = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(table, B, ids_dev, out)
+        ctx.sync()
+        res[on] = out.numpy().copy()
+    ref = oc.forward(oc.make_model(oc.XDEEPFM, Fm, K, fc=(400, 400), cin=cin), B, index, np.array([0.01], np.float32),
+                     w, e, mats, 1)
+    e_map, e_plain = float(np.abs(res[1] - ref).max()), float(np.abs(res[0] - ref).max())
+    print("F=%d cin=%s B=%d max|p - p_fp64|: map %.3g, plain %.3g" % (Fm, cin, B, e_map, e_plain))
+    assert e_map <= TOL and e_plain <= TOL
+    assert e_map <= 2 * e_plain + 1e-7
 
 
 def test_split_host_arrays_path(ctx):
