@@ -308,10 +308,16 @@ int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, in
   }
   if (L.W3 && f32_split_enabled() && L.Npad == kS3BN) {
     p.Wp = reinterpret_cast<const float*>(L.W3);
+    p.cin_pair_hc = -1;
     if (L.map_on) {  // W3 packed in the chunk-map order (cin_chunk_map)
-      p.cmap = L.cmap;
-      p.ncmap = L.ncm;
       p.K = L.ncm * 16;
+      if (L.tri || tuning_get("cin_map_lds", 0)) {  // the triangle: entries staged in LDS
+        p.cmap = L.cmap;
+        p.ncmap = L.ncm;
+      } else {  // decoded in closed form (k_gemm.hpp cin_chunk)
+        const int last = (L.Hp + 15) / 16 - 1;
+        if (L.Hp - 16 * last <= 8) p.cin_pair_hc = last;
+      }
     }
     p.Kpad = round_up(p.K, 32);
     return launch_cin_s3(s, p);

@@ -113,6 +113,7 @@ struct GemmArgs {
   int ldu, XS, cin_first;
   const int* cmap;  // kPrecS3 chunk map (CinLayer::cmap, staged in LDS), nullptr: chunk c16 = hc * F + f
   int ncmap;
+  int cin_pair_hc;  // kPrecS3 without cmap: the h-chunk whose chunks carry two fields (-1: none)
   const float* Wp;     // [Kpad/16][Npad][16]
   const float* bias;   // [Npad]
   float* C;            // kEpiRelu / kEpiCin (u_out, may be null): [M][ldc]
@@ -500,9 +501,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       f = (e & 0xffff) + (pr ? (g >> 1) : 0);
       key = ((e >> 16) & 0x3fff) * 2 + pr;
     } else {
+      // the same order in closed form for a map without the triangle: h-chunk hc = c16 / F plain,
+      // except a paired last h-chunk p.cin_pair_hc (its chunk j carries fields 2j, 2j + 1)
       const int hc = div_f(c16);
-      f = c16 - hc * F;
-      key = hc * 2;
+      const int j = c16 - hc * F;
+      const int pr = S3 && hc == p.cin_pair_hc ? 1 : 0;
+      f = pr ? 2 * j + (g >> 1) : j;
+      key = hc * 2 + pr;
     }
   };
   auto cin_x0 = [&](int c16, float* xv) {  // the x0 scalars of chunk c16 (LDS)

@@ -9,9 +9,10 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_train.
 tail -3 $O/t2.log
 timeout -k 10 300 python bench.py --workload xdeepfm --no-cpu-baseline > $O/b_on.json 2> $O/b_on.err || exit 1
 timeout -k 10 300 python bench.py --workload xdeepfm --no-cpu-baseline --set cin_map=0 > $O/b_off.json 2> $O/b_off.err || exit 1
+timeout -k 10 300 python bench.py --workload xdeepfm --no-cpu-baseline --set cin_map_lds=1 > $O/b_lds.json 2> $O/b_lds.err || exit 1
 python3 - $O <<'PY'
 import json, sys
-for n in ("b_on", "b_off"):
+for n in ("b_on", "b_off", "b_lds"):
     d = json.load(open(sys.argv[1] + "/" + n + ".json"))
     print(n, d["value"], d["ms_per_step"], {k: v["avg_ms"] for k, v in d["stages"].items()})
 PY
