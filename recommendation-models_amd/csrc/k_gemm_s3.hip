@@ -223,13 +223,14 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 
 // CIN layer, kPrecS3 (H <= 208): only the B planes go through LDS (39 KiB per K step); the A
 // operand x0[f] * u[h] is formed in fp32 registers and split there.  Knob "s3_cin":
-//   0  MT = 1, 2-deep LDS-DMA ring;  1  MT = 1, 3-deep ring;  2  MT = 2, 2-deep ring (CIN 200^3 at
-//   B = 16,384, layer 2: 3.73 ms vs 4.60 (MT = 1, 8 waves) and 6.69 on the f32 MFMA engine);
-//   3  MT = 1, register-staged double buffer;  4 (default) MT = 1, 16 waves (4 per SIMD), 2-deep ring:
-//   twice the B-fragment LDS reads of 2, hidden by the extra waves (B = 16,384: layer 1 0.827 ->
-//   0.795 ms, layers 2+ 3.037 -> 3.022 ms).
+//   0  MT = 1, 2-deep LDS-DMA ring;  1  MT = 1, 3-deep ring;  2 (default)  MT = 2, 8 waves, 2-deep
+//   ring (CIN 200^3 at B = 16,384, layer 2: 3.73 ms vs 4.60 (MT = 1, 8 waves) and 6.69 on the f32
+//   MFMA engine);  3  MT = 1, register-staged double buffer;  4  MT = 1, 16 waves (4 per SIMD), 2-deep
+//   ring: twice the B-fragment LDS reads of 2, hidden by the extra waves on some boxes (layers 2+
+//   3.022 vs 3.037 ms) but not on others: with the chunk map, 3 boxes gave layers 2+ 3.04-3.07 ms on
+//   2 against 3.25-3.27 on 4 (xDeepFM 2.29 -> 2.42 M examples/s).
 int launch_cin_s3(hipStream_t s, GemmArgs& p) {
-  const int var = tuning_get("s3_cin", 4);
+  const int var = tuning_get("s3_cin", 2);
   p.prio = tuning_get("gemm_prio", 0);
   if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   if (var == 2) {

@@ -35,7 +35,7 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     yield
-    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense": 5, "s3_cin": 4, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None,
+    for k, v in {"f32_split": 1, "s3_tower": 1, "s3_dense": 5, "s3_cin": None, "fm_fuse": 1, "fo_fuse": 2, "fm_y1": 2, "tower_variant": None,
                  "cin_map": 1}.items():
         rmx.set_tuning(k, v)
 
