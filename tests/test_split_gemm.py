@@ -200,7 +200,8 @@ def test_split_headline_xdeepfm_full_batch(ctx):
     assert np.array_equal(out.numpy(), got)
 
 
-@pytest.mark.parametrize("Fm,cin", [(39, (200, 196, 208)), (24, (200, 200)), (17, (208,)), (40, (200,))])
+@pytest.mark.parametrize("Fm,cin", [(39, (200, 196, 208)), (24, (200, 200)), (17, (208,)), (40, (200,)),
+                                    (39, (150, 200)), (13, (200, 200))])
 @pytest.mark.parametrize("B", [1, 300])
 def test_cin_chunk_map_matches_oracle_and_plain_order(ctx, Fm, cin, B):
     """The split CIN's K order (k_gemm.hip cin_chunk_map, knob cin_map, packed at setMats): layer 1 on
