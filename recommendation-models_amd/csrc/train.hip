@@ -612,9 +612,13 @@ struct WgZ {
 };
 
 // TT x TT output tile per block (TT = 64: 2 x 2 waves of 32 x 32; TT = 128: 2 x 4 waves of 64 x 32,
-// halving the L2 reads and LDS fragment reads per output), LDS [buf][A | X][plane][col][32 rows] bf16
-template <int TT, bool GZ = false>
-__global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows, int N, int K,
+// halving the L2 reads and LDS fragment reads per output), LDS [buf][A | X][plane][col][32 rows] bf16.
+// SB (knob "wgrad_sb"): one LDS buffer (48 KiB at TT = 128) and a second barrier per chunk, so two
+// blocks share a CU (4 waves per SIMD): one block's MFMAs run while the other splits and stores its
+// next chunk, where the double-buffered block's waves all reach that phase together.  Same chunks,
+// same MFMA order per output: bitwise the same gradients.
+template <int TT, bool GZ = false, bool SB = false>
+__global__ __launch_bounds__(TT == 64 ? 256 : 512, SB ? 4 : 1) void wgrad_s3_kernel(int rows, int N, int K,
                                                                         const float* __restrict__ A, int lda,
                                                                         const float* __restrict__ X, int ldx,
                                                                         int rows_per_slice, int tiles,
@@ -671,13 +675,16 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows
     for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int cur) {
     if constexpr (RMX_WGRAD_DIAG & 2) return;
-    wg_bf16x8 fa[TI][3], fx[TJ][3];
-#pragma unroll
-    for (int t = 0; t < TI; ++t) {
+    // SB: an A fragment is read just before its MFMAs (fewer live VGPRs for 4 waves per SIMD)
+    wg_bf16x8 fa[SB ? 1 : TI][3], fx[TJ][3];
+    auto lda_frag = [&](int t, wg_bf16x8* f) {
       const int ca = wi * TI * 16 + t * 16 + r16;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) fa[t][pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
-    }
+      for (int pl = 0; pl < 3; ++pl) f[pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+    };
+    if constexpr (!SB)
+#pragma unroll
+      for (int t = 0; t < TI; ++t) lda_frag(t, fa[t]);
 #pragma unroll
     for (int t = 0; t < TJ; ++t) {
       const int cx = wj * TJ * 16 + t * 16 + r16;
@@ -685,34 +692,51 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512) void wgrad_s3_kernel(int rows
       for (int pl = 0; pl < 3; ++pl) fx[t][pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
     }
 #pragma unroll
-    for (int a = 0; a < TI; ++a)
+    for (int ai = 0; ai < TI; ++ai) {
+      if constexpr (SB) lda_frag(ai, fa[0]);
+      const int a = SB ? 0 : ai;
 #pragma unroll
       for (int b = 0; b < TJ; ++b) {
-        f32x4 d = acc[a][b];
+        f32x4 d = acc[ai][b];
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fx[b][1], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][2], fx[b][0], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][2], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][1], fx[b][0], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][1], d, 0, 0, 0);
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][0], d, 0, 0, 0);
+        acc[ai][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a][0], fx[b][0], d, 0, 0, 0);
       }
+    }
   };
   if (nch > 0) {
     gload(0, a0, x0);
     sstore(0, a0, x0);
   }
   if (nch > 1) gload(1, a0, x0);
-  if (nch > 2) gload(2, a1, x1);
+  if (!SB && nch > 2) gload(2, a1, x1);
   __syncthreads();
-  for (int c = 0; c < nch; c += 2) {
+  if constexpr (SB) {
+    // one register set (no spills at 4 waves per SIMD): chunk c + 2's loads fly during chunk c + 1's
+    // MFMAs; the partner block's MFMAs cover this block's split / store phase
+    for (int c = 0; c < nch; ++c) {
+      compute(0);
+      __syncthreads();  // every wave is done reading the one buffer
+      if (c + 1 < nch) {
+        if (!(RMX_WGRAD_DIAG & 1)) sstore(0, a0, x0);
+        if (!(RMX_WGRAD_DIAG & 4) && c + 2 < nch) gload(c + 2, a0, x0);
+      }
+      __syncthreads();
+    }
+  }
+  constexpr int B1 = 1;  // the odd chunks' buffer
+  for (int c = 0; !SB && c < nch; c += 2) {
     compute(0);  // chunk c (even) in buffer 0
     if (c + 1 < nch) {
-      if (!(RMX_WGRAD_DIAG & 1)) sstore(1, a0, x0);
+      if (!(RMX_WGRAD_DIAG & 1)) sstore(B1, a0, x0);
       if (!(RMX_WGRAD_DIAG & 4) && c + 3 < nch) gload(c + 3, a0, x0);
     }
     __syncthreads();
     if (c + 1 >= nch) break;
-    compute(1);  // chunk c + 1 in buffer 1
+    compute(B1);  // chunk c + 1
     if (c + 2 < nch) {
       if (!(RMX_WGRAD_DIAG & 1)) sstore(0, a1, x1);
       if (!(RMX_WGRAD_DIAG & 4) && c + 4 < nch) gload(c + 4, a1, x1);
@@ -785,17 +809,18 @@ int ensure_part(TrainState& T, int64_t n) {
 
 // out (N x K row-major) (= or +=) A[rows][lda](N columns)^T . X[rows][ldx](K columns); zg (split GEMM
 // only, wgrad_z_ok): X is the CIN outer product generated from x0 / up instead of read
-bool wgrad_z_ok() { return f32_split_enabled() && tuning_get("wgrad_s3", 1) != 0; }
+bool wgrad_z_ok() { return f32_split_enabled() && tuning_get("wgrad_s3", 2) != 0; }
 
 int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, int lda, const float* X, int ldx,
           float* out, bool accum, const WgZ* zg = nullptr) {
   if (rows <= 0 || N <= 0 || K <= 0) return RMX_OK;
   // knob "wgrad_s3": 0 = the f32 MFMA kernel, 1 = split GEMM with 64 x 64 tiles, 2 = 128 x 128 tiles
-  int var = f32_split_enabled() ? tuning_get("wgrad_s3", 1) : 0;
+  // default 2 since the single-buffered kernel (wgrad_sb): DeepFM training at B = 65,536 2.25 ->
+  // 2.12 ms per step (on the double-buffered kernel the tower's dW, K <= 624, ran faster on 64 x 64)
+  int var = f32_split_enabled() ? tuning_get("wgrad_s3", 2) : 0;
   // the generated CIN operand (N = H, K = F * Hp, rows = B * k) runs on the 128 x 128 tiles unless
-  // "wgrad_gz" = 64: xDeepFM training at B = 4,096: CIN backward 14.88 -> 14.00 ms (the tower's dW,
-  // K <= 624, stays faster on 64 x 64 tiles)
-  if (zg && var == 1 && tuning_get("wgrad_gz", 128) == 128) var = 2;
+  // "wgrad_gz" = 64: xDeepFM training at B = 4,096: CIN backward 14.88 -> 14.00 ms
+  if (zg && var != 0) var = tuning_get("wgrad_gz", 128) == 64 ? 1 : 2;
   if (zg && !var) {
     set_error("wgrad: the generated CIN operand needs the split GEMM");
     return RMX_E_INVALID;
@@ -810,7 +835,17 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   const int rps = round_up((rows + S - 1) / S, var ? kWgR : 16);
   int st = ensure_part(T, (int64_t)S * N * K);
   if (st) return st;
-  if (var == 2) {
+  // knob "wgrad_sb": 1 (default) the single-buffered kernel on the 128 x 128 tiles (two blocks per CU),
+  // 2 also on the 64 x 64 tiles, 0 off
+  if (var == 2 && tuning_get("wgrad_sb", 1) != 0) {
+    const size_t lds = sizeof(wg_bf16x8) * 2 * 3 * 128 * 4;  // 48 KiB
+    if (zg)
+      hipLaunchKernelGGL((wgrad_s3_kernel<128, true, true>), dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X,
+                         ldx, rps, tiles, T.part2, z);
+    else
+      hipLaunchKernelGGL((wgrad_s3_kernel<128, false, true>), dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda,
+                         X, ldx, rps, tiles, T.part2, z);
+  } else if (var == 2) {
     const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * 128 * 4;
     static bool attr = false;
     if (!attr) {
@@ -825,6 +860,14 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
                          rps, tiles, T.part2, z);
     else
       hipLaunchKernelGGL((wgrad_s3_kernel<128, false>), dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X,
+                         ldx, rps, tiles, T.part2, z);
+  } else if (var && tuning_get("wgrad_sb", 1) == 2) {  // 2: the 64 x 64 tiles single-buffered too
+    const size_t lds = sizeof(wg_bf16x8) * 2 * 3 * 64 * 4;
+    if (zg)
+      hipLaunchKernelGGL((wgrad_s3_kernel<64, true, true>), dim3(tiles * S), dim3(256), lds, s, rows, N, K, A, lda, X,
+                         ldx, rps, tiles, T.part2, z);
+    else
+      hipLaunchKernelGGL((wgrad_s3_kernel<64, false, true>), dim3(tiles * S), dim3(256), lds, s, rows, N, K, A, lda, X,
                          ldx, rps, tiles, T.part2, z);
   } else if (var) {
     const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * 64 * 4;

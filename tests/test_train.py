@@ -238,6 +238,49 @@ def test_backward_weight_grad_variants(kind, variant, gz):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,gz", [("deepfm", 128), ("xdeepfm", 128), ("xdeepfm", 64), ("dcn", 128)])
+@pytest.mark.parametrize("B", [512, 4099])
+def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
+    """dW on the single-buffered split kernel (wgrad_sb 1: 128 x 128 tiles, two blocks per CU; 2: the
+    64 x 64 tiles too) stages the same chunks and issues the same MFMA sequence per output as the
+    double-buffered one (wgrad_sb 0): every gradient is bitwise equal, tower / CIN / cross dW alike."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K, fc = 20_000, 39, 16, (400, 400, 400)
+    m = _gpu_model(rmx, kind, V, F, K, fc)
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 11, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(7).random(B) > 0.7).astype(np.float32))
+    ml = len(mats)
+
+    def grads():
+        out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, ml, 1)]
+        m.backward_ids(t, B, ids, targets, *out)
+        ctx.sync()
+        return [o.numpy().copy() for o in out]
+
+    rmx.set_tuning("wgrad_gz", gz)
+    try:
+        res = {}
+        for sb in (0, 1, 2):
+            rmx.set_tuning("wgrad_sb", sb)
+            res[sb] = grads()
+    finally:
+        rmx.set_tuning("wgrad_sb", None)
+        rmx.set_tuning("wgrad_gz", None)
+    for sb in (1, 2):
+        for a, b in zip(res[0], res[sb]):
+            assert np.array_equal(a, b)
+    assert np.isfinite(res[1][3]).all() and np.abs(res[1][3]).max() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", GPU_KINDS)
 def test_backward_host_arrays_in_place(kind):
     """L-A RecModel.backward: the caller's arrays come back holding the gradients."""
