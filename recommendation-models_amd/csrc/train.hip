@@ -757,6 +757,135 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512, SB ? 4 : 1) void wgrad_s3_ker
     }
 }
 
+// The same single-buffered split dW on a 208 x 128 tile (knob "wgrad_nk", default on for the CIN): n (the dPre /
+// gpre columns) in 13 MFMA tiles, so N = 400 pads to 416 and the CIN's N = 200 to 208 instead of 512 /
+// 256 on the square 128 tiles (19-28 % fewer MFMAs, fewer blocks); k in 128.  8 waves, wave w owns
+// k tile w and all 13 n tiles.  Staging items (col, row octet): [208 A cols | 128 X cols] x 4 octets,
+// up to 3 per thread.  Per output the chunks and the 6 MFMAs run in the same order as the 128 x 128
+// kernel; only the row-slice split S (a function of the tile count) can differ.
+constexpr int kNkN = 208, kNkK = 128, kNkItems = (kNkN + kNkK) * 4, kNkPer = (kNkItems + 511) / 512;
+template <bool GZ>
+__global__ __launch_bounds__(512, 4) void wgrad_nk_kernel(int rows, int N, int K, const float* __restrict__ A, int lda,
+                                                          const float* __restrict__ X, int ldx, int rows_per_slice,
+                                                          int tiles, float* __restrict__ part, WgZ zg) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) wg_bf16x8 wlds[];
+  // LDS [A planes 3][208 cols][4 slots] then [X planes 3][128 cols][4 slots]
+  auto LA = [&](int pl) { return wlds + pl * kNkN * 4; };
+  auto LX = [&](int pl) { return wlds + 3 * kNkN * 4 + pl * kNkK * 4; };
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = blockIdx.x, xcd = bid & 7, idx = bid >> 3;
+  const int slice = (idx / tiles) * 8 + xcd, tile = idx % tiles;
+  const int ntn = (N + kNkN - 1) / kNkN;
+  const int n0 = (tile % ntn) * kNkN, k0 = (tile / ntn) * kNkK;
+  const int r_begin = slice * rows_per_slice;
+  const int r_end = min(rows, r_begin + rows_per_slice);
+  const int nch = r_end > r_begin ? (r_end - r_begin + kWgR - 1) / kWgR : 0;
+  // this thread's staging items, packed col | h << 8 | op << 10 | ok << 11 (few live VGPRs), and (GZ)
+  // the (f, h) of an X column
+  int it[kNkPer], it_zf[kNkPer], it_zh[kNkPer];
+#pragma unroll
+  for (int q = 0; q < kNkPer; ++q) {
+    const int i = tid + q * 512;
+    const bool a = i < kNkN * 4;
+    const int j = a ? i : i - kNkN * 4;
+    const int col = a ? j % kNkN : j % kNkK, h = a ? j / kNkN : j / kNkK;
+    const bool ok = i < kNkItems && (a ? n0 + col < N : k0 + col < K);
+    it[q] = col | h << 8 | (a ? 0 : 1) << 10 | (ok ? 1 : 0) << 11;
+    const int kk = k0 + col;
+    it_zf[q] = GZ && !a ? kk / zg.Hp : 0;
+    it_zh[q] = GZ && !a ? kk - it_zf[q] * zg.Hp : 0;
+  }
+  float v[kNkPer][8];
+  auto gload = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < kNkPer; ++q) {
+      const int col = it[q] & 255, h = (it[q] >> 8) & 3, op = (it[q] >> 10) & 1;
+      const bool ok = (it[q] >> 11) & 1;
+      const int r0 = r_begin + c * kWgR + 8 * h;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = r0 + e;
+        float x = 0.f;
+        if (ok && r < r_end) {
+          if (op == 0)
+            x = A[(int64_t)r * lda + n0 + col];
+          else if constexpr (GZ)
+            x = zg.x0[(int64_t)r * zg.F + it_zf[q]] * zg.up[(int64_t)r * zg.ldup + it_zh[q]];
+          else
+            x = X[(int64_t)r * ldx + k0 + col];
+        }
+        v[q][e] = x;
+      }
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int q = 0; q < kNkPer; ++q) {
+      if (tid + q * 512 >= kNkItems) continue;
+      const int col = it[q] & 255, o = col * 4 + wg_slot(col, (it[q] >> 8) & 3);
+      wg_bf16x8 p0, p1, p2;
+      wg_split(v[q], p0, p1, p2);
+      if (((it[q] >> 10) & 1) == 0) {
+        LA(0)[o] = p0;
+        LA(1)[o] = p1;
+        LA(2)[o] = p2;
+      } else {
+        LX(0)[o] = p0;
+        LX(1)[o] = p1;
+        LX(2)[o] = p2;
+      }
+    }
+  };
+  const int g = lane >> 4, r16 = lane & 15;
+  f32x4 acc[13];
+#pragma unroll
+  for (int a = 0; a < 13; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&]() {
+    wg_bf16x8 fx[3], fa[3];
+    const int cx = wid * 16 + r16;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) fx[pl] = LX(pl)[cx * 4 + wg_slot(cx, g)];
+#pragma unroll
+    for (int a = 0; a < 13; ++a) {
+      const int ca = a * 16 + r16;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fa[pl] = LA(pl)[ca * 4 + wg_slot(ca, g)];
+      f32x4 d = acc[a];
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fx[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[2], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[1], d, 0, 0, 0);
+      acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[0], d, 0, 0, 0);
+    }
+  };
+  if (nch > 0) {
+    gload(0);
+    sstore();
+  }
+  if (nch > 1) gload(1);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    compute();
+    __syncthreads();  // every wave is done reading the one buffer
+    if (c + 1 < nch) {
+      sstore();
+      if (c + 2 < nch) gload(c + 2);
+    }
+    __syncthreads();
+  }
+  float* out = part + (int64_t)slice * N * K;
+  const int k = k0 + wid * 16 + r16;
+#pragma unroll
+  for (int a = 0; a < 13; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + a * 16 + 4 * g + r;
+      if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][r];
+    }
+}
+
 // out[i] (=, or += when accum) sum_s part[s][i]: a block covers 64 outputs with 4 wave-groups, group
 // q summing slices q, q + 4, ...; the 4 group sums are added in fixed order (deterministic).
 __global__ __launch_bounds__(256) void slice_reduce_kernel(int S, int64_t n, const float* __restrict__ part,
@@ -826,8 +955,13 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     return RMX_E_INVALID;
   }
   const WgZ z = zg ? *zg : WgZ{};
+  // knob "wgrad_nk": the 208 x 128 tile in place of the 128 x 128 one -- 1 (default) for the CIN's
+  // generated operand (xDeepFM training at B = 4,096: CIN backward 9.49 -> 8.73 ms), 2 for every dW
+  // (the tower's 400 x 400 / 624 dW ran slower on it: DeepFM training 1.95 -> 2.19 ms), 0 off
+  const int nkv = tuning_get("wgrad_nk", 1);
+  const bool nk = var == 2 && (nkv == 2 || (nkv == 1 && zg));
   const int TT = var == 2 ? 128 : kWgT;
-  const int tiles = ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
+  const int tiles = nk ? ((N + kNkN - 1) / kNkN) * ((K + kNkK - 1) / kNkK) : ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
   // slices of ~1024 rows (one slice of both operands, (N + K) * 4 KiB, stays in an XCD's 4 MiB L2),
   // at least ~1024 blocks in flight, S a multiple of the 8 XCDs
   int S = std::max((rows + 1023) / 1024, std::min((1024 + tiles - 1) / tiles, std::max(1, rows / 64)));
@@ -837,7 +971,23 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   if (st) return st;
   // knob "wgrad_sb": 1 (default) the single-buffered kernel on the 128 x 128 tiles (two blocks per CU),
   // 2 also on the 64 x 64 tiles, 0 off
-  if (var == 2 && tuning_get("wgrad_sb", 1) != 0) {
+  if (nk) {
+    const size_t lds = sizeof(wg_bf16x8) * 3 * (kNkN + kNkK) * 4;  // 63 KiB: two blocks per CU
+    static bool attr = false;
+    if (!attr) {
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_nk_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_nk_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      attr = true;
+    }
+    if (zg)
+      hipLaunchKernelGGL(wgrad_nk_kernel<true>, dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx, rps,
+                         tiles, T.part2, z);
+    else
+      hipLaunchKernelGGL(wgrad_nk_kernel<false>, dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx, rps,
+                         tiles, T.part2, z);
+  } else if (var == 2 && tuning_get("wgrad_sb", 1) != 0) {
     const size_t lds = sizeof(wg_bf16x8) * 2 * 3 * 128 * 4;  // 48 KiB
     if (zg)
       hipLaunchKernelGGL((wgrad_s3_kernel<128, true, true>), dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X,

@@ -266,14 +266,23 @@ def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
         return [o.numpy().copy() for o in out]
 
     rmx.set_tuning("wgrad_gz", gz)
+    rmx.set_tuning("wgrad_nk", 0)
     try:
         res = {}
         for sb in (0, 1, 2):
             rmx.set_tuning("wgrad_sb", sb)
             res[sb] = grads()
+        # the 208 x 128 tile (every dW, then the default: the CIN's only): same bar as the others
+        rmx.set_tuning("wgrad_sb", None)
+        for nk in (2, 1):
+            rmx.set_tuning("wgrad_nk", nk)
+            g_nk = grads()
+            for a, b in zip(res[0], g_nk):
+                assert np.abs(a - b).max() <= 2e-5 * max(np.abs(a).max(), 1e-30)
     finally:
         rmx.set_tuning("wgrad_sb", None)
         rmx.set_tuning("wgrad_gz", None)
+        rmx.set_tuning("wgrad_nk", None)
     for sb in (1, 2):
         for a, b in zip(res[0], res[sb]):
             assert np.array_equal(a, b)
