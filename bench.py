@@ -9,9 +9,14 @@ set; successive steps walk the set.  The default line also carries an "models.xd
 Other workloads: xdeepfm, deepfm_sharded (configs[3]), dcn_bf16 / pnn_bf16 (configs[4]),
 lr_plumbing (configs[0]: LIBSVM text -> parse -> LR predict -> AUC), deepfm_train / xdeepfm_train.
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank owns a replica of the 1M-row
-table and its own batches (replicas only: the V = 1M forward has no exchange step), so
-scaling is weak and value = sum of all ranks' examples / max rank time.
+Multi-GPU: one process per GPU.  `bench.py --gpus N` launches its N ranks itself (fresh child
+processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT; the launching parent makes
+no GPU call and imports nothing of librmx), or runs as one rank of an external
+`torch.distributed.run` (WORLD_SIZE set).  Every rank owns a replica of the 1M-row table and its own
+batches (replicas only: the V = 1M forward has no exchange step), so scaling is weak and value = sum
+of all ranks' examples / max rank time; deepfm_sharded hash-shards the 100M-row table over the ranks
+(RCCL exchange per batch).  At N > 1 every rank checks its own bench rows against the oracle after
+timing (`parity_check_ranks`).
 
 Prints ONE JSON line (rank 0).  Only the cpu_baseline leg touches oracle/ (the checker).
 """
@@ -378,20 +383,13 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     if sharded:
         # configs[3]: table hash-sharded over the ranks, RCCL exchange per batch
         # RCCL prints its version banner on fd 1 at init; keep stdout for the one JSON line
-        sys.stdout.flush()
-        saved_fd1 = os.dup(1)
-        os.dup2(2, 1)
-        try:
+        with stdout_to_stderr():
             uid = rmx.comm_unique_id() if rank == 0 else None
             if dist:
                 box = [uid]
                 dist.broadcast_object_list(box, src=0)
                 uid = box[0]
             table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
-        finally:
-            sys.stdout.flush()
-            os.dup2(saved_fd1, 1)
-            os.close(saved_fd1)
         table.set_dedupe(False if args.no_dedupe else "auto")
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
@@ -602,15 +600,94 @@ def config_of(workload, r, world, zipf):
         "parallelism": ("hashshard%d_rccl" % world) if workload == "deepfm_sharded" else "replicas%d" % world}
 
 
+class stdout_to_stderr:
+    """fd 1 -> fd 2 for a block (library banners: gloo, RCCL), so stdout carries only the JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, script=None, grace_s=10.0):
+    """`--gpus N` without an external launcher: start N fresh rank processes of `script` (this file)
+    with the torch.distributed env (RANK, LOCAL_RANK = rank, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a
+    free MASTER_PORT), relay rank 0's stdout (the one JSON line) and return the job's exit status: 0
+    when every rank exits 0, else the first failing rank's status, after the other ranks are stopped
+    (SIGTERM, then SIGKILL after grace_s).  Only child processes are started (no exec) and this
+    process touches no GPU: each rank initialises its own device."""
+    import signal
+    import subprocess
+    import threading
+    script = os.path.abspath(script or __file__)
+    port = _free_port()
+    procs, out0 = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+
+    def pump():  # rank 0's stdout, read while it runs (a full pipe would block the rank)
+        for line in procs[0].stdout:
+            out0.append(line)
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    status = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                sys.stderr.write("bench.py: rank %d exited with status %d; stopping the other ranks\n" % (r, rc))
+                for q in live:
+                    procs[q].send_signal(signal.SIGTERM)
+                t_end = time.time() + grace_s
+                for q in list(live):
+                    try:
+                        procs[q].wait(max(0.1, t_end - time.time()))
+                    except subprocess.TimeoutExpired:
+                        procs[q].kill()
+                        procs[q].wait()
+                live.clear()
+                break
+        time.sleep(0.05)
+    th.join(5.0)
+    for line in out0:
+        sys.stdout.write(line.decode(errors="replace"))
+    sys.stdout.flush()
+    return status
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # this process is the launcher only: the ranks are fresh children (no GPU call here)
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist  # CPU (gloo) barrier / max only: the GPU work is librmx
-        dist.init_process_group("gloo")
+        with stdout_to_stderr():  # gloo prints a connection banner on fd 1: stdout is the JSON line
+            dist.init_process_group("gloo")
     import rmx
     for kv in filter(None, args.set.split(",")):
         k_, v_ = kv.split("=")
@@ -624,7 +701,11 @@ def main():
         import torch
         ndev = max(1, torch.cuda.device_count())
     if args.workload == "deepfm_sharded" and world > ndev:
-        raise SystemExit("deepfm_sharded needs one GPU per rank (RCCL rejects ranks sharing a GPU)")
+        sys.stderr.write("bench.py: deepfm_sharded needs one GPU per rank (%d ranks, %d GPU(s) visible): RCCL "
+                         "rejects ranks sharing a GPU\n" % (world, ndev))
+        if dist:
+            dist.destroy_process_group()
+        raise SystemExit(3)
     rmx.set_device(local % ndev)
     ctx = rmx.default_context()
 
@@ -647,8 +728,18 @@ def main():
             # out holds the predict loop's probabilities of the whole rank-0 row set
             cpu["parity_check"] = parity_check(args.workload, r["out"], 0)
         if companion:
-            cpu2 = cpu_baseline_sweep("xdeepfm", max(3.0, args.cpu_seconds * 0.5), short=True)
+            cpu2 = cpu_baseline_sweep("xdeepfm", max(3.0, args.cpu_seconds * 0.5))
             cpu2["parity_check"] = parity_check("xdeepfm", companion["out"], 0)
+
+    # N > 1: every rank checks rows of its own bench set against the oracle (after timing), rank 0
+    # reports them all
+    parity_ranks = None
+    if world > 1 and not train and args.workload != "lr_plumbing" and not args.zipf:
+        pc = parity_check(args.workload, r["out"], rank * r["nrows"], vocab=r["Vw"])
+        if companion:
+            pc = {"deepfm": pc, "xdeepfm": parity_check("xdeepfm", companion["out"], rank * companion["nrows"])}
+        parity_ranks = [None] * world
+        dist.all_gather_object(parity_ranks, pc)
 
     if rank == 0:
         line = {
@@ -658,6 +749,8 @@ def main():
             "value": round(r["value"], 1),
             "unit": "examples/s",
             "n_gpus": world,
+            **({"gpus_visible": ndev, "note_ranks": "%d ranks share %d visible GPU(s) (rehearsal, not a "
+                                                    "scaling point)" % (world, ndev)} if world > ndev else {}),
             "steps": args.steps,
             "warmup": args.warmup,
             **({"settle": {"ms": args.settle_ms, "untimed_steps": r["settle_steps"]}} if "settle_steps" in r else {}),
@@ -676,6 +769,9 @@ def main():
             **({"exchange": r["exchange"]} if "exchange" in r else {}),
             "roofline": r["roofline"],
             "cpu_baseline": cpu,
+            **({"parity_check_ranks": parity_ranks,
+                "parity_ok": all(p["ok"] if "ok" in p else all(q["ok"] for q in p.values()) for p in parity_ranks)}
+               if parity_ranks else {}),
             **({"predict_auc": r["predict_auc"]} if r.get("predict_auc") else {}),
             **({"auc": r["auc"]} if "auc" in r else {}),
             "stages": r["stages"],

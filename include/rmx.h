@@ -178,6 +178,7 @@ int rmx_table_upload(rmx_table* t, const float* weights, const float* embedding,
 /* Deterministic synthetic fill, bit-identical to oracle/orc_gen_table (U(-0.05, 0.05)). */
 int rmx_table_fill_synthetic(rmx_table* t, uint64_t seed);
 int64_t rmx_table_rows(const rmx_table* t);
+int rmx_table_embedding_dim(const rmx_table* t);  /* k of the table (-1: NULL) */
 /* Device pointers of the table (for debugging/parity only; elements of the table's dtype). */
 int rmx_table_device_ptrs(const rmx_table* t, void** d_weights, void** d_embedding);
 
@@ -232,7 +233,8 @@ int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32
 /* -------------------------------------------------------- sharded table ---- */
 /* Hash-sharded table over nranks processes, one GPU each (BASELINE.json configs[3]): replaces
  * the column-range-partitioned Angel PS matrices and their sparse pulls (ParRecModel.scala:74-105,
- * :165-199).  owner(id) = id mod nranks, local row = id div nranks.  One exchange per batch over
+ * :165-199).  owner(id) = p(id) mod nranks, local row = p(id) div nranks, p the keyed permutation of
+ * rmx_shard_set_owner_hash (default key RMX_OWNER_HASH_DEFAULT).  One exchange per batch over
  * RCCL (grouped send/recv = all-to-all over xGMI): ids to owners, rows back.
  * rmx_comm_unique_id: rank 0 creates the RCCL id (RMX_UNIQUE_ID_BYTES bytes) and the caller
  * broadcasts it (e.g. torch.distributed / MPI / Spark broadcast).  unique_id == NULL creates a
@@ -246,12 +248,17 @@ int rmx_shard_destroy(rmx_shard* sh);
 /* Owned rows from the same generator as rmx_table_fill_synthetic (bit-identical rows). */
 int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);
 int64_t rmx_shard_local_rows(const rmx_shard* sh);
-/* Owner function (before rmx_shard_fill_synthetic; every rank the same key): key 0 = id mod nranks
- * (default); else owner = p(id) mod nranks, local row = p(id) div nranks with p a keyed pseudo-random
- * permutation of [0, num_rows) (4-round Feistel, cycle-walked), so strided or clustered id spaces
- * spread evenly.  rmx_shard_owner_of: the rank owning id (-1 if out of range). */
+/* Owner function (before rmx_shard_fill_synthetic; every rank the same key): owner = p(id) mod
+ * nranks, local row = p(id) div nranks with p a keyed pseudo-random permutation of [0, num_rows)
+ * (4-round Feistel, cycle-walked), so strided or clustered id spaces spread evenly (the table is
+ * HASH-sharded by default: key RMX_OWNER_HASH_DEFAULT); key 0 = the identity, owner = id mod nranks.
+ * rmx_shard_owner_of: the rank owning id (-1 if out of range).  rmx_owner_hash: the same function
+ * without a shard (host only): the owner of id, *local_row (nullable) its row there; -1 if id is
+ * outside [0, num_rows) or the arguments are bad. */
+#define RMX_OWNER_HASH_DEFAULT 0x5EED5A4D0C7A11EDULL
 int rmx_shard_set_owner_hash(rmx_shard* sh, uint64_t key);
 int64_t rmx_shard_owner_of(const rmx_shard* sh, int64_t id);
+int64_t rmx_owner_hash(uint64_t key, int64_t num_rows, int nranks, int64_t id, int64_t* local_row);
 /* Step 0 of the exchange: send each DISTINCT id of the batch once, as
  * ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull; results are identical.
  * on: 0 off, 1 on, 2 auto (default: off at one rank; else on for a batch, then off for the next 63

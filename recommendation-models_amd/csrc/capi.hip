@@ -312,6 +312,7 @@ extern "C" int rmx_table_destroy(rmx_table* t) {
 
 extern "C" int64_t rmx_table_rows(const rmx_table* t) { return t ? t->V : -1; }
 extern "C" int rmx_table_dtype(const rmx_table* t) { return t ? t->dtype : -1; }
+extern "C" int rmx_table_embedding_dim(const rmx_table* t) { return t ? t->k : -1; }
 
 extern "C" int rmx_table_device_ptrs(const rmx_table* t, void** w, void** e) {
   CHECK_ARG(t, "rmx_table_device_ptrs: NULL");

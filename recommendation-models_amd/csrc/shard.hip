@@ -5,10 +5,11 @@
 // that are sharded over GPUs (BASELINE.json configs[3]: V = 100M over 8 x MI355X).
 //
 // Partitioning: owner(id) = p(id) mod N, local row = p(id) div N, a bijection [0, V) -> [N] x [ceil(V/N)].
-// p = identity by default (Criteo ids are feature hashes, so modulo partitioning balances), or
-// (rmx_shard_set_owner_hash) a keyed pseudo-random permutation of [0, V): a 4-round Feistel network
-// on the smallest even-width bit domain >= V, cycle-walked back into [0, V) -- strided or clustered
-// real id spaces then spread evenly over the owners, with no lookup table.
+// p = a keyed pseudo-random permutation of [0, V) (default key RMX_OWNER_HASH_DEFAULT, or
+// rmx_shard_set_owner_hash): a 4-round Feistel network on the smallest even-width bit domain >= V,
+// cycle-walked back into [0, V) -- strided or clustered real id spaces spread evenly over the owners,
+// with no lookup table (BASELINE.json north_star: the table HASH-shards).  Key 0 = identity
+// (owner = id mod N).
 // One exchange step per batch on the caller's stream:
 //   0. dedupe  : (rmx_shard_set_dedupe: off / on / auto, default auto) the batch's distinct ids, as
 //                ParRecModel.distinctIntIndices (ParRecModel.scala:337-345) before the pull: an
@@ -93,12 +94,13 @@ struct rmx_shard {
   rmx_group* group = nullptr;           // in-process exchange group (or null)
   std::unique_ptr<rmx::Transport> tr;   // RCCL or group transport (null: loopback)
   int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
-  uint64_t owner_key = 0;               // 0: owner = id mod N; else the Feistel key of p (set_owner_hash)
+  uint64_t owner_key = RMX_OWNER_HASH_DEFAULT;  // Feistel key of p (set_owner_hash); 0: owner = id mod N
   bool filled = false;                  // rows written (the owner function is then fixed)
   int rs = 0;                           // row stride in floats: [emb k | w | pad], one 128-B line at k < 32
   std::vector<float*> part;             // partitions held here: [rows_per][rs] (loopback: N)
   // per-batch buffers (grow only)
   int64_t cap_send = 0, cap_recv = 0;
+  int64_t cap_slot[2] = {0, 0};         // ids each pull slot's buffers hold (grown one slot at a time)
   int32_t* counts = nullptr;            // [4N]: send counts, recv counts, cursors, scratch
   int32_t* h_counts = nullptr;          // pinned host [2N]
   int32_t* send_ids = nullptr;          // [nnz] local rows, bucketed by owner
@@ -205,21 +207,25 @@ __device__ __host__ __forceinline__ int64_t owner_perm(int64_t id, const OwnerPe
   return y;
 }
 
-OwnerPerm owner_perm_of(const rmx_shard& sh) {
+OwnerPerm owner_perm_of(uint64_t key, int64_t V) {
   OwnerPerm op;
-  op.key = sh.owner_key;
-  op.V = sh.V;
+  op.key = key;
+  op.V = V;
   int b = 1;
-  while ((int64_t(1) << b) < sh.V) ++b;
+  while ((int64_t(1) << b) < V) ++b;
   op.h = std::max(1, (b + 1) / 2);
   return op;
 }
+OwnerPerm owner_perm_of(const rmx_shard& sh) { return owner_perm_of(sh.owner_key, sh.V); }
 
 __device__ __forceinline__ int route_owner(const int32_t* ids, int64_t n, int64_t nnz, int N, int* loc,
                                            const OwnerPerm& op) {
   if (n >= nnz) return -1;
   const int id = ids[n];
-  if (id < 0) return -1;  // an empty hash-set slot (dedupe)
+  // an empty hash-set slot (dedupe, -1), or an id outside [0, V): no owner.  (The cycle walk of the
+  // keyed permutation ends only for ids inside [0, V): an id's cycle re-enters [0, V) only if it
+  // started there.)
+  if (id < 0 || id >= op.V) return -1;
   const int64_t p = owner_perm(id, op, false);
   *loc = (int)(p / N);
   return (int)(p % N);
@@ -292,10 +298,13 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nn
 #pragma unroll
   for (int u = 0; u < kRoutePer; ++u) {
     const int rk = wave_reserve(own[u], h);
+    const int64_t n = base + u * kRouteThreads + threadIdx.x;
     if (own[u] >= 0) {
       const int slot = start[own[u]] + rk;
       send_ids[slot] = loc[u];
-      perm[base + u * kRouteThreads + threadIdx.x] = slot;
+      perm[n] = slot;
+    } else if (n < nnz) {
+      perm[n] = 0;  // no owner: a defined in-range slot, never an out-of-bounds read downstream
     }
   }
 }
@@ -328,6 +337,42 @@ __global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, const int3
   const float* row = part + (int64_t)rows[t] * rs;
   for (int j = 0; j < k; ++j) out_emb[t * k + j] = row[j];
   out_w[t] = row[k];
+}
+
+// One rank, no dedupe: routing is the identity (every id is this rank's own, bucket order = batch
+// order), so the count / scan / scatter passes are skipped and one pass gathers the rows in batch
+// order: perm[n] = n, rows[n] = partition row p(ids[n]).  Same row layout and lane map as
+// owner_gather_kernel; an id outside [0, V) gets a zero row (no read).
+__global__ __launch_bounds__(256) void own_gather_kernel(int64_t n, int k, int rs, const int32_t* __restrict__ ids,
+                                                        const float* __restrict__ part, float* __restrict__ out_emb,
+                                                        float* __restrict__ out_w, int32_t* __restrict__ perm,
+                                                        OwnerPerm op) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 16 && rs == 32) {
+    const int64_t i = t >> 3;
+    const int c = (int)(t & 7);
+    if (i >= n || c > 5) return;
+    if (c == 5) {
+      perm[i] = (int32_t)i;
+      return;
+    }
+    const int id = ids[i];
+    const bool ok = id >= 0 && id < op.V;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) v = reinterpret_cast<const float4*>(part)[owner_perm(id, op, false) * 8 + c];
+    if (c < 4)
+      reinterpret_cast<float4*>(out_emb)[i * 4 + c] = v;
+    else
+      out_w[i] = v.x;
+    return;
+  }
+  if (t >= n) return;
+  const int id = ids[t];
+  const bool ok = id >= 0 && id < op.V;
+  const float* row = part + (ok ? owner_perm(id, op, false) : 0) * rs;
+  for (int j = 0; j < k; ++j) out_emb[t * k + j] = ok ? row[j] : 0.f;
+  out_w[t] = ok ? row[k] : 0.f;
+  perm[t] = (int32_t)t;
 }
 
 // step 0: insert ids[n] into the hash set; hslot[n] = its slot (first inserter claims an empty one)
@@ -402,22 +447,33 @@ int realloc_dev(T** p, int64_t n) {
   return RMX_OK;
 }
 
-// [nnz]-sized buffers of this rank's batch
-int ensure_batch(rmx_shard& sh, int64_t nnz) {
-  if (nnz <= sh.cap_send) return RMX_OK;
+// [nnz]-sized buffers of this rank's batch: the exchange's scratch, and pull slot `slot` only.
+// The other slot may hold a pull its forward has not consumed (or is still reading): it is never
+// touched here.  The slot being grown has no pending pull (rmx_shard_pull refuses one), and the
+// device sync retires any forward still reading its old buffers.
+int ensure_batch(rmx_shard& sh, int64_t nnz, int slot) {
+  if (nnz <= sh.cap_send && nnz <= sh.cap_slot[slot]) return RMX_OK;
   RMX_HIP(hipDeviceSynchronize());  // in-flight work on any stream may still use the old buffers
   int st;
-  int64_t hc = 1024;
-  while (hc < 2 * nnz) hc <<= 1;
-  if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.hslot, nnz)) || (st = realloc_dev(&sh.hkeys, hc)) ||
-      (st = realloc_dev(&sh.hvals, hc)))
-    return st;
-  for (int q = 0; q < 2; ++q)
-    if ((st = realloc_dev(&sh.perm_s[q], nnz)) || (st = realloc_dev(&sh.recv_emb_s[q], nnz * sh.k)) ||
-        (st = realloc_dev(&sh.recv_w_s[q], nnz)))
+  if (nnz > sh.cap_send) {
+    int64_t hc = 1024;
+    while (hc < 2 * nnz) hc <<= 1;
+    if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.hslot, nnz)) ||
+        (st = realloc_dev(&sh.hkeys, hc)) || (st = realloc_dev(&sh.hvals, hc))) {
+      sh.cap_send = sh.cap_hash = 0;
       return st;
-  sh.cap_send = nnz;
-  sh.cap_hash = hc;
+    }
+    sh.cap_send = nnz;
+    sh.cap_hash = hc;
+  }
+  if (nnz > sh.cap_slot[slot]) {
+    if ((st = realloc_dev(&sh.perm_s[slot], nnz)) || (st = realloc_dev(&sh.recv_emb_s[slot], nnz * sh.k)) ||
+        (st = realloc_dev(&sh.recv_w_s[slot], nnz))) {
+      sh.cap_slot[slot] = 0;
+      return st;
+    }
+    sh.cap_slot[slot] = nnz;
+  }
   return RMX_OK;
 }
 
@@ -435,9 +491,12 @@ int ensure_tiles(rmx_shard& sh, int64_t tiles) {
 int ensure_recv(rmx_shard& sh, int64_t n) {
   if (n <= sh.cap_recv) return RMX_OK;
   int st;
+  RMX_HIP(hipDeviceSynchronize());  // a peer's copy of the old rows may still be in flight
   if ((st = realloc_dev(&sh.recv_ids, n)) || (st = realloc_dev(&sh.send_emb, n * sh.k)) ||
-      (st = realloc_dev(&sh.send_w, n)))
+      (st = realloc_dev(&sh.send_w, n))) {
+    sh.cap_recv = 0;
     return st;
+  }
   sh.cap_recv = n;
   return RMX_OK;
 }
@@ -734,50 +793,79 @@ void dedupe_auto(rmx_shard& sh, bool dd, int64_t nnz) {
 
 // Steps 1-5 of the exchange: fills pull slot `slot` (sh.perm / sh.recv_emb / sh.recv_w) for this
 // rank's batch.
-int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot = 0) {
-  const int N = sh.N, k = sh.k;
+// Step 0-1 (dedupe + route) of this rank's batch into pull slot `slot`; *dd = dedupe ran.
+int shard_route(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot, bool* dd_out) {
+  const int N = sh.N;
   int st;
-  if ((st = ensure_batch(sh, nnz))) return st;
+  *dd_out = false;
+  if ((st = ensure_batch(sh, nnz, slot))) return st;
   sh.perm = sh.perm_s[slot];
   sh.recv_emb = sh.recv_emb_s[slot];
   sh.recv_w = sh.recv_w_s[slot];
-  int32_t* cnt = sh.counts;           // [N] send counts
-  int32_t* rcnt = sh.counts + N;      // [N] recv counts
+  int32_t* cnt = sh.counts;  // [N] send counts
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
   // (auto at one rank: off -- no link traffic to save, the duplicates' rows are local reads)
   const bool dd = nnz > 0 && (sh.dedupe == 1 || (sh.dedupe == 2 && sh.N > 1 && sh.dedupe_skip == 0));
+  *dd_out = dd;
   int64_t rn = nnz;
-  if (nnz > 0) {
-    // route the batch's ids, or (dedupe) the distinct ids held by the hash set's slots
-    const int32_t* rids = d_ids;
-    int32_t* rslot = sh.perm;
-    if (dd) {
-      RMX_HIP(hipMemsetAsync(sh.hkeys, 0xFF, sizeof(int32_t) * sh.cap_hash, s));
-      hipLaunchKernelGGL(dedupe_insert_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, d_ids,
-                         (uint32_t)(sh.cap_hash - 1), 64 - __builtin_ctzll((unsigned long long)sh.cap_hash),
-                         sh.hkeys, sh.hslot);
-      RMX_HIP(hipGetLastError());
-      rids = sh.hkeys;
-      rn = sh.cap_hash;
-      rslot = sh.hvals;
-    }
-    const int nb = (int)((rn + kRouteTile - 1) / kRouteTile);
-    if ((st = ensure_tiles(sh, nb))) return st;
-    const OwnerPerm op = owner_perm_of(sh);
-    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, sh.bcnt, op);
+  if (nnz <= 0) return RMX_OK;
+  // route the batch's ids, or (dedupe) the distinct ids held by the hash set's slots
+  const int32_t* rids = d_ids;
+  int32_t* rslot = sh.perm;
+  if (dd) {
+    RMX_HIP(hipMemsetAsync(sh.hkeys, 0xFF, sizeof(int32_t) * sh.cap_hash, s));
+    hipLaunchKernelGGL(dedupe_insert_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, d_ids,
+                       (uint32_t)(sh.cap_hash - 1), 64 - __builtin_ctzll((unsigned long long)sh.cap_hash),
+                       sh.hkeys, sh.hslot);
     RMX_HIP(hipGetLastError());
-    hipLaunchKernelGGL(route_scan_kernel, dim3(N), dim3(1024), 0, s, nb, sh.bcnt, cnt);
-    RMX_HIP(hipGetLastError());
-    hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, cnt, sh.bcnt,
-                       sh.send_ids, rslot, op);
-    RMX_HIP(hipGetLastError());
-    if (dd) {
-      hipLaunchKernelGGL(dedupe_perm_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, sh.hslot,
-                         sh.hvals, sh.perm);
-      RMX_HIP(hipGetLastError());
-    }
+    rids = sh.hkeys;
+    rn = sh.cap_hash;
+    rslot = sh.hvals;
   }
+  const int nb = (int)((rn + kRouteTile - 1) / kRouteTile);
+  if ((st = ensure_tiles(sh, nb))) return st;
+  const OwnerPerm op = owner_perm_of(sh);
+  hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, sh.bcnt, op);
+  RMX_HIP(hipGetLastError());
+  hipLaunchKernelGGL(route_scan_kernel, dim3(N), dim3(1024), 0, s, nb, sh.bcnt, cnt);
+  RMX_HIP(hipGetLastError());
+  hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, cnt, sh.bcnt,
+                     sh.send_ids, rslot, op);
+  RMX_HIP(hipGetLastError());
+  if (dd) {
+    hipLaunchKernelGGL(dedupe_perm_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, sh.hslot,
+                       sh.hvals, sh.perm);
+    RMX_HIP(hipGetLastError());
+  }
+  return RMX_OK;
+}
+
+// Steps 1-5 of the exchange: fills pull slot `slot` (sh.perm / sh.recv_emb / sh.recv_w) for this
+// rank's batch.
+int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot = 0) {
+  const int N = sh.N, k = sh.k;
+  int st;
+  bool dd = false;
+  if (N == 1 && !sh.loopback && sh.dedupe != 1) {
+    // one rank, no dedupe (auto is off at one rank): identity routing, one gather pass, no host sync
+    if ((st = ensure_batch(sh, nnz, slot))) return st;
+    sh.perm = sh.perm_s[slot];
+    sh.recv_emb = sh.recv_emb_s[slot];
+    sh.recv_w = sh.recv_w_s[slot];
+    sh.last_sent = nnz;
+    sh.last_sent_dev = false;
+    if (nnz <= 0) return RMX_OK;
+    const int64_t threads = (k == 16 && sh.rs == 32) ? nnz * 8 : nnz;
+    hipLaunchKernelGGL(own_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, nnz, k, sh.rs,
+                       d_ids, sh.part[0], sh.recv_emb, sh.recv_w, sh.perm, owner_perm_of(sh));
+    RMX_HIP(hipGetLastError());
+    return RMX_OK;
+  }
+  const int route_err = shard_route(sh, s, nnz, d_ids, slot, &dd);
+  int32_t* cnt = sh.counts;       // [N] send counts
+  int32_t* rcnt = sh.counts + N;  // [N] recv counts
   if (sh.loopback) {
+    if (route_err) return route_err;
     // loopback: partition o serves bucket o in place
     RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * N, hipMemcpyDeviceToHost, s));
     RMX_HIP(hipStreamSynchronize(s));
@@ -796,28 +884,45 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     return RMX_OK;
   }
   if (N == 1) {
+    if (route_err) return route_err;
     // one rank: no exchange.  The bucket is this rank's own; its size (nnz, or the distinct ids
     // when deduplicating) stays on the device and bounds the gather there -- no host sync.
     sh.last_sent = nnz;
     sh.last_sent_dev = dd;
     dedupe_auto(sh, dd, nnz);
-    return launch_owner_gather(s, nnz, k, sh.rs, sh.send_ids, sh.part[0], sh.recv_emb, sh.recv_w,
-                               dd ? cnt : nullptr);
+    // (the device count also bounds a batch holding ids outside [0, V), which route no row)
+    return launch_owner_gather(s, nnz, k, sh.rs, sh.send_ids, sh.part[0], sh.recv_emb, sh.recv_w, cnt);
   }
   Transport& tr = *sh.tr;
   const int me = sh.rank;
+  // From here every rank passes all three start() / end() rendezvous, also after a local error
+  // (the route above, a transport call, the owner-side buffers): a failed rank posts no more ops,
+  // so its peers fail the receives they expected from it with RMX_E_COMM at once, instead of
+  // waiting out the group timeout that would break the group for good.  (RCCL has no such
+  // recovery: a peer's unmatched receive there waits for the communicator's abort.)
+  int err = route_err;
+  auto keep = [&](int e) {
+    if (e && err == RMX_OK) err = e;
+    return err == RMX_OK;
+  };
   // 2. counts: one int to every peer, then one D2H of the 2N counts (the only host sync: the
   //    transport needs host-side message sizes); this rank's own entry is a local copy
-  if ((st = tr.start())) return st;
-  for (int o = 0; o < N; ++o) {
+  keep(tr.start());
+  for (int o = 0; o < N && err == RMX_OK; ++o) {
     if (o == me) continue;
-    if ((st = tr.send(cnt + o, sizeof(int32_t), o, s)) || (st = tr.recv(rcnt + o, sizeof(int32_t), o, s))) return st;
+    if (keep(tr.send(cnt + o, sizeof(int32_t), o, s))) keep(tr.recv(rcnt + o, sizeof(int32_t), o, s));
   }
-  if ((st = tr.end(s))) return st;
-  RMX_HIP(hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * 2 * N, hipMemcpyDeviceToHost, s));
-  RMX_HIP(hipStreamSynchronize(s));
-  const int32_t* hc = sh.h_counts;
+  keep(tr.end(s));
+  int32_t* hc = sh.h_counts;
   int32_t* hr = sh.h_counts + N;
+  if (err == RMX_OK) {
+    if (hipMemcpyAsync(sh.h_counts, cnt, sizeof(int32_t) * 2 * N, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      set_error("shard exchange: the counts' device-to-host copy failed");
+      keep(RMX_E_HIP);
+    }
+  }
+  if (err != RMX_OK) std::fill(sh.h_counts, sh.h_counts + 2 * N, 0);  // post nothing from here
   hr[me] = hc[me];
   sh.last_sent = 0;
   sh.last_sent_dev = false;
@@ -831,36 +936,31 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     if (o != me) npeer += hr[o];
     if (o < me) so_me += hc[o];
   }
-  if ((st = ensure_recv(sh, npeer))) return st;
+  if (err == RMX_OK) keep(ensure_recv(sh, npeer));
   // 3. ids to owners
-  if ((st = tr.start())) return st;
-  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += (o == me ? 0 : hr[o]), ++o) {
+  keep(tr.start());
+  for (int64_t o = 0, so = 0, ro = 0; o < N && err == RMX_OK; so += hc[o], ro += (o == me ? 0 : hr[o]), ++o) {
     if (o == me) continue;
-    if (hc[o] && (st = tr.send(sh.send_ids + so, sizeof(int32_t) * hc[o], (int)o, s))) return st;
-    if (hr[o] && (st = tr.recv(sh.recv_ids + ro, sizeof(int32_t) * hr[o], (int)o, s))) return st;
+    if (hc[o]) keep(tr.send(sh.send_ids + so, sizeof(int32_t) * hc[o], (int)o, s));
+    if (hr[o] && err == RMX_OK) keep(tr.recv(sh.recv_ids + ro, sizeof(int32_t) * hr[o], (int)o, s));
   }
-  if ((st = tr.end(s))) return st;
+  keep(tr.end(s));
   // 4. owner gather: every peer's request in one launch, then the own bucket
-  if ((st = launch_owner_gather(s, npeer, k, sh.rs, sh.recv_ids, sh.part[0], sh.send_emb, sh.send_w))) return st;
-  if ((st = launch_owner_gather(s, hc[me], k, sh.rs, sh.send_ids + so_me, sh.part[0], sh.recv_emb + so_me * k,
-                                sh.recv_w + so_me)))
-    return st;
+  if (err == RMX_OK) keep(launch_owner_gather(s, npeer, k, sh.rs, sh.recv_ids, sh.part[0], sh.send_emb, sh.send_w));
+  if (err == RMX_OK)
+    keep(launch_owner_gather(s, hc[me], k, sh.rs, sh.send_ids + so_me, sh.part[0], sh.recv_emb + so_me * k,
+                             sh.recv_w + so_me));
   // 5. rows back, into the requester's bucket order
-  if ((st = tr.start())) return st;
-  for (int64_t o = 0, so = 0, ro = 0; o < N; so += hc[o], ro += (o == me ? 0 : hr[o]), ++o) {
+  keep(tr.start());
+  for (int64_t o = 0, so = 0, ro = 0; o < N && err == RMX_OK; so += hc[o], ro += (o == me ? 0 : hr[o]), ++o) {
     if (o == me) continue;
-    if (hr[o]) {
-      if ((st = tr.send(sh.send_emb + ro * k, sizeof(float) * hr[o] * k, (int)o, s)) ||
-          (st = tr.send(sh.send_w + ro, sizeof(float) * hr[o], (int)o, s)))
-        return st;
-    }
-    if (hc[o]) {
-      if ((st = tr.recv(sh.recv_emb + so * k, sizeof(float) * hc[o] * k, (int)o, s)) ||
-          (st = tr.recv(sh.recv_w + so, sizeof(float) * hc[o], (int)o, s)))
-        return st;
-    }
+    if (hr[o] && keep(tr.send(sh.send_emb + ro * k, sizeof(float) * hr[o] * k, (int)o, s)))
+      keep(tr.send(sh.send_w + ro, sizeof(float) * hr[o], (int)o, s));
+    if (hc[o] && err == RMX_OK && keep(tr.recv(sh.recv_emb + so * k, sizeof(float) * hc[o] * k, (int)o, s)))
+      keep(tr.recv(sh.recv_w + so, sizeof(float) * hc[o], (int)o, s));
   }
-  return tr.end(s);
+  keep(tr.end(s));
+  return err;
 }
 
 }  // namespace rmx
@@ -946,6 +1046,13 @@ extern "C" int rmx_shard_set_owner_hash(rmx_shard* sh, uint64_t key) {
 extern "C" int64_t rmx_shard_owner_of(const rmx_shard* sh, int64_t id) {
   if (!sh || id < 0 || id >= sh->V) return -1;
   return owner_perm(id, owner_perm_of(*sh), false) % sh->N;
+}
+
+extern "C" int64_t rmx_owner_hash(uint64_t key, int64_t num_rows, int nranks, int64_t id, int64_t* local_row) {
+  if (num_rows < 1 || num_rows >= (int64_t(1) << 31) || nranks < 1 || id < 0 || id >= num_rows) return -1;
+  const int64_t p = owner_perm(id, owner_perm_of(key, num_rows), false);
+  if (local_row) *local_row = p / nranks;
+  return p % nranks;
 }
 
 extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {

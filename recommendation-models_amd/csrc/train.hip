@@ -395,10 +395,10 @@ __global__ __launch_bounds__(256) void cin_back_fused_kernel(int64_t rows, int F
     for (int e = 0; e < VEC; ++e) redu[fg * Hp + hw * VEC + e] = gacc[e];
   }
   __syncthreads();
-  if (t < F) {
+  for (int f = t; f < F; f += 256) {  // every field, also F > 256
     float sx = 0.f;
-    for (int i = 0; i < HW; ++i) sx += redx[t * HW + i];
-    gx0[r * F + t] += sx;
+    for (int i = 0; i < HW; ++i) sx += redx[f * HW + i];
+    gx0[r * F + f] += sx;
   }
   __syncthreads();
   for (int h = t; h < Hp; h += 256) {

@@ -56,10 +56,23 @@ static void throw_status(JNIEnv* env, int st) {
   if (c) (*env)->ThrowNew(env, c, rmx_last_error());
 }
 
+/* The reference's require(...) on an argument (IllegalArgumentException, bnn/Scatter.scala:29-30):
+ * every L-B native checks the Java arrays' lengths against what librmx will read or write BEFORE
+ * staging anything, so a short or null array never reaches the device or a host copy. */
+static int require_arg(JNIEnv* env, int ok, const char* msg) {
+  if (ok) return 1;
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+  return 0;
+}
+
+static jlong alen(JNIEnv* env, jarray a) { return a ? (jlong)(*env)->GetArrayLength(env, a) : -1; }
+
 /* ---- model handle: rmx_model + device staging for the L-B calls ---- */
 typedef struct {
   rmx_model* m;
   rmx_ctx* ctx;          /* the model's context (NULL: metadata-only model) */
+  int n_fields, k;       /* F and k of the model: the L-B array lengths are checked against them */
   pthread_mutex_t mu;    /* guards the staging buffers */
   void* d_ids;           /* int32 [cap_ids] */
   void* d_f;             /* float [cap_f]: outputs / targets / gradients, carved per call */
@@ -122,6 +135,8 @@ JNIEXPORT jlong JNICALL JFN(createModel)(JNIEnv* env, jclass cls, jlong ctx, jin
   }
   j->m = m;
   j->ctx = (rmx_ctx*)(intptr_t)ctx;
+  j->n_fields = n_fields;
+  j->k = k;
   pthread_mutex_init(&j->mu, NULL);
   return (jlong)(intptr_t)j;
 }
@@ -285,6 +300,12 @@ JNIEXPORT void JNICALL JFN(destroyTable)(JNIEnv* env, jclass cls, jlong t) {
 JNIEXPORT void JNICALL JFN(uploadTable)(JNIEnv* env, jclass cls, jlong t, jfloatArray w, jfloatArray emb,
                                         jint layout) {
   (void)cls;
+  const rmx_table* tb = (const rmx_table*)(intptr_t)t;
+  const jlong V = rmx_table_rows(tb), kk = rmx_table_embedding_dim(tb);
+  if (!require_arg(env, V >= 0 && (!w || alen(env, w) == V), "uploadTable: weights must hold the table's rows") ||
+      !require_arg(env, !emb || alen(env, emb) == V * kk,
+                   "uploadTable: embedding must hold rows * embeddingDim floats"))
+    return;
   crit c = {{0}, {0}, {0}, 0};
   const float* pw = (const float*)crit_get(env, &c, w, JNI_ABORT);
   const float* pe = (const float*)crit_get(env, &c, emb, JNI_ABORT);
@@ -324,7 +345,10 @@ static int unstage(JNIEnv* env, jmodel* j, size_t off, size_t n, jfloatArray dst
 JNIEXPORT jfloatArray JNICALL JFN(forwardIds)(JNIEnv* env, jclass cls, jlong h, jlong t, jint batch, jintArray ids) {
   (void)cls;
   jmodel* j = JM(h);
-  const jsize n = ids ? (*env)->GetArrayLength(env, ids) : 0;
+  if (!require_arg(env, batch >= 0 && alen(env, ids) == (jlong)batch * j->n_fields,
+                   "forwardIds: ids must hold batch * nFields ints"))
+    return NULL;
+  const jsize n = (*env)->GetArrayLength(env, ids);
   jfloatArray out = (*env)->NewFloatArray(env, batch);
   if (!out) return NULL;
   pthread_mutex_lock(&j->mu);
@@ -346,7 +370,11 @@ JNIEXPORT jfloatArray JNICALL JFN(predictIds)(JNIEnv* env, jclass cls, jlong h, 
                                               jint batch) {
   (void)cls;
   jmodel* j = JM(h);
-  const jsize n = ids ? (*env)->GetArrayLength(env, ids) : 0;
+  if (!require_arg(env, n_rows >= 0 && n_rows <= 0x7fffffff && batch > 0 &&
+                            alen(env, ids) == n_rows * (jlong)j->n_fields,
+                   "predictIds: need nRows >= 0, batch > 0 and ids of nRows * nFields ints"))
+    return NULL;
+  const jsize n = (*env)->GetArrayLength(env, ids);
   jfloatArray out = (*env)->NewFloatArray(env, (jsize)n_rows);
   if (!out) return NULL;
   pthread_mutex_lock(&j->mu);
@@ -374,7 +402,17 @@ JNIEXPORT jfloat JNICALL JFN(backwardIds)(JNIEnv* env, jclass cls, jlong h, jlon
                                           jfloatArray g_m) {
   (void)cls;
   jmodel* j = JM(h);
-  const jsize n = ids ? (*env)->GetArrayLength(env, ids) : 0;
+  const jlong nnz = (jlong)batch * j->n_fields;
+  const int64_t ml = rmx_model_mats_len(j->m);
+  if (!require_arg(env, batch >= 0 && alen(env, ids) == nnz, "backwardIds: ids must hold batch * nFields ints") ||
+      !require_arg(env, alen(env, targets) >= batch, "backwardIds: targets must hold batch floats") ||
+      !require_arg(env, !g_bias || alen(env, g_bias) >= 1, "backwardIds: gBias must hold 1 float") ||
+      !require_arg(env, !g_w || alen(env, g_w) == nnz, "backwardIds: gWeights must hold batch * nFields floats") ||
+      !require_arg(env, !g_e || alen(env, g_e) == nnz * j->k,
+                   "backwardIds: gEmbedding must hold batch * nFields * embeddingDim floats") ||
+      !require_arg(env, !g_m || alen(env, g_m) == ml, "backwardIds: gMats must hold the model's mats length"))
+    return 0.f;
+  const jsize n = (*env)->GetArrayLength(env, ids);
   const size_t nb = (size_t)batch, ng = g_w ? (size_t)(*env)->GetArrayLength(env, g_w) : 0,
                ne = g_e ? (size_t)(*env)->GetArrayLength(env, g_e) : 0,
                nm = g_m ? (size_t)(*env)->GetArrayLength(env, g_m) : 0;
@@ -409,7 +447,10 @@ JNIEXPORT jfloat JNICALL JFN(backwardIds)(JNIEnv* env, jclass cls, jlong h, jlon
 JNIEXPORT jdouble JNICALL JFN(auc)(JNIEnv* env, jclass cls, jlong h, jfloatArray labels, jfloatArray scores) {
   (void)cls;
   jmodel* j = JM(h);
-  const jsize n = labels ? (*env)->GetArrayLength(env, labels) : 0;
+  if (!require_arg(env, labels && scores && alen(env, labels) == alen(env, scores),
+                   "auc: labels and scores must be arrays of the same length"))
+    return 0.0;
+  const jsize n = (*env)->GetArrayLength(env, labels);
   double a = 0.0;
   pthread_mutex_lock(&j->mu);
   int st = grow(j->ctx, &j->d_f, &j->cap_f, 2 * (size_t)(n > 0 ? n : 1), sizeof(float));
@@ -486,7 +527,10 @@ JNIEXPORT jfloatArray JNICALL JFN(forwardIdsSharded)(JNIEnv* env, jclass cls, jl
                                                      jintArray ids) {
   (void)cls;
   jmodel* j = JM(h);
-  const jsize n = ids ? (*env)->GetArrayLength(env, ids) : 0;
+  if (!require_arg(env, batch >= 0 && alen(env, ids) == (jlong)batch * j->n_fields,
+                   "forwardIdsSharded: ids must hold batch * nFields ints"))
+    return NULL;
+  const jsize n = (*env)->GetArrayLength(env, ids);
   jfloatArray out = (*env)->NewFloatArray(env, batch);
   if (!out) return NULL;
   pthread_mutex_lock(&j->mu);

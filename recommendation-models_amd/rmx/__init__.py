@@ -248,8 +248,9 @@ class ExchangeGroup:
 
 
 class ShardedTable:
-    """Hash-sharded table (owner = id mod nranks) over nranks processes, one GPU each, exchanging ids
-    and rows over RCCL (replaces the PS partitions + sparse pulls, ParRecModel.scala:74-105, :165-199).
+    """Hash-sharded table (owner = p(id) mod nranks, p a keyed permutation of the ids: OWNER_HASH_DEFAULT
+    unless set_owner_hash picks another key, 0 = id mod nranks) over nranks processes, one GPU each,
+    exchanging ids and rows over RCCL (replaces the PS partitions + sparse pulls, ParRecModel.scala:74-105, :165-199).
     unique_id=None makes a loopback shard: all partitions in this process (single-GPU testing)."""
 
     def __init__(self, ctx, num_rows, embedding_dim, nranks, rank=0, unique_id=None, group=None):
@@ -282,7 +283,8 @@ class ShardedTable:
         return int(_lib.lib.rmx_shard_local_rows(self.handle))
 
     def set_owner_hash(self, key):
-        """Owner = keyed permutation of the id mod nranks (before fill_synthetic; 0 = id mod nranks)."""
+        """Owner = keyed permutation of the id mod nranks (before fill_synthetic; default
+        OWNER_HASH_DEFAULT; 0 = id mod nranks)."""
         check(_lib.lib.rmx_shard_set_owner_hash(self.handle, int(key)))
 
     def owner_of(self, gid):
@@ -323,6 +325,18 @@ class ShardedTable:
             self.close()
         except Exception:
             pass
+
+
+OWNER_HASH_DEFAULT = 0x5EED5A4D0C7A11ED  # include/rmx.h RMX_OWNER_HASH_DEFAULT
+
+
+def owner_hash(key, num_rows, nranks, gid):
+    """(owner rank, local row) of id gid under the keyed owner permutation (host only, rmx_owner_hash)."""
+    loc = ctypes.c_int64()
+    o = int(_lib.lib.rmx_owner_hash(int(key), int(num_rows), int(nranks), int(gid), ctypes.byref(loc)))
+    if o < 0:
+        raise ValueError("owner_hash: id %d outside [0, %d) or bad arguments" % (gid, num_rows))
+    return o, int(loc.value)
 
 
 def auc(ctx, labels_dev, scores_dev, n=None, stream=None):

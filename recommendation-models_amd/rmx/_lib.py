@@ -76,6 +76,7 @@ SIGNATURES = [
     ("rmx_table_upload", c_int, [c_vp, P(c_f32), P(c_f32), c_int]),
     ("rmx_table_fill_synthetic", c_int, [c_vp, c_u64]),
     ("rmx_table_rows", c_i64, [c_vp]),
+    ("rmx_table_embedding_dim", c_int, [c_vp]),
     ("rmx_table_device_ptrs", c_int, [c_vp, P(c_vp), P(c_vp)]),
     ("rmx_backward", c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp,
                              c_vp, c_vp]),
@@ -97,6 +98,7 @@ SIGNATURES = [
     ("rmx_shard_local_rows", c_i64, [c_vp]),
     ("rmx_shard_set_owner_hash", c_int, [c_vp, c_u64]),
     ("rmx_shard_owner_of", c_i64, [c_vp, c_i64]),
+    ("rmx_owner_hash", c_i64, [c_u64, c_i64, c_int, c_i64, c_vp]),
     ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),
     ("rmx_shard_last_sent", c_i64, [c_vp]),
     ("rmx_predict_ids", c_int, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -97,6 +97,47 @@ def _i32(v):
     return ctypes.c_int32(v)
 
 
+def test_jni_lb_natives_check_array_lengths():
+    """every L-B native checks its Java arrays against batch * nFields (* k), the targets
+    against batch and the gradients against the model's sizes BEFORE staging anything -- a short or
+    null array throws IllegalArgumentException (the reference's require) instead of reaching the
+    device.  The checks run on the host, so a metadata-only model (context 0) exercises them here."""
+    j = Jvm()
+    V, B = 1000, 8
+    jm = j.call("createModel", ctypes.c_int64, ctypes.c_int64(0), _i32(1), ctypes.c_int64(V), _i32(F), _i32(K),
+                j.arr(INT, [16]), None, _i32(0))
+    assert j.exception() is None and jm
+    ml = F * K * 16 + 16 + 16 + 1
+    ok_ids = np.zeros(B * F, np.int32)
+    short = ok_ids[:-1]
+    z = lambda n: j.arr(FLOAT, np.zeros(n, np.float32))  # noqa: E731
+
+    def raises(name, restype, *args, what):
+        j.call(name, restype, ctypes.c_int64(jm), *args)
+        exc = j.exception()
+        assert exc and exc[0] == "java/lang/IllegalArgumentException", (name, exc)
+        assert what in exc[1], (name, exc)
+
+    T = ctypes.c_int64(0)
+    for ids in (None, j.arr(INT, short)):
+        raises("forwardIds", ctypes.c_void_p, T, _i32(B), ids, what="batch * nFields")
+        raises("forwardIdsSharded", ctypes.c_void_p, T, _i32(B), ids, what="batch * nFields")
+        raises("backwardIds", ctypes.c_float, T, _i32(B), ids, z(B), None, None, None, None, what="batch * nFields")
+    raises("predictIds", ctypes.c_void_p, T, ctypes.c_int64(B), j.arr(INT, short), _i32(4), what="nRows * nFields")
+    raises("predictIds", ctypes.c_void_p, T, ctypes.c_int64(B), j.arr(INT, ok_ids), _i32(0), what="batch > 0")
+    ids = j.arr(INT, ok_ids)
+    raises("backwardIds", ctypes.c_float, T, _i32(B), ids, None, None, None, None, None, what="targets")
+    raises("backwardIds", ctypes.c_float, T, _i32(B), ids, z(B - 1), None, None, None, None, what="targets")
+    raises("backwardIds", ctypes.c_float, T, _i32(B), ids, z(B), z(0), None, None, None, what="gBias")
+    raises("backwardIds", ctypes.c_float, T, _i32(B), ids, z(B), None, z(B * F - 1), None, None, what="gWeights")
+    raises("backwardIds", ctypes.c_float, T, _i32(B), ids, z(B), None, None, z(B * F * K + 1), None,
+           what="gEmbedding")
+    raises("backwardIds", ctypes.c_float, T, _i32(B), ids, z(B), None, None, None, z(ml - 1), what="gMats")
+    raises("auc", ctypes.c_double, z(B), z(B - 1), what="same length")
+    raises("auc", ctypes.c_double, None, z(B), what="same length")
+    j.call("destroyModel", None, ctypes.c_int64(jm))
+
+
 @pytest.mark.gpu
 def test_jni_host_array_forward_backward_match_c_abi():
     import rmx

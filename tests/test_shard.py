@@ -50,6 +50,40 @@ def test_route_is_a_bijection():
         owner_of_slot = np.repeat(np.arange(N), counts)
         assert np.array_equal(owner_of_slot[perm], ids % N)
         assert np.array_equal(send_ids[perm] * N + ids % N, ids)
+        # keyed owner map: slot owners follow p(id), the local rows invert back to the ids
+        counts, send_ids, perm = shard_ref.route(ids, N, shard_ref.OWNER_HASH_DEFAULT, 1000)
+        p = shard_ref.owner_perm(ids, shard_ref.OWNER_HASH_DEFAULT, 1000)
+        assert np.array_equal(np.repeat(np.arange(N), counts)[perm], p % N)
+        assert np.array_equal(send_ids[perm] * N + p % N, p)
+
+
+@pytest.mark.parametrize("V,N", [(5003, 2), (100_003, 8), (1 << 20, 3), (100_000_000, 8)])
+def test_owner_hash_host_matches_numpy_restatement(V, N):
+    """rmx_owner_hash (the C function every route kernel inlines) against the numpy restatement of
+    the keyed Feistel permutation; the default key is on (configs[3] hash-shards), key 0 = id mod N."""
+    import rmx
+    import shard_ref
+    ids = np.random.default_rng(V).integers(0, V, 2000)
+    ids[:3] = [0, V - 1, V // 2]
+    for key in (rmx.OWNER_HASH_DEFAULT, 0, 99):
+        p = shard_ref.owner_perm(ids, key, V)
+        got = [rmx.owner_hash(key, V, N, int(i)) for i in ids]
+        assert [o for o, _ in got] == (p % N).tolist()
+        assert [l for _, l in got] == (p // N).tolist()
+    assert rmx.OWNER_HASH_DEFAULT == shard_ref.OWNER_HASH_DEFAULT
+    with pytest.raises(ValueError):
+        rmx.owner_hash(rmx.OWNER_HASH_DEFAULT, V, N, V)  # outside [0, V): no owner
+
+
+def test_owner_hash_is_a_bijection_and_balances():
+    import shard_ref
+    V = 100_003
+    p = shard_ref.owner_perm(np.arange(V), shard_ref.OWNER_HASH_DEFAULT, V)
+    assert np.array_equal(np.sort(p), np.arange(V))
+    assert np.array_equal(shard_ref.owner_perm(p, shard_ref.OWNER_HASH_DEFAULT, V, inverse=True), np.arange(V))
+    strided = np.arange(0, V, 8)  # all multiples of 8: one owner under id mod 8
+    c = np.bincount(shard_ref.owner_perm(strided, shard_ref.OWNER_HASH_DEFAULT, V) % 8, minlength=8)
+    assert c.min() > 0.9 * len(strided) / 8 and c.max() < 1.1 * len(strided) / 8
 
 
 # ------------------------------------------------------------------ GPU ----
@@ -513,7 +547,10 @@ def test_owner_hash_balances_strided_ids_and_stays_bitwise(N):
     cnt = np.bincount([sh.owner_of(i) for i in strided], minlength=N)
     assert cnt.min() > 0.85 * len(strided) / N and cnt.max() < 1.15 * len(strided) / N
     plain = rmx.ShardedTable(ctx, V, K, N)
+    plain.set_owner_hash(0)  # the identity: owner = id mod N
     assert all(plain.owner_of(i) == 0 for i in range(0, 3000, N))
+    dflt = rmx.ShardedTable(ctx, V, K, N)  # hash-sharded by default
+    assert all(dflt.owner_of(i) == rmx.owner_hash(rmx.OWNER_HASH_DEFAULT, V, N, i)[0] for i in range(0, 3000, 7))
     sh.fill_synthetic(SEED_TAB)
     with pytest.raises(rmx.RmxError):
         sh.set_owner_hash(7)  # fixed once the rows are filled
@@ -575,3 +612,69 @@ def test_group_exchange_owner_hash(N=4):
         m.forward_ids(table, B, ids, ref)
         ctx.sync()
         assert np.array_equal(got, ref.numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 4])
+def test_pull_slots_grow_independently(N):
+    """a pull into slot 1 with a LARGER batch than the pending pull in slot 0 grows only
+    slot 1's buffers -- slot 0's rows survive and both forwards stay bitwise the replicated table's."""
+    import rmx
+    ctx, ctx_x = rmx.default_context(), rmx.Context(0)
+    V = 100_003
+    Bs = (300, 1300, 2100)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    m = rmx.DeepFM(V, F, K, [64, 32])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, N, 0, rmx.comm_unique_id() if N == 1 else None)
+    sh.fill_synthetic(SEED_TAB)
+    ids = [rmx.DeviceArray(ctx, B * F, np.int32) for B in Bs]
+    for i, B in enumerate(Bs):
+        rmx.gen_ids(ctx, SEED_IDS, 1000 * i, B, F, V, ids[i])
+    outs = [rmx.DeviceArray(ctx, B, np.float32) for B in Bs]
+    ctx.sync()
+    sh.pull(ids[0], Bs[0] * F, 0, ctx_x.stream)
+    sh.pull(ids[1], Bs[1] * F, 1, ctx_x.stream)   # grows slot 1 while slot 0 is pending
+    m.forward_pulled(sh, Bs[0], 0, outs[0], ctx.stream)
+    sh.pull(ids[2], Bs[2] * F, 0, ctx_x.stream)   # grows slot 0 while slot 1 is pending
+    m.forward_pulled(sh, Bs[1], 1, outs[1], ctx.stream)
+    m.forward_pulled(sh, Bs[2], 0, outs[2], ctx.stream)
+    ctx.sync()
+    ctx_x.sync()
+    for i, B in enumerate(Bs):
+        ref = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(table, B, ids[i], ref)
+        ctx.sync()
+        assert np.array_equal(outs[i].numpy(), ref.numpy()), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 3])
+def test_out_of_range_ids_do_not_hang_the_route(N):
+    """with the keyed owner map an id outside [0, V) has no finite cycle walk; routing
+    gives it no owner (a defined in-range slot, a zero row at one rank), so the exchange returns and
+    every sample that holds only valid ids is bitwise the replicated forward."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 100_003, 400
+    table, ids = _setup(ctx, V, B, seed_row=31)
+    h = ids.numpy().reshape(B, F).copy()
+    bad_rows = [0, 7, B - 1]
+    h[0, 3], h[7, 0], h[B - 1, F - 1] = V + 5, -2, (1 << 30)
+    bad = rmx.DeviceArray(ctx, B * F, np.int32)
+    bad.upload(h.ravel())
+    m = rmx.DeepFM(V, F, K, [64, 32])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, N, 0, rmx.comm_unique_id() if N == 1 else None)
+    sh.fill_synthetic(SEED_TAB)
+    got = rmx.DeviceArray(ctx, B, np.float32)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids_sharded(sh, B, bad, got)
+    m.forward_ids(table, B, ids, ref)
+    ctx.sync()
+    keep = np.setdiff1d(np.arange(B), bad_rows)
+    assert np.array_equal(got.numpy()[keep], ref.numpy()[keep])
+    assert np.isfinite(got.numpy()).all()

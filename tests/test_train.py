@@ -175,9 +175,20 @@ def _tie_free(kind, E, mats, fc, rel=1e-5):
 @pytest.mark.parametrize("kind", GPU_KINDS)
 @pytest.mark.parametrize("B,fc", [(512, (400, 400, 400)), (37, (24, 8)), (64, (16,))])
 def test_backward_ids_matches_oracle(kind, B, fc):
+    _backward_ids_check(kind, B, fc)
+
+
+@pytest.mark.gpu
+def test_backward_cin_more_than_256_fields():
+    """the fused dL/dz contraction (cin_back_fused_kernel, 256 threads per row) reduces
+    the x0 gradient of EVERY field; F = 260 with CIN (8, 4) takes the fused path on layer 2."""
+    _backward_ids_check("xdeepfm", 16, (24, 8), F=260, V=30_000)
+
+
+def _backward_ids_check(kind, B, fc, F=39, V=20_000):
     import rmx
     ctx = rmx.default_context()
-    V, F, K = 20_000, 39, 16
+    K = 16
     m = _gpu_model(rmx, kind, V, F, K, fc)
     mats = m.initMats(SEED_MATS) if kind != "lr" else np.zeros(0, np.float32)
     if kind != "lr":

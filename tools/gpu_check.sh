@@ -64,6 +64,13 @@ for s in $STEPS; do
               run settle_$ms 200 python bench.py --steps 20 --warmup 5 --no-companion --no-cpu-baseline --settle-ms $ms
             done ;;
     list) run list 120 rocprofv3 -L ;;
+    bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
+    bench2s) echo "== bench_gpus2_sharded (expects a clean refusal on a 1-GPU box)" | tee -a "$OUT/steps.log"
+         timeout -k 10 300 python bench.py --workload deepfm_sharded --gpus 2 --steps 5 --warmup 1 \
+            > "$OUT/bench_gpus2_sharded.log" 2>&1
+         echo "== bench_gpus2_sharded rc=$?" | tee -a "$OUT/steps.log"; tail -n 5 "$OUT/bench_gpus2_sharded.log" ;;
+    profd) run profd 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profd" -o driver -- \
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench:*) wl=${s#bench:}
          run bench_$wl 400 python bench.py --workload $wl ;;
     benchq:*) wl=${s#benchq:}
