@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="Zipf exponent of the ids within a field (SURVEY.md §8d secondary; 0 = uniform)")
     ap.add_argument("--no-dedupe", action="store_true", help="deepfm_sharded: skip the distinct-id step (default: auto)")
+    ap.add_argument("--dedupe-on", action="store_true", help="deepfm_sharded: always run the distinct-id step")
     ap.add_argument("--no-overlap", action="store_true",
                     help="deepfm_sharded: exchange and forward on one stream (default: batch i + 1's exchange "
                          "on a second stream beside batch i's forward)")
@@ -77,14 +78,18 @@ def parse():
     return ap.parse_args()
 
 
-def stage_work(workload, stage, B):
-    """Algorithmic work of one launch of a stage: ('flop'|'byte', amount)."""
+def stage_work(workload, stage, B, direct=False):
+    """Algorithmic work of one launch of a stage: ('flop'|'byte', amount).  direct: the
+    one-rank sharded table read in place (the "exchange" maps the batch's ids to partition rows)."""
     D = F * K
     P = F * (F - 1) // 2
     es = 2 if workload.endswith("bf16") else 4  # table element bytes
     if stage == "first_order_sigmoid":  # LR: ids + w + p
         return "byte", B * (F * 4 + F * es + 4)
-    if stage == "shard_exchange":  # ids out + (k+1)-float rows back, all ranks' shares incl. self
+    if stage == "shard_exchange":
+        if direct:  # ids in, partition rows out
+            return "byte", B * F * 8
+        # ids out + (k+1)-float rows back, all ranks' shares incl. self
         return "byte", B * F * (4 + 4 + (K + 1) * 4 * 2)
     if stage == "encoder_fm":  # ids + w + emb rows + y  (SURVEY.md §8d: 2,812 B / example)
         return "byte", B * (F * 4 + F * es + F * K * es + 4)
@@ -390,7 +395,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
                 dist.broadcast_object_list(box, src=0)
                 uid = box[0]
             table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
-        table.set_dedupe(False if args.no_dedupe else "auto")
+        table.set_dedupe(False if args.no_dedupe else (True if args.dedupe_on else "auto"))
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
     table.fill_synthetic(SEED_TAB)
@@ -512,10 +517,12 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
             return PEAK_BF16_TFLOPS
         return PEAK_S3_TFLOPS if split and stage.startswith(S3_STAGES) else PEAK_FP32_TFLOPS
 
+    # one rank without dedupe: the sharded table is read in place (csrc/shard.hip direct_eligible)
+    direct = sharded and world == 1 and not args.dedupe_on
     per_stage = {}
     for name, tot in stages.items():
         avg_ms = tot / max(calls, 1)
-        kind, work = stage_work(workload, name, B)
+        kind, work = stage_work(workload, name, B, direct)
         ent = {"avg_ms": round(avg_ms, 4)}
         if kind == "flop":
             ent["tflops"] = round(work / (avg_ms / 1e3) / 1e12, 2)
@@ -526,7 +533,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
         per_stage[name] = ent
     stage_sum = sum(stages.values()) / max(calls, 1)
     dom = max(stages.items(), key=lambda kv: kv[1])[0]
-    kind, work = stage_work(workload, dom, B)
+    kind, work = stage_work(workload, dom, B, direct)
     avg_s = stages[dom] / max(calls, 1) / 1e3
     if kind == "byte":
         roof = {"bound": "hbm", "achieved": round(work / avg_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
@@ -576,7 +583,12 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
            "settle_steps": settle,
            "out": out.numpy()[:512], "bf16": bf16, "split": split}
     if sharded:
-        res["exchange"] = {"dedupe": "off" if args.no_dedupe else "auto", "ids_sent_last_step": table.last_sent(),
+        res["exchange"] = {"dedupe": "off" if args.no_dedupe else ("on" if args.dedupe_on else "auto"),
+                           "mode": ("one rank: the batch's ids map to partition rows p(id) and the forward reads "
+                                    "the [emb | w | pad] lines in place (no exchange, no row copy)") if direct else
+                                   "RCCL exchange (ids to owners, rows back)",
+                           "owner_map": "keyed Feistel permutation p (rmx.OWNER_HASH_DEFAULT): owner = p(id) mod N",
+                           "ids_sent_last_step": table.last_sent(),
                            "nnz_per_step": B * F,
                            "overlap": ("batch i + 1's exchange (rmx_shard_pull) on a second stream beside batch i's "
                                        "forward (rmx_forward_pulled)") if not args.no_overlap else "none (one stream)",
@@ -766,6 +778,9 @@ def main():
                      + ("; LIBSVM text of the same ids, Bernoulli(0.25) labels" if args.workload == "lr_plumbing"
                         else "")),
             "config": config_of(args.workload, r, world, args.zipf),
+            **({"table_layout": "[V][32] fp32 line rows [emb 16 | w | pad]: one 128-B memory line per id "
+                                "(rmx_table::line, knob table_lines)"}
+               if args.workload == "deepfm" and rmx.get_tuning("table_lines", 1) else {}),
             **({"exchange": r["exchange"]} if "exchange" in r else {}),
             "roofline": r["roofline"],
             "cpu_baseline": cpu,

@@ -300,12 +300,42 @@ extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
   return rmx_table_create_ex(c, V, k, RMX_DTYPE_F32, out);
 }
 
+// the [V][32] line copy of an fp32 k = 16 table (rmx_table::line), rebuilt from emb / w; knob
+// "table_lines" 0 drops it (the forward then reads emb / w)
+int rmx::table_refresh_lines(rmx_table& t) {
+  const bool want = t.dtype == RMX_DTYPE_F32 && t.k == 16 && tuning_get("table_lines", 1) != 0;
+  if (!want) {
+    if (t.line) {
+      RMX_HIP(hipStreamSynchronize(t.ctx->stream));
+      (void)hipFree(t.line);
+      t.line = nullptr;
+    }
+    return RMX_OK;
+  }
+  if (!t.line && hipMalloc(&t.line, sizeof(float) * 32 * t.V) != hipSuccess) {
+    t.line = nullptr;
+    set_error("rmx_table: out of device memory for the line copy (set knob table_lines 0)");
+    return RMX_E_NOMEM;
+  }
+  const int st = launch_pack_lines(t.ctx->stream, t.V, (const float*)t.emb, (const float*)t.w, t.line);
+  if (st) return st;
+  RMX_HIP(hipStreamSynchronize(t.ctx->stream));
+  return RMX_OK;
+}
+
+extern "C" int rmx_table_refresh_lines(rmx_table* t) {
+  CHECK_ARG(t, "rmx_table_refresh_lines: NULL table");
+  RMX_HIP(hipSetDevice(t->ctx->device));
+  return table_refresh_lines(*t);
+}
+
 extern "C" int rmx_table_destroy(rmx_table* t) {
   if (!t) return RMX_OK;
   (void)hipSetDevice(t->ctx->device);
   (void)hipStreamSynchronize(t->ctx->stream);
   if (t->w) (void)hipFree(t->w);
   if (t->emb) (void)hipFree(t->emb);
+  if (t->line) (void)hipFree(t->line);
   delete t;
   return RMX_OK;
 }
@@ -358,6 +388,7 @@ extern "C" int rmx_table_upload(rmx_table* t, const float* weights, const float*
   }
   RMX_HIP(hipStreamSynchronize(s));
   if (tmp) (void)hipFree(tmp);
+  if (st == RMX_OK) st = table_refresh_lines(*t);
   return st;
 }
 
@@ -367,7 +398,7 @@ extern "C" int rmx_table_fill_synthetic(rmx_table* t, uint64_t seed) {
   const int st = launch_fill_table(t->ctx->stream, seed, t->V, t->k, t->w, t->emb, t->dtype);
   if (st != RMX_OK) return st;
   RMX_HIP(hipStreamSynchronize(t->ctx->stream));
-  return RMX_OK;
+  return table_refresh_lines(*t);
 }
 
 extern "C" int rmx_gen_ids(rmx_ctx* c, uint64_t seed, int64_t row0, int32_t B, int32_t F, int64_t V,
@@ -423,9 +454,7 @@ extern "C" int rmx_forward_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
   FwdInputs in;
   in.B = B;
   in.ids = d_ids;
-  in.table = t->emb;
-  in.wtab = t->w;
-  in.dtype = t->dtype;
+  table_inputs(*t, *m, in);
   in.beta = m->beta;
   in.out = d_out;
   return model_forward(*m, s, in);

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
                                                           const T* __restrict__ table,
                                                           const T* __restrict__ wtab, int F,
                                                           float* __restrict__ y, float beta,
-                                                          float* __restrict__ prob) {
+                                                          float* __restrict__ prob, int ld, int wld) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int s = lane >> 2, c = lane & 3;
@@ -47,8 +47,8 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
     float wv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if (MODE == 1 || MODE == 3) v[u] = load4(table + (int64_t)id[u] * 16 + c * 4);
-      if (MODE != 3) wv[u] = (c == 0) ? ld1(wtab + id[u]) : 0.f;
+      if (MODE == 1 || MODE == 3) v[u] = load4(table + (int64_t)id[u] * ld + c * 4);
+      if (MODE != 3) wv[u] = (c == 0) ? ld1(wtab + (int64_t)id[u] * wld) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -63,11 +63,11 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
   for (; f < F; ++f) {
     const int id = ids ? ids[(int64_t)bb * F + f] : bb * F + f;
     if (MODE == 1 || MODE == 3) {
-      const float4 v = load4(table + (int64_t)id * 16 + c * 4);
+      const float4 v = load4(table + (int64_t)id * ld + c * 4);
       s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
       q4.x += v.x * v.x; q4.y += v.y * v.y; q4.z += v.z * v.z; q4.w += v.w * v.w;
     }
-    if (MODE != 3 && c == 0) y1 += ld1(wtab + id);
+    if (MODE != 3 && c == 0) y1 += ld1(wtab + (int64_t)id * wld);
   }
   float y2 = 0.f;
   if (MODE == 1 || MODE == 3) {
@@ -98,7 +98,8 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
                                                               const T* __restrict__ table,
                                                               const T* __restrict__ wtab, int F,
                                                               int k, float* __restrict__ y,
-                                                              float beta, float* __restrict__ prob) {
+                                                              float beta, float* __restrict__ prob, int ld,
+                                                              int wld) {
 #pragma clang fp contract(off)
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= M) return;
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
   if (MODE != 3)
     for (int f = 0; f < F; ++f) {
       const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
-      y1 += ld1(wtab + id);
+      y1 += ld1(wtab + (int64_t)id * wld);
     }
   if (MODE == 1 || MODE == 3) {
     float acc = 0.f;
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
       float s = 0.f, q = 0.f;
       for (int f = 0; f < F; ++f) {
         const int id = ids ? ids[(int64_t)b * F + f] : b * F + f;
-        const float v = ld1(table + (int64_t)id * k + j);
+        const float v = ld1(table + (int64_t)id * ld + j);
         s += v;
         q += v * v;
       }
@@ -130,33 +131,35 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
 
 template <class T>
 static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids, const T* table, const T* wtab, int F,
-                             int k, float* y, float bt, float* prob) {
+                             int k, float* y, float bt, float* prob, int ld, int wld) {
   if (k == 16 || mode == 2) {  // LR (mode 2) never reads the table: any k takes the 4-lane path
     dim3 grid((M + 63) / 64);
     switch (mode) {
-      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
-      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
-      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
-      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob); break;
+      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
+      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
+      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
+      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
     }
   } else {
     dim3 grid((M + 255) / 256);
     switch (mode) {
-      case 0: hipLaunchKernelGGL((encoder_generic_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
-      case 1: hipLaunchKernelGGL((encoder_generic_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
-      default: hipLaunchKernelGGL((encoder_generic_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob); break;
+      case 0: hipLaunchKernelGGL((encoder_generic_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob, ld, wld); break;
+      case 1: hipLaunchKernelGGL((encoder_generic_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob, ld, wld); break;
+      default: hipLaunchKernelGGL((encoder_generic_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, k, y, bt, prob, ld, wld); break;
     }
   }
 }
 
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table, const void* wtab, int dt,
-                   int F, int k, float* y, const float* beta, float* prob) {
+                   int F, int k, float* y, const float* beta, float* prob, int ld, int wld) {
   if (M <= 0) return RMX_OK;
   const float bt = beta ? *beta : 0.f;
+  ld = ld > 0 ? ld : (k == 16 || mode == 2 ? 16 : k);
+  wld = wld > 0 ? wld : 1;
   if (dt == kBF16)
-    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob);
+    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob, ld, wld);
   else
-    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob);
+    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob, ld, wld);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
@@ -235,6 +238,27 @@ int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int
   if (n <= 0) return RMX_OK;
   hipLaunchKernelGGL(gen_ids_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, seed, row0, B,
                      F, (uint64_t)(V / F), ids);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// [V][32] line copy of an fp32 k = 16 table: row i = [emb[i][0..16) | w[i] | 15 zeros], one 128-B
+// memory line per id (rmx_table::line).  Eight lanes per row, one float4 each (coalesced 128-B rows).
+__global__ __launch_bounds__(256) void pack_lines_kernel(int64_t V, const float* __restrict__ emb,
+                                                        const float* __restrict__ w, float* __restrict__ line) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t >> 3;
+  const int c = (int)(t & 7);
+  if (i >= V) return;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < 4) v = reinterpret_cast<const float4*>(emb)[i * 4 + c];
+  else if (c == 4) v.x = w[i];
+  reinterpret_cast<float4*>(line)[i * 8 + c] = v;
+}
+
+int launch_pack_lines(hipStream_t s, int64_t V, const float* emb, const float* w, float* line) {
+  if (V <= 0) return RMX_OK;
+  hipLaunchKernelGGL(pack_lines_kernel, dim3((unsigned)((V * 8 + 255) / 256)), dim3(256), 0, s, V, emb, w, line);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -224,7 +224,15 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
   p.Npad = L.Npad;
   p.A = A;
   p.lda = lda;
-  if (ga) p.ga = *ga;
+  if (ga) {
+    p.ga = *ga;
+    if (p.ga.ld == 0) p.ga.ld = p.ga.k;
+    if (p.ga.ld < p.ga.k || (p.ga.k == 16 && (p.ga.ld & (p.ga.ld - 1)))) {
+      set_error("gemm: table row stride must be >= k (a power of two at k = 16)");
+      return RMX_E_INVALID;
+    }
+    p.gsh = __builtin_ctz((unsigned)p.ga.ld);
+  }
   p.Wp = L.W16 ? reinterpret_cast<const float*>(L.W16) : L.W;
   p.bias = L.b;
   p.C = C;
@@ -245,6 +253,12 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
     p.fm_sums = fm->sums;
     p.fm_add = fm->add;
     p.fm_y = fm->y;
+    const int wld = fm->wld ? fm->wld : 1;
+    if (wld & (wld - 1)) {
+      set_error("gemm: first-order weight stride must be a power of two");
+      return RMX_E_INVALID;
+    }
+    p.fm_wsh = __builtin_ctz((unsigned)wld);
   }
   const int amode = !ga ? kDenseA : (ga->k == 16 ? kGatherK16 : kGatherAny);
   if (L.W16) {
@@ -276,7 +290,8 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
 }
 
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
-                     const int32_t* ids, const float* table, const float* u_prev, float* u_out, float* rowdot) {
+                     const int32_t* ids, const float* table, const float* u_prev, float* u_out, float* rowdot,
+                     int ld) {
   if (B <= 0) return RMX_OK;
   if (!first && !u_prev) {
     set_error("cin: missing previous layer maps");
@@ -287,7 +302,7 @@ int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, in
   p.K = L.Hp_pad * F;
   p.Kpad = p.K;
   p.Npad = L.Npad;
-  p.ga = AGatherArgs{ids, table, F, k};
+  p.ga = AGatherArgs{ids, table, F, k, ld > 0 ? ld : k};
   p.u_prev = u_prev;
   p.ldu = L.Hp_pad;
   p.XS = round_up(std::max(F, first ? L.Hp_pad : 0), 16) + 4;  // 16-B rows; x0 and (layer 1) u

@@ -129,8 +129,9 @@ struct GemmArgs {
   // fm_y[m] = y1 + y2 (bit-identical to encoder_k16_kernel<1>: same fp32 order, no contraction).
   // Without the FM sums (fm_sums = 0) the same epilogue gives the first order alone (y1, the other
   // models' Scatter term, bit-identical to encoder_k16_kernel<0>) for any k = 16 gather layer 1.
-  const void* fm_w;    // first-order weights [V] (bf16 when fm_w_bf16)
-  int fm_w_bf16, fm_sums;
+  const void* fm_w;    // first-order weights [V] (bf16 when fm_w_bf16), weight of id at fm_w[id << fm_wsh]
+  int fm_w_bf16, fm_sums, fm_wsh;
+  int gsh;             // kGatherK16: log2 of the table's row stride ga.ld (row of id at table + (id << gsh))
   int fm_add;          // 1: fm_y already holds y1 (a first-order kernel ran): fm_y = fm_y + y2
   float* fm_y;         // [M], nullptr = off
   // kEpiRelu variants for the backward's dX = dPre W (train.hip): raw = store acc (+ bias when
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       if (f < F && m < M) {
         const int b = m / k;
         const int id = p.ga.ids ? p.ga.ids[(int64_t)b * F + f] : b * F + f;
-        v = p.ga.table[(int64_t)id * k + j];
+        v = p.ga.table[(int64_t)id * p.ga.ld + j];
       }
       extra[r * XS + f] = v;
     }
@@ -390,13 +391,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         // fp32: chunk c = field c; bf16: chunk c = fields 2c, 2c+1 (two 32-B rows)
         const int f = BF ? 2 * c + (g >> 1) : c;
         const int id = sids[r * F + f];
-        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * 16 + (g & 1) * 8)
-                  : (const void*)(p.ga.table + (int64_t)id * 16 + g * 4);
+        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + ((int64_t)id << p.gsh) + (g & 1) * 8)
+                  : (const void*)(p.ga.table + ((int64_t)id << p.gsh) + g * 4);
       } else if constexpr (AMODE == kGatherAny) {
         const int f = kk / p.ga.k, j = kk - f * p.ga.k;
         const int id = sids[r * F + f];
-        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * p.ga.k + j)
-                  : (const void*)(p.ga.table + (int64_t)id * p.ga.k + j);
+        return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.ga.table) + (int64_t)id * p.ga.ld + j)
+                  : (const void*)(p.ga.table + (int64_t)id * p.ga.ld + j);
       } else {
         return BF ? (const void*)(reinterpret_cast<const bf16_t*>(p.A) + (int64_t)m * p.lda + kk)
                   : (const void*)(p.A + (int64_t)m * p.lda + kk);
@@ -772,7 +773,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                                         : (const void*)zero16;
             } else if constexpr (IDRING) {
               const int id = idring[((c & 1) * 2 + cc) * BM + r];
-              src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)zero16;
+              src = id >= 0 ? (const void*)(p.ga.table + ((int64_t)id << p.gsh) + g * 4) : (const void*)zero16;
             } else {
               src = src_of(row, g, c);
               if (!src) src = zero16;
@@ -833,7 +834,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                                       : (const void*)zero16;
           } else if constexpr (IDRING) {
             const int id = get_id();
-            src = id >= 0 ? (const void*)(p.ga.table + (int64_t)id * 16 + g * 4) : (const void*)zero16;
+            src = id >= 0 ? (const void*)(p.ga.table + ((int64_t)id << p.gsh) + g * 4) : (const void*)zero16;
           } else {
             src = src_of(row, g, cs);
             if (!src) src = zero16;
@@ -876,12 +877,14 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         const int id = get_id();
         const int e = (c & 1) * 2 * BM + ins * 64;
         if (!S3 && p.fm_w_bf16) {  // (kPrecS3 models have fp32 tables: launch_tower_s3 checks)
-          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const bf16_t*>(p.fm_w) + id) : (const void*)zero16;
+          const void* src = id >= 0 ? (const void*)(reinterpret_cast<const bf16_t*>(p.fm_w) + ((int64_t)id << p.fm_wsh))
+                                    : (const void*)zero16;
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 2, 0, 0);
         } else {
           // (kPrecS3 issues this unconditionally: zeros when the launch fuses no first order)
           const bool ok = id >= 0 && (!S3 || wfuse);
-          const void* src = ok ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + id) : (const void*)zero16;
+          const void* src = ok ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + ((int64_t)id << p.fm_wsh))
+                               : (const void*)zero16;
           __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 4, 0, 0);
         }
       }
@@ -1214,8 +1217,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
             if constexpr (IDRING) id = p.ga.ids[(int64_t)(m0 + arow[i] < M ? m0 + arow[i] : m0) * F + f];
             else id = sids[arow[i] * F + f];
           }
-          wv[u] = f < F ? (p.fm_w_bf16 ? (float)reinterpret_cast<const bf16_t*>(p.fm_w)[id]
-                                       : reinterpret_cast<const float*>(p.fm_w)[id])
+          wv[u] = f < F ? (p.fm_w_bf16 ? (float)reinterpret_cast<const bf16_t*>(p.fm_w)[(int64_t)id << p.fm_wsh]
+                                       : reinterpret_cast<const float*>(p.fm_w)[(int64_t)id << p.fm_wsh])
                         : 0.f;
         }
         float y1 = 0.f;

@@ -176,9 +176,7 @@ extern "C" int rmx_predict_ids(rmx_model* m, const rmx_table* t, int64_t n_rows,
     FwdInputs in;
     in.B = (int)std::min<int64_t>(batch, n_rows - r0);
     in.ids = d_ids + r0 * m->F;
-    in.table = t->emb;
-    in.wtab = t->w;
-    in.dtype = t->dtype;
+    table_inputs(*t, *m, in);
     in.beta = m->beta;
     in.out = d_scores + r0;
     const int st = model_forward(*m, s, in);

@@ -665,6 +665,24 @@ int model_collect_timing(rmx_model& m) {
   return RMX_OK;
 }
 
+bool model_reads_lines(const rmx_model& m) {
+  return m.type == RMX_MODEL_LR ||
+         ((m.type == RMX_MODEL_DEEPFM || m.type == RMX_MODEL_DNN) && m.k == 16 && !needs_gather_x(m));
+}
+
+void table_inputs(const rmx_table& t, const rmx_model& m, FwdInputs& in) {
+  in.dtype = t.dtype;
+  if (t.line && model_reads_lines(m)) {
+    in.table = t.line;
+    in.wtab = t.line + 16;
+    in.ld = in.wld = 32;
+  } else {
+    in.table = t.emb;
+    in.wtab = t.w;
+    in.ld = in.wld = 0;
+  }
+}
+
 // The per-model kernel sequence.  in.ids == nullptr means implicit ids (L-A gathered rows).
 int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   const int B = in.B;
@@ -674,15 +692,23 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   if (m.timing) ++m.timed_calls;
   const int F = m.F, k = m.k;
 
+  // strided ([emb | w | pad] line) tables reach only kernels that take a row stride: the encoder and
+  // the gathered tower layer 1 (DeepFM / DNN / LR)
+  const bool strided = (in.ld > 0 && in.ld != k) || in.wld > 1;
+  if (strided && !(m.type == RMX_MODEL_LR || ((m.type == RMX_MODEL_DEEPFM || m.type == RMX_MODEL_DNN) &&
+                                              !needs_gather_x(m) && k == 16))) {
+    set_error("forward: a strided (line-row) table needs a DeepFM / DNN model with k = 16 or LR");
+    return RMX_E_INVALID;
+  }
   if (m.type == RMX_MODEL_LR) {
     StageTimer t(m, s, "first_order_sigmoid");
     if (in.y1) return launch_sigmoid_out(s, B, in.y1, in.beta, in.out);
-    return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out);
+    return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out, in.ld, in.wld);
   }
 
   // 1. first order (+ FM for DeepFM; fused into tower layer 1 when it gathers through the split GEMM)
   const float* pre = nullptr;
-  AGatherArgs ga{in.ids, (const float*)in.table, F, k};
+  AGatherArgs ga{in.ids, (const float*)in.table, F, k, in.ld};
   bool gather_first = !needs_gather_x(m);
   // DeepFM on the split GEMM: first order + FM inside tower layer 1; the other models with a
   // gathered layer 1 (xDeepFM, DCN): the first order there
@@ -700,18 +726,21 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
                       (fm_y1 == 0 || (fm_y1 == 2 && !tower_wring(m.layers[0], B, &ga)));
   if (fm_add) {
     StageTimer t(m, s, "first_order");
-    if ((st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr))) return st;
+    if ((st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr, in.ld,
+                             in.wld)))
+      return st;
   }
   if (fm_fused) {
     pre = m.y12;
   } else if (m.type == RMX_MODEL_DEEPFM) {
     StageTimer t(m, s, "encoder_fm");
-    st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr);
+    st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr, in.ld,
+                        in.wld);
     pre = m.y12;
   } else if (m.type != RMX_MODEL_DNN) {
     if (!in.y1) {
       StageTimer t(m, s, "first_order");
-      st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr);
+      st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr, in.ld, in.wld);
     }
     pre = m.y12;  // (the L-A irregular path already wrote y1 here)
   }
@@ -775,7 +804,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
     XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
-    FmArgs fm{in.wtab, in.dtype == kBF16 ? 1 : 0, deepfm ? 1 : 0, fm_add ? 1 : 0, m.y12};
+    FmArgs fm{in.wtab, in.dtype == kBF16 ? 1 : 0, deepfm ? 1 : 0, fm_add ? 1 : 0, m.y12, in.wld};
     st = launch_tower_layer(s, L, B, A, lda, (i == 0 && gather_first) ? &ga : nullptr, C, L.Npad,
                             last ? Epi::kOutput : Epi::kReluStore, last ? &oa : nullptr,
                             (i == 0 && m.dcn_fused) ? &xc : nullptr, (i == 0 && fm_fused) ? &fm : nullptr);

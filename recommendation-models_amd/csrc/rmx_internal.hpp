@@ -76,8 +76,10 @@ inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 // A operand producer for the first tower layer.
 struct AGatherArgs {
   const int32_t* ids;  // [M][F] or nullptr (implicit id = m*F + f, the L-A path)
-  const float* table;  // [rows][k] (bf16 elements for bf16 models: reinterpreted)
+  const float* table;  // [rows][ld] (bf16 elements for bf16 models: reinterpreted)
   int F, k;
+  int ld;              // row stride in elements (0 = k); a power of two on k = 16 gathers (e.g. 32: the
+                       // [emb 16 | w | pad] line rows of a sharded partition or a replicated line table)
 };
 
 enum class Epi : int {
@@ -111,6 +113,7 @@ struct FmArgs {
   int sums;        // 1: y = y1 + y2 (DeepFM, split-GEMM layer 1); 0: y = y1
   int add;         // 1 (with sums): y already holds y1, y = y + y2
   float* y;        // [M]
+  int wld;         // stride of the weights in elements (0 = 1; 32: the w slot of [emb | w | pad] line rows)
 };
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
@@ -124,8 +127,10 @@ bool tower_wring(const DenseLayer& L, int M, const AGatherArgs* ga);
 
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
+// ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1)
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table,
-                   const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob);
+                   const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob, int ld = 0,
+                   int wld = 0);
 int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y);
 int launch_sigmoid_out(hipStream_t s, int B, const float* y, float beta, float* out);
 int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids);

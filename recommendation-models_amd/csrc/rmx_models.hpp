@@ -21,6 +21,11 @@ struct rmx_table {
   int dtype = 0;          // RMX_DTYPE_F32 / RMX_DTYPE_BF16 (elements of w and emb)
   void* w = nullptr;      // [V]     first-order weights (Angel "weights" row 0)
   void* emb = nullptr;    // [V][k]  embeddings, row-major (Angel "embedding" rows 0..k-1, transposed)
+  // fp32 k = 16 tables (knob "table_lines", default on): a [V][32] line copy, row = [emb 16 | w | pad 15]
+  // -- one 128-B memory line per id instead of a 64-B row line plus a separate weight line.  Rebuilt
+  // from emb / w by every upload / fill (rmx_table_refresh_lines after writes through device_ptrs);
+  // read by the models whose every table access takes a row stride (rmx::model_reads_lines).
+  float* line = nullptr;
 };
 
 namespace rmx {
@@ -34,6 +39,10 @@ struct FwdInputs {
   const void* table = nullptr;     // [rows][k]  (elements of dtype)
   const void* wtab = nullptr;      // [rows]
   int dtype = 0;                   // kF32 / kBF16
+  // row stride of `table` and stride of `wtab` in elements (0: k and 1).  ld = wld = 32 with
+  // wtab = table + 16: [emb 16 | w | pad] line rows (a sharded partition read in place at one rank,
+  // or a replicated table's line copy); DeepFM / DNN / LR only (model_forward checks)
+  int ld = 0, wld = 0;
   const float* y1 = nullptr;       // precomputed first order (L-A irregular index) or nullptr
   float beta = 0.f;
   float* out = nullptr;            // [B]
@@ -154,6 +163,13 @@ void model_release(rmx_model& m);
 int model_load_mats(rmx_model& m, const float* host_mats, bool sync);
 int model_set_precision(rmx_model& m, int dtype);
 int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in);
+// models whose every table read takes a row stride (DeepFM / DNN at k = 16, LR): they can read
+// [emb | w | pad] line rows in place (FwdInputs::ld / wld)
+bool model_reads_lines(const rmx_model& m);
+// the forward's table operands: the line copy when the table has one and the model reads lines
+void table_inputs(const rmx_table& t, const rmx_model& m, FwdInputs& in);
+int table_refresh_lines(rmx_table& t);
+int launch_pack_lines(hipStream_t s, int64_t V, const float* emb, const float* w, float* line);
 int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
                        float bias, const float* weights, const float* embedding, const float* mats,
                        float* out);
@@ -225,7 +241,7 @@ int launch_pack_cin_t(hipStream_t s, const float* mats_dev, int F, CinLayer& c);
 int launch_cin_dz_s3(hipStream_t s, const CinLayer& c, int rows, const float* gpre, int ldg, float* dz, int ldz);
 int launch_cin_layer(hipStream_t s, const CinLayer& L, bool first, bool last, int B, int F, int k,
                      const int32_t* ids, const float* table, const float* u_prev, float* u_out,
-                     float* rowdot);
+                     float* rowdot, int ld = 0);
 int launch_cross_finish(hipStream_t s, int B, int L, const float* xcol, const CrossScalars& cs, float* pre2);
 int launch_cross(hipStream_t s, int B, int F, int k, int L, const int32_t* ids, const void* table, int dt,
                  const float* cross_w, const float* cross_b, const float* wo_x, float* pre2);

@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstring>
 #include <memory>
@@ -97,7 +98,8 @@ struct rmx_shard {
   uint64_t owner_key = RMX_OWNER_HASH_DEFAULT;  // Feistel key of p (set_owner_hash); 0: owner = id mod N
   bool filled = false;                  // rows written (the owner function is then fixed)
   int rs = 0;                           // row stride in floats: [emb k | w | pad], one 128-B line at k < 32
-  std::vector<float*> part;             // partitions held here: [rows_per][rs] (loopback: N)
+  std::vector<float*> part;             // partitions held here: [rows_per + 1][rs] (loopback: N); the
+                                        // extra row stays zero (the row of an out-of-range id read in place)
   // per-batch buffers (grow only)
   int64_t cap_send = 0, cap_recv = 0;
   int64_t cap_slot[2] = {0, 0};         // ids each pull slot's buffers hold (grown one slot at a time)
@@ -118,6 +120,9 @@ struct rmx_shard {
   hipEvent_t ready[2] = {nullptr, nullptr};     // slot filled (recorded on the pull's stream)
   hipEvent_t consumed[2] = {nullptr, nullptr};  // slot read by its forward (on the forward's stream)
   bool consumed_rec[2] = {false, false};
+  // one rank, no dedupe: the slot holds the batch's partition rows p(id) (perm_s), not copied rows --
+  // the forward reads the [emb | w | pad] lines of the partition in place (no exchange, no row copy)
+  bool slot_direct[2] = {false, false};
   int64_t slot_nnz[2] = {-1, -1};               // ids pulled into the slot, -1 = none pending
   // dedupe (step 0): 0 off, 1 on, 2 auto -- on for one batch, then off for the next kAutoSkip
   // batches when it removed under 10 % of the ids (uniform ids over a large V: the hash pass costs
@@ -168,42 +173,51 @@ __device__ __forceinline__ int wave_reserve(int o, int* h) {
 // Routing = count -> scan -> scatter with no global atomics: block b histograms its tile of
 // kRouteTile ids by owner into bcnt[o][b] (wave-aggregated LDS counters), one block per owner scans
 // its column into the tile's start offset, and the scatter pass recomputes the in-tile ranks.
-// The keyed permutation p of [0, V) (OwnerPerm.key == 0: identity).  Feistel rounds over 2h bits
-// (2^(2h) >= V, h >= 1), the round function a splitmix64 finaliser of (half, round, key); inverse = the
-// rounds backwards; cycle-walking keeps it a bijection on [0, V) (every cycle re-enters [0, V)).
+// The keyed permutation p of [0, V) (OwnerPerm.key == 0: identity): a 4-round Feistel network on
+// the square domain Z_a x Z_a, a = ceil(sqrt(V)) (x = L a + R), each round (L, R) -> (R, (L + F_r(R))
+// mod a) with F_r(R) = mulhi(fmix32(R ^ k_r), a) (the murmur3 finaliser; k_r four 32-bit round keys
+// drawn from the key by splitmix64).  Cycle-walked back into [0, V): the domain exceeds V by < 2a,
+// so a walk is rare (none at V = a^2, e.g. V = 10^8); every cycle re-enters [0, V) only if it started
+// there.  All 32-bit integer work, ~40 instructions per id.
 struct OwnerPerm {
   uint64_t key = 0;
-  int h = 1;
+  uint32_t a = 1;
+  uint32_t rk[4] = {0, 0, 0, 0};
   int64_t V = 0;
 };
-__device__ __host__ __forceinline__ uint32_t feistel_f(uint32_t x, int r, uint64_t key, uint32_t mask) {
-  uint64_t z = ((uint64_t)x << 8) ^ (uint64_t)r ^ key;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-  return (uint32_t)(z ^ (z >> 31)) & mask;
+__device__ __host__ __forceinline__ uint32_t owner_round(uint32_t x, uint32_t rk, uint32_t a) {
+  uint32_t h = x ^ rk;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (uint32_t)(((uint64_t)h * a) >> 32);  // uniform in [0, a)
 }
-__device__ __host__ __forceinline__ int64_t feistel_once(int64_t x, const OwnerPerm& op, bool inverse) {
-  const uint32_t mask = (1u << op.h) - 1u;
-  uint32_t L = (uint32_t)(x >> op.h) & mask, R = (uint32_t)x & mask;
+__device__ __host__ __forceinline__ uint32_t feistel_once(uint32_t x, const OwnerPerm& op, bool inverse) {
+  const uint32_t a = op.a;
+  uint32_t L = x / a, R = x - L * a;
   if (!inverse) {
     for (int r = 0; r < 4; ++r) {
-      const uint32_t t = L ^ feistel_f(R, r, op.key, mask);
+      const uint32_t t = owner_round(R, op.rk[r], a);
+      const uint32_t s = L + t;
       L = R;
-      R = t;
+      R = s >= a ? s - a : s;
     }
   } else {
     for (int r = 3; r >= 0; --r) {
-      const uint32_t t = R ^ feistel_f(L, r, op.key, mask);
+      const uint32_t t = owner_round(L, op.rk[r], a);
+      const uint32_t l = R >= t ? R - t : R + a - t;
       R = L;
-      L = t;
+      L = l;
     }
   }
-  return ((int64_t)L << op.h) | R;
+  return L * a + R;
 }
 __device__ __host__ __forceinline__ int64_t owner_perm(int64_t id, const OwnerPerm& op, bool inverse) {
   if (!op.key) return id;
-  int64_t y = feistel_once(id, op, inverse);
-  while (y >= op.V) y = feistel_once(y, op, inverse);
+  uint32_t y = feistel_once((uint32_t)id, op, inverse);
+  while ((int64_t)y >= op.V) y = feistel_once(y, op, inverse);
   return y;
 }
 
@@ -211,9 +225,18 @@ OwnerPerm owner_perm_of(uint64_t key, int64_t V) {
   OwnerPerm op;
   op.key = key;
   op.V = V;
-  int b = 1;
-  while ((int64_t(1) << b) < V) ++b;
-  op.h = std::max(1, (b + 1) / 2);
+  uint64_t a = (uint64_t)std::sqrt((double)std::max<int64_t>(V, 1));
+  while ((int64_t)(a * a) < V) ++a;
+  while (a > 1 && (int64_t)((a - 1) * (a - 1)) >= V) --a;
+  op.a = (uint32_t)a;
+  uint64_t z = key;
+  for (int r = 0; r < 4; ++r) {  // round keys: splitmix64 of the key, successive states
+    z += 0x9E3779B97F4A7C15ULL;
+    uint64_t x = z;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    op.rk[r] = (uint32_t)(x ^ (x >> 31));
+  }
   return op;
 }
 OwnerPerm owner_perm_of(const rmx_shard& sh) { return owner_perm_of(sh.owner_key, sh.V); }
@@ -373,6 +396,17 @@ __global__ __launch_bounds__(256) void own_gather_kernel(int64_t n, int k, int r
   for (int j = 0; j < k; ++j) out_emb[t * k + j] = ok ? row[j] : 0.f;
   out_w[t] = ok ? row[k] : 0.f;
   perm[t] = (int32_t)t;
+}
+
+// One rank, read in place: rows[n] = p(ids[n]), the partition row of id n (an id outside [0, V)
+// gets the zero row `zrow`).  The forward then gathers the [emb | w | pad] lines straight from the
+// partition: no route, no row copy.
+__global__ __launch_bounds__(256) void own_rows_kernel(int64_t n, const int32_t* __restrict__ ids, int32_t zrow,
+                                                      int32_t* __restrict__ rows, OwnerPerm op) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int id = ids[i];
+  rows[i] = (id >= 0 && id < op.V) ? (int32_t)owner_perm(id, op, false) : zrow;
 }
 
 // step 0: insert ids[n] into the hash set; hslot[n] = its slot (first inserter claims an empty one)
@@ -706,7 +740,7 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
   const int parts = sh->loopback ? N : 1;
   for (int p = 0; p < parts; ++p) {
     float* r = nullptr;
-    if (hipMalloc(&r, sizeof(float) * sh->rows_per * sh->rs) != hipSuccess) {
+    if (hipMalloc(&r, sizeof(float) * (sh->rows_per + 1) * sh->rs) != hipSuccess) {
       for (float* q : sh->part) (void)hipFree(q);
       set_error("rmx_shard_create: out of device memory for the partition");
       return RMX_E_NOMEM;
@@ -770,6 +804,7 @@ int shard_fill_synthetic(rmx_shard& sh, uint64_t seed) {
   hipStream_t s = sh.ctx->stream;
   const float scale = 0.05f * (1.0f / 8388608.0f);
   const int64_t tot = sh.rows_per * sh.rs;
+  for (float* q : sh.part) RMX_HIP(hipMemsetAsync(q + tot, 0, sizeof(float) * sh.rs, s));  // the zero row
   for (size_t p = 0; p < sh.part.size(); ++p) {
     const int part = sh.loopback ? (int)p : sh.rank;
     hipLaunchKernelGGL(shard_fill_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, seed, sh.V,
@@ -963,6 +998,54 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   return err;
 }
 
+// The in-place read at one rank (no dedupe, k = 16 line rows): fills perm_s[slot] with the batch's
+// partition rows.  Returns false (nothing done) when the shard does not qualify.
+bool direct_eligible(const rmx_shard& sh) {
+  return sh.N == 1 && !sh.loopback && sh.dedupe != 1 && sh.k == 16 && sh.rs == 32 && sh.rows_per < (int64_t(1) << 31);
+}
+
+int shard_map_rows(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot) {
+  int st;
+  if ((st = ensure_batch(sh, nnz, slot))) return st;
+  sh.last_sent = nnz;
+  sh.last_sent_dev = false;
+  if (nnz <= 0) return RMX_OK;
+  hipLaunchKernelGGL(own_rows_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, d_ids,
+                     (int32_t)sh.rows_per, sh.perm_s[slot], owner_perm_of(sh));
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+// the forward of a directly-mapped slot: in place for models that read line rows, else the rows
+// are copied out first (owner gather through the mapped rows) and the forward runs on them in batch
+// order (implicit ids n)
+int forward_direct(rmx_model& m, rmx_shard& sh, hipStream_t s, int B, const int32_t* rows, int slot, float* d_out) {
+  FwdInputs in;
+  in.B = B;
+  in.dtype = kF32;
+  in.beta = m.beta;
+  in.out = d_out;
+  if (model_reads_lines(m)) {
+    in.ids = rows;
+    in.table = sh.part[0];
+    in.wtab = sh.part[0] + sh.k;
+    in.ld = sh.rs;
+    in.wld = sh.rs;
+    return model_forward(m, s, in);
+  }
+  const int64_t n = (int64_t)B * m.F;
+  int st;
+  {
+    StageTimer t(m, s, "shard_exchange");
+    if ((st = launch_owner_gather(s, n, sh.k, sh.rs, rows, sh.part[0], sh.recv_emb_s[slot], sh.recv_w_s[slot])))
+      return st;
+  }
+  in.ids = nullptr;  // rows in batch order
+  in.table = sh.recv_emb_s[slot];
+  in.wtab = sh.recv_w_s[slot];
+  return model_forward(m, s, in);
+}
+
 }  // namespace rmx
 
 // ------------------------------------------------------------------ C ABI --
@@ -1132,8 +1215,10 @@ extern "C" int rmx_shard_pull(rmx_shard* sh, int64_t n, const int32_t* d_ids, in
     }
   // the slot's previous forward must have read it before the exchange overwrites it
   if (sh->consumed_rec[slot]) RMX_HIP(hipStreamWaitEvent(s, sh->consumed[slot], 0));
-  int st = shard_exchange(*sh, s, n, d_ids, slot);
+  const bool direct = direct_eligible(*sh);
+  int st = direct ? shard_map_rows(*sh, s, n, d_ids, slot) : shard_exchange(*sh, s, n, d_ids, slot);
   if (st) return st;
+  sh->slot_direct[slot] = direct;
   RMX_HIP(hipEventRecord(sh->ready[slot], s));
   sh->slot_nnz[slot] = n;
   return RMX_OK;
@@ -1178,7 +1263,11 @@ extern "C" int rmx_forward_pulled(rmx_model* m, rmx_shard* sh, int32_t B, int sl
     w = sh->recv_w_s[slot];
   }
   int st;
-  {
+  if (sh->slot_direct[slot]) {
+    ModelUse use(*m, s);
+    if (use.st) return use.st;
+    st = forward_direct(*m, *sh, s, B, perm, slot, d_out);
+  } else {
     ModelUse use(*m, s);
     if (use.st) return use.st;
     FwdInputs in;
@@ -1232,6 +1321,15 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
   }
   if (sh->consumed_rec[0]) RMX_HIP(hipStreamWaitEvent(s, sh->consumed[0], 0));
   int st;
+  if (direct_eligible(*sh)) {
+    // one rank: the batch's partition rows, then the forward reads the lines in place
+    {
+      StageTimer t(*m, s, "shard_exchange");
+      st = shard_map_rows(*sh, s, (int64_t)B * m->F, d_ids, 0);
+    }
+    if (st) return st;
+    return forward_direct(*m, *sh, s, B, sh->perm_s[0], 0, d_out);
+  }
   {
     StageTimer t(*m, s, "shard_exchange");
     st = shard_exchange(*sh, s, (int64_t)B * m->F, d_ids, 0);

@@ -1202,6 +1202,10 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     set_error("backward: DCN crossDepth must be <= " + std::to_string(kMaxFusedCross));
     return RMX_E_INVALID;
   }
+  if ((in.ld > 0 && in.ld != m.k) || in.wld > 1) {
+    set_error("backward: line-row (strided) tables are forward-only");
+    return RMX_E_INVALID;
+  }
   if (B <= 0) return RMX_OK;
   int st = model_ensure_ws(m, B);  // y12 (first order + FM) lives in the inference workspace
   if (st) return st;

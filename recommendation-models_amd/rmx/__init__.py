@@ -200,6 +200,10 @@ class EmbeddingTable:
     def fill_synthetic(self, seed):
         check(_lib.lib.rmx_table_fill_synthetic(self.handle, int(seed)))
 
+    def refresh_lines(self):
+        """Rebuild (or, with knob table_lines 0, drop) the [rows][32] line copy of an fp32 k = 16 table."""
+        check(_lib.lib.rmx_table_refresh_lines(self.handle))
+
     def gather(self, ids_dev, n, w_out=None, emb_out=None, stream=None):
         """Debug gather (makeWeights / makeEmbeddings): bit-exact copies into device buffers."""
         check(_lib.lib.rmx_gather(self.handle, int(n), ids_dev.ptr, w_out.ptr if w_out else None,

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("rmx_table_fill_synthetic", c_int, [c_vp, c_u64]),
     ("rmx_table_rows", c_i64, [c_vp]),
     ("rmx_table_embedding_dim", c_int, [c_vp]),
+    ("rmx_table_refresh_lines", c_int, [c_vp]),
     ("rmx_table_device_ptrs", c_int, [c_vp, P(c_vp), P(c_vp)]),
     ("rmx_backward", c_int, [c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp,
                              c_vp, c_vp]),

@@ -17,40 +17,57 @@ OWNER_HASH_DEFAULT = 0x5EED5A4D0C7A11ED  # include/rmx.h RMX_OWNER_HASH_DEFAULT
 _M64 = (1 << 64) - 1
 
 
-def _feistel_f(x, r, key, mask):
-    z = ((x << np.uint64(8)) ^ np.uint64(r) ^ np.uint64(key)) & np.uint64(_M64)
-    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-    return (z ^ (z >> np.uint64(31))) & np.uint64(mask)
+def _round_keys(key):
+    z, rk = key, []
+    for _ in range(4):  # splitmix64 of the key, successive states
+        z = (z + 0x9E3779B97F4A7C15) & _M64
+        x = z
+        x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+        x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+        rk.append((x ^ (x >> 31)) & 0xFFFFFFFF)
+    return rk
 
 
-def _half_bits(V):
-    b = 1
-    while (1 << b) < V:
-        b += 1
-    return max(1, (b + 1) // 2)
+def _side(V):
+    a = int(np.sqrt(max(V, 1)))
+    while a * a < V:
+        a += 1
+    while a > 1 and (a - 1) * (a - 1) >= V:
+        a -= 1
+    return a
+
+
+def _round(x, rk, a):
+    """F_r(x) = mulhi(fmix32(x ^ k_r), a): uniform in [0, a) (shard.hip owner_round)."""
+    h = (x ^ np.uint64(rk)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return (h * np.uint64(a)) >> np.uint64(32)
 
 
 def owner_perm(ids, key, V, inverse=False):
-    """p(ids) (shard.hip owner_perm): 4 Feistel rounds on 2h bits, cycle-walked back into [0, V)."""
+    """p(ids) (shard.hip owner_perm): 4 Feistel rounds on Z_a x Z_a (a = ceil(sqrt(V))), each
+    (L, R) -> (R, (L + F_r(R)) mod a), cycle-walked back into [0, V); key 0 = identity."""
     ids = np.asarray(ids, np.int64)
     if not key:
         return ids.copy()
-    h = _half_bits(V)
-    mask = (1 << h) - 1
-    hb, mk = np.uint64(h), np.uint64(mask)
+    a = _side(V)
+    rk = _round_keys(key)
+    A = np.uint64(a)
 
     def once(x):
         x = x.astype(np.uint64)
-        L, R = (x >> hb) & mk, x & mk
-        rounds = range(3, -1, -1) if inverse else range(4)
-        with np.errstate(over="ignore"):
-            for r in rounds:
-                if inverse:
-                    L, R = R ^ _feistel_f(L, r, key, mask), L
-                else:
-                    L, R = R, L ^ _feistel_f(R, r, key, mask)
-        return ((L << hb) | R).astype(np.int64)
+        L, R = x // A, x % A
+        if not inverse:
+            for r in range(4):
+                L, R = R, (L + _round(R, rk[r], a)) % A
+        else:
+            for r in range(3, -1, -1):
+                L, R = (R + A - _round(L, rk[r], a)) % A, L
+        return (L * A + R).astype(np.int64)
 
     y = once(ids)
     out = y >= V

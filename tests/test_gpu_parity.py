@@ -264,3 +264,42 @@ def test_xdeepfm_cin3x200_config(ctx):
     index = np.repeat(np.arange(B, dtype=np.int64), F)
     ref = oc.forward(om, B, index, np.array([0.01], np.float32), w, e, mats, 1)
     assert np.abs(out.numpy() - ref).max() <= TOL
+
+
+# ------------------------------------------------- line-row tables (rmx_table::line) ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "dnn", "lr", "xdeepfm", "dcn", "pnn"])
+@pytest.mark.parametrize("B", [1, 300, 65536])
+def test_line_table_forward_bitwise_equals_row_table(kind, B):
+    """fp32 k = 16 tables keep a [V][32] [emb | w | pad] line copy that DeepFM / DNN / LR forwards read
+    (one memory line per id); the gathers are copies, so every model's output is BITWISE the one read
+    from the plain emb / w arrays (knob table_lines 0), through forward_ids and the predict loop."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K = 100_003, 39, 16
+    fc = [400, 400, 400] if B == 65536 else [64, 32]
+    m = {"deepfm": lambda: rmx.DeepFM(V, F, K, fc), "dnn": lambda: rmx.DNN(V, F, K, fc), "lr": lambda: rmx.LR(V, F),
+         "xdeepfm": lambda: rmx.XDeepFM(V, F, K, fc, [48, 32]), "dcn": lambda: rmx.DCN(V, F, K, 3, fc),
+         "pnn": lambda: rmx.PNN(V, F, K, fc)}[kind]()
+    if kind != "lr":
+        m.setMats(m.initMats(0x3A75))
+    m.setBias(0.01)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, 0x5EED2026, 17, B, F, V, ids)
+    outs = []
+    for lines in (1, 0):
+        rmx.set_tuning("table_lines", lines)
+        try:
+            t = rmx.EmbeddingTable(ctx, V, K)
+            t.fill_synthetic(0x7AB1E)
+        finally:
+            rmx.set_tuning("table_lines", None)
+        o = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(t, B, ids, o)
+        p = rmx.DeviceArray(ctx, B, np.float32)
+        m.predict_ids(t, B, ids, p, batch=max(1, B // 3))
+        ctx.sync()
+        outs.append((o.numpy(), p.numpy()))
+        t.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][0], outs[0][1])

@@ -678,3 +678,30 @@ def test_out_of_range_ids_do_not_hang_the_route(N):
     keep = np.setdiff1d(np.arange(B), bad_rows)
     assert np.array_equal(got.numpy()[keep], ref.numpy()[keep])
     assert np.isfinite(got.numpy()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn", "pnn", "lr"])
+def test_rccl_single_rank_reads_partition_in_place(kind):
+    """One rank (no dedupe): no exchange and no row copy -- the batch's ids map to partition rows p(id)
+    and DeepFM / DNN / LR read the [emb | w | pad] lines in place; the other models copy the mapped
+    rows out first.  Every model bitwise equals the replicated table, one-shot and pipelined."""
+    import rmx
+    ctx, ctx_x = rmx.default_context(), rmx.Context(0)
+    V, B = 100_003, 700
+    table, ids = _setup(ctx, V, B, seed_row=41)
+    m = _models()[kind]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    sh = rmx.ShardedTable(ctx, V, K, 1, 0, rmx.comm_unique_id())
+    sh.fill_synthetic(SEED_TAB)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    got = rmx.DeviceArray(ctx, B, np.float32)
+    got2 = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids, ref)
+    m.forward_ids_sharded(sh, B, ids, got)
+    ctx.sync()
+    sh.pull(ids, B * F, 1, ctx_x.stream)
+    m.forward_pulled(sh, B, 1, got2, ctx.stream)
+    ctx.sync()
+    assert np.array_equal(got.numpy(), ref.numpy()) and np.array_equal(got2.numpy(), ref.numpy())

@@ -64,6 +64,10 @@ for s in $STEPS; do
               run settle_$ms 200 python bench.py --steps 20 --warmup 5 --no-companion --no-cpu-baseline --settle-ms $ms
             done ;;
     list) run list 120 rocprofv3 -L ;;
+    ablines) run ab_lines1 300 python bench.py --no-companion --no-cpu-baseline --steps 200 &&
+         run ab_lines0 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 &&
+         run ab_lines1b 300 python bench.py --no-companion --no-cpu-baseline --steps 200 &&
+         run ab_lines0b 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
     bench2s) echo "== bench_gpus2_sharded (expects a clean refusal on a 1-GPU box)" | tee -a "$OUT/steps.log"
          timeout -k 10 300 python bench.py --workload deepfm_sharded --gpus 2 --steps 5 --warmup 1 \
