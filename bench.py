@@ -780,7 +780,7 @@ def main():
             "config": config_of(args.workload, r, world, args.zipf),
             **({"table_layout": "[V][32] fp32 line rows [emb 16 | w | pad]: one 128-B memory line per id "
                                 "(rmx_table::line, knob table_lines)"}
-               if args.workload == "deepfm" and rmx.get_tuning("table_lines", 1) else {}),
+               if args.workload == "deepfm" and rmx.get_tuning("table_lines", 0) else {}),
             **({"exchange": r["exchange"]} if "exchange" in r else {}),
             "roofline": r["roofline"],
             "cpu_baseline": cpu,

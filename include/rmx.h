@@ -179,9 +179,10 @@ int rmx_table_upload(rmx_table* t, const float* weights, const float* embedding,
 int rmx_table_fill_synthetic(rmx_table* t, uint64_t seed);
 int64_t rmx_table_rows(const rmx_table* t);
 int rmx_table_embedding_dim(const rmx_table* t);  /* k of the table (-1: NULL) */
-/* fp32 k = 16 tables also hold a [rows][32] line copy ([emb 16 | w | pad]: one 128-B memory line per
- * id) that DeepFM / DNN / LR forwards read; every upload / fill rebuilds it (knob "table_lines" 0:
- * none).  After writing the table through rmx_table_device_ptrs, call rmx_table_refresh_lines. */
+/* With knob "table_lines" 1 (default 0), fp32 k = 16 tables also hold a [rows][32] line copy
+ * ([emb 16 | w | pad]: one 128-B memory line per id) that DeepFM / DNN / LR forwards read; every
+ * upload / fill rebuilds it.  After writing the table through rmx_table_device_ptrs, call
+ * rmx_table_refresh_lines (it also builds or drops the copy after the knob changes). */
 int rmx_table_refresh_lines(rmx_table* t);
 /* Device pointers of the table (for debugging/parity only; elements of the table's dtype). */
 int rmx_table_device_ptrs(const rmx_table* t, void** d_weights, void** d_embedding);

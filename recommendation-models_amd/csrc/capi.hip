@@ -303,7 +303,7 @@ extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
 // the [V][32] line copy of an fp32 k = 16 table (rmx_table::line), rebuilt from emb / w; knob
 // "table_lines" 0 drops it (the forward then reads emb / w)
 int rmx::table_refresh_lines(rmx_table& t) {
-  const bool want = t.dtype == RMX_DTYPE_F32 && t.k == 16 && tuning_get("table_lines", 1) != 0;
+  const bool want = t.dtype == RMX_DTYPE_F32 && t.k == 16 && tuning_get("table_lines", 0) != 0;
   if (!want) {
     if (t.line) {
       RMX_HIP(hipStreamSynchronize(t.ctx->stream));

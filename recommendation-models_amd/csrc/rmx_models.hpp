@@ -21,10 +21,12 @@ struct rmx_table {
   int dtype = 0;          // RMX_DTYPE_F32 / RMX_DTYPE_BF16 (elements of w and emb)
   void* w = nullptr;      // [V]     first-order weights (Angel "weights" row 0)
   void* emb = nullptr;    // [V][k]  embeddings, row-major (Angel "embedding" rows 0..k-1, transposed)
-  // fp32 k = 16 tables (knob "table_lines", default on): a [V][32] line copy, row = [emb 16 | w | pad 15]
-  // -- one 128-B memory line per id instead of a 64-B row line plus a separate weight line.  Rebuilt
-  // from emb / w by every upload / fill (rmx_table_refresh_lines after writes through device_ptrs);
-  // read by the models whose every table access takes a row stride (rmx::model_reads_lines).
+  // fp32 k = 16 tables with knob "table_lines" 1 (default 0): a [V][32] line copy, row = [emb 16 | w |
+  // pad 15] -- one 128-B memory line per id instead of a 64-B row line plus a separate weight line.
+  // Rebuilt from emb / w by every upload / fill (rmx_table_refresh_lines after writes through
+  // device_ptrs); read by the models whose every table access takes a row stride
+  // (rmx::model_reads_lines).  Measured ~1 % SLOWER for DeepFM layer 1 at V = 1M (0.1851 vs 0.1829 ms,
+  // two A/B pairs on one box): the weight lines it saves hit the Infinity Cache, so it is off.
   float* line = nullptr;
 };
 

@@ -398,6 +398,11 @@ __global__ __launch_bounds__(256) void own_gather_kernel(int64_t n, int k, int r
   perm[t] = (int32_t)t;
 }
 
+__global__ __launch_bounds__(256) void iota_kernel(int64_t n, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)i;
+}
+
 // One rank, read in place: rows[n] = p(ids[n]), the partition row of id n (an id outside [0, V)
 // gets the zero row `zrow`).  The forward then gathers the [emb | w | pad] lines straight from the
 // partition: no route, no row copy.
@@ -1039,8 +1044,15 @@ int forward_direct(rmx_model& m, rmx_shard& sh, hipStream_t s, int B, const int3
     StageTimer t(m, s, "shard_exchange");
     if ((st = launch_owner_gather(s, n, sh.k, sh.rs, rows, sh.part[0], sh.recv_emb_s[slot], sh.recv_w_s[slot])))
       return st;
+    // the rows are in batch order now: the slot's row list becomes the identity (stream-ordered after
+    // the gather read it), so the forward runs the same id-array kernels as every other path
+    if (n > 0) {
+      hipLaunchKernelGGL(iota_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n,
+                         const_cast<int32_t*>(rows));
+      RMX_HIP(hipGetLastError());
+    }
   }
-  in.ids = nullptr;  // rows in batch order
+  in.ids = rows;
   in.table = sh.recv_emb_s[slot];
   in.wtab = sh.recv_w_s[slot];
   return model_forward(m, s, in);

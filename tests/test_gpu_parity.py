@@ -271,9 +271,10 @@ def test_xdeepfm_cin3x200_config(ctx):
 @pytest.mark.parametrize("kind", ["deepfm", "dnn", "lr", "xdeepfm", "dcn", "pnn"])
 @pytest.mark.parametrize("B", [1, 300, 65536])
 def test_line_table_forward_bitwise_equals_row_table(kind, B):
-    """fp32 k = 16 tables keep a [V][32] [emb | w | pad] line copy that DeepFM / DNN / LR forwards read
-    (one memory line per id); the gathers are copies, so every model's output is BITWISE the one read
-    from the plain emb / w arrays (knob table_lines 0), through forward_ids and the predict loop."""
+    """With knob table_lines 1, fp32 k = 16 tables keep a [V][32] [emb | w | pad] line copy that
+    DeepFM / DNN / LR forwards read (one memory line per id); the gathers are copies, so every model's
+    output is BITWISE the one read from the plain emb / w arrays (table_lines 0), through forward_ids
+    and the predict loop."""
     import rmx
     ctx = rmx.default_context()
     V, F, K = 100_003, 39, 16

@@ -68,6 +68,13 @@ for s in $STEPS; do
          run ab_lines0 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 &&
          run ab_lines1b 300 python bench.py --no-companion --no-cpu-baseline --steps 200 &&
          run ab_lines0b 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 ;;
+    lines) for wl in deepfm_sharded dcn_bf16 pnn_bf16 lr_plumbing deepfm_train xdeepfm_train; do
+             run line_$wl 400 python bench.py --workload $wl --steps 100 --warmup 10 || exit $?
+             grep '^{' "$OUT/line_$wl.log" | tail -n 1 > "$OUT/line_$wl.json"
+           done ;;
+    blas) run probe_blas 300 python tools/probe_blas.py ;;
+    profx20) run profx20 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx20" -o xdeepfm -- \
+            python3 bench.py --workload xdeepfm --gpus 1 --steps 20 --warmup 5 ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
     bench2s) echo "== bench_gpus2_sharded (expects a clean refusal on a 1-GPU box)" | tee -a "$OUT/steps.log"
          timeout -k 10 300 python bench.py --workload deepfm_sharded --gpus 2 --steps 5 --warmup 1 \
