@@ -75,6 +75,21 @@ for s in $STEPS; do
     blas) run probe_blas 300 python tools/probe_blas.py ;;
     profx20) run profx20 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx20" -o xdeepfm -- \
             python3 bench.py --workload xdeepfm --gpus 1 --steps 20 --warmup 5 ;;
+    ab:*) kv=${s#ab:}   # ab:<knob>=<v1>/<v2>: DeepFM and xDeepFM, v1 v2 v1 v2 at 200 / 60 steps
+         knob=${kv%%=*}; vals=${kv#*=}; v1=${vals%/*}; v2=${vals#*/}
+         i=0
+         for v in $v1 $v2 $v1 $v2; do i=$((i+1))
+           run ab_${knob}_${v}_${i}_d 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set $knob=$v || exit $?
+           run ab_${knob}_${v}_${i}_x 300 python bench.py --workload xdeepfm --no-cpu-baseline --steps 60 --warmup 5 --set $knob=$v || exit $?
+         done ;;
+    abt:*) kv=${s#abt:}   # abt:<knob>=<v1>/<v2>: DeepFM / xDeepFM training, v1 v2 v1 v2
+         knob=${kv%%=*}; vals=${kv#*=}; v1=${vals%/*}; v2=${vals#*/}; i=0
+         for v in $v1 $v2 $v1 $v2; do i=$((i+1))
+           run abt_${knob}_${v}_${i}_d 300 python bench.py --workload deepfm_train --steps 60 --warmup 5 --set $knob=$v || exit $?
+           run abt_${knob}_${v}_${i}_x 300 python bench.py --workload xdeepfm_train --steps 20 --warmup 3 --set $knob=$v || exit $?
+         done ;;
+    testk:*) k=${s#testk:}
+         run pytest_$k 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k $k ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
     bench2s) echo "== bench_gpus2_sharded (expects a clean refusal on a 1-GPU box)" | tee -a "$OUT/steps.log"
          timeout -k 10 300 python bench.py --workload deepfm_sharded --gpus 2 --steps 5 --warmup 1 \
