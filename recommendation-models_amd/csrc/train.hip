@@ -770,147 +770,6 @@ __global__ __launch_bounds__(TT == 64 ? 256 : 512, SB ? 4 : 1) void wgrad_s3_ker
     }
 }
 
-// The single-buffered 128 x 128 split dW with 16-B staging loads (knob "wgrad_v4", default 1; the
-// tower's dW, not the CIN's generated operand).  wgrad_s3_kernel<128, false, true> stages with 4-B
-// loads, 16 per thread per 32-row chunk (a thread owns one column x 8 rows), which dominated the
-// kernel.  Here a thread owns 4 consecutive columns x 4 rows of one operand: 4 float4
-// loads per chunk, split into three bf16 planes and written as 8-B pieces of an LDS image
-// [op][plane][col][5 slots of 16 B] -- 4 row octets + 1 pad, an 80-B column stride: the 8-B stores of
-// a 16-lane group (two columns 320 B apart) and the 16-B fragment reads of 16 consecutive columns
-// (starts 20 banks apart) are both conflict-free without the XOR swizzle.  The MFMA operands, their
-// K order and the MFMA sequence are those of wgrad_s3_kernel: bitwise the same gradients.
-constexpr int kV4S = 5;  // 16-B slots per LDS column
-__device__ __forceinline__ void wg_split4(const float* v, __bf16* hi, __bf16* mi, __bf16* lo) {
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const __bf16 h = (__bf16)v[q];
-    const float r = v[q] - (float)h;
-    const __bf16 m = (__bf16)r;
-    hi[q] = h;
-    mi[q] = m;
-    lo[q] = (__bf16)(r - (float)m);
-  }
-}
-
-__global__ __launch_bounds__(512, 4) void wgrad_v4_kernel(int rows, int N, int K, const float* __restrict__ A, int lda,
-                                                          const float* __restrict__ X, int ldx, int rows_per_slice,
-                                                          int tiles, float* __restrict__ part, int vec) {
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-  constexpr int TT = 128, WJ = 4, TI = 4, TJ = 2;
-  extern __shared__ __attribute__((aligned(16))) wg_bf16x8 wlds[];
-  auto L = [&](int op, int pl) { return wlds + (op * 3 + pl) * TT * kV4S; };
-  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bid = blockIdx.x, xcd = bid & 7, idx = bid >> 3;
-  const int slice = (idx / tiles) * 8 + xcd, tile = idx % tiles;
-  const int ntn = (N + TT - 1) / TT;
-  const int n0 = (tile % ntn) * TT, k0 = (tile / ntn) * TT;
-  const int r_begin = slice * rows_per_slice;
-  const int r_end = min(rows, r_begin + rows_per_slice);
-  const int nch = r_end > r_begin ? (r_end - r_begin + kWgR - 1) / kWgR : 0;
-  // staging item: operand op (waves 0-3: A = dPre columns n0.., waves 4-7: X columns k0..), columns
-  // c4 .. c4 + 3 of the tile, rows 4 hh .. 4 hh + 3 of the chunk
-  const int op = tid >> 8, q = tid & 255, c4 = (q >> 3) * 4, hh = q & 7;
-  const float* src = op ? X : A;
-  const int ld = op ? ldx : lda, c0 = (op ? k0 : n0) + c4, lim = op ? K : N;
-  const bool full = vec && c0 + 3 < lim;
-  float v[4][4];  // [row][col]
-  auto gload = [&](int c) {
-    const int r0 = r_begin + c * kWgR + 4 * hh;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = r0 + e;
-      const float* p = src + (int64_t)r * ld + c0;
-      if (r < r_end && full) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(p);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[e][j] = t[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[e][j] = (r < r_end && c0 + j < lim) ? p[j] : 0.f;
-      }
-    }
-  };
-  auto sstore = [&]() {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float col[4] = {v[0][j], v[1][j], v[2][j], v[3][j]};
-      bf16x4_t p0, p1, p2;
-      __bf16 h0[4], h1[4], h2[4];
-      wg_split4(col, h0, h1, h2);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        p0[e] = h0[e];
-        p1[e] = h1[e];
-        p2[e] = h2[e];
-      }
-      // bf16 element offset: column (c4 + j) at 8 kV4S elements, rows 4 hh .. at 4 hh
-      const int o = (c4 + j) * (8 * kV4S) + 4 * hh;
-      *reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(L(op, 0)) + o) = p0;
-      *reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(L(op, 1)) + o) = p1;
-      *reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(L(op, 2)) + o) = p2;
-    }
-  };
-  const int wi = wid / WJ, wj = wid - (wid / WJ) * WJ, g = lane >> 4, r16 = lane & 15;
-  f32x4 acc[TI][TJ];
-#pragma unroll
-  for (int a = 0; a < TI; ++a)
-#pragma unroll
-    for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&]() {
-    wg_bf16x8 fa[3], fx[TJ][3];
-#pragma unroll
-    for (int t = 0; t < TJ; ++t) {
-      const int cx = wj * TJ * 16 + t * 16 + r16;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) fx[t][pl] = L(1, pl)[cx * kV4S + g];
-    }
-#pragma unroll
-    for (int ai = 0; ai < TI; ++ai) {
-      const int ca = wi * TI * 16 + ai * 16 + r16;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) fa[pl] = L(0, pl)[ca * kV4S + g];
-#pragma unroll
-      for (int b = 0; b < TJ; ++b) {
-        f32x4 d = acc[ai][b];
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[b][1], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fx[b][0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[b][2], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[b][0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[b][1], d, 0, 0, 0);
-        acc[ai][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[b][0], d, 0, 0, 0);
-      }
-    }
-  };
-  if (nch > 0) {
-    gload(0);
-    sstore();
-  }
-  if (nch > 1) gload(1);
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    compute();
-    __syncthreads();  // every wave is done reading the one buffer
-    if (c + 1 < nch) {
-      sstore();
-      if (c + 2 < nch) gload(c + 2);
-    }
-    __syncthreads();
-  }
-  float* out = part + (int64_t)slice * N * K;
-#pragma unroll
-  for (int a = 0; a < TI; ++a)
-#pragma unroll
-    for (int b = 0; b < TJ; ++b) {
-      const int k = k0 + wj * TJ * 16 + b * 16 + r16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wi * TI * 16 + a * 16 + 4 * g + r;
-        if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][b][r];
-      }
-    }
-}
-
 // The same single-buffered split dW on a 208 x 128 tile (knob "wgrad_nk", default on for the CIN): n (the dPre /
 // gpre columns) in 13 MFMA tiles, so N = 400 pads to 416 and the CIN's N = 200 to 208 instead of 512 /
 // 256 on the square 128 tiles (19-28 % fewer MFMAs, fewer blocks); k in 128.  8 waves, wave w owns
@@ -1141,11 +1000,6 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     else
       hipLaunchKernelGGL(wgrad_nk_kernel<false>, dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, z);
-  } else if (var == 2 && !zg && tuning_get("wgrad_sb", 1) != 0 && tuning_get("wgrad_v4", 1) != 0) {
-    const size_t lds = sizeof(wg_bf16x8) * 2 * 3 * 128 * kV4S;  // 60 KiB: two blocks per CU
-    const int vec = lda % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)X & 15) == 0;
-    hipLaunchKernelGGL(wgrad_v4_kernel, dim3(tiles * S), dim3(512), lds, s, rows, N, K, A, lda, X, ldx, rps, tiles,
-                       T.part2, vec);
   } else if (var == 2 && tuning_get("wgrad_sb", 1) != 0) {
     const size_t lds = sizeof(wg_bf16x8) * 2 * 3 * 128 * 4;  // 48 KiB
     if (zg)

@@ -252,11 +252,10 @@ def test_backward_weight_grad_variants(kind, variant, gz):
 @pytest.mark.parametrize("kind,gz", [("deepfm", 128), ("xdeepfm", 128), ("xdeepfm", 64), ("dcn", 128), ("pnn", 128)])
 @pytest.mark.parametrize("B", [512, 4099])
 def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
-    """dW on the single-buffered split kernel (wgrad_sb 1: 128 x 128 tiles, two blocks per CU -- for the
-    tower's dW the 16-B-staging wgrad_v4_kernel, for the CIN's generated operand the 4-B one; 2: the
+    """dW on the single-buffered split kernel (wgrad_sb 1: 128 x 128 tiles, two blocks per CU; 2: the
     64 x 64 tiles too) stages the same chunks and issues the same MFMA sequence per output as the
-    double-buffered one (wgrad_sb 0): every gradient is bitwise equal, tower / CIN / cross dW alike
-    (PNN: K = 624 + 741 columns, the ragged last float4 of a row staged by scalar loads)."""
+    double-buffered one (wgrad_sb 0): every gradient is bitwise equal, tower / CIN / cross / product
+    dW alike (PNN: K = 624 + 741 columns)."""
     import rmx
     ctx = rmx.default_context()
     V, F, K, fc = 20_000, 39, 16, (400, 400, 400)
@@ -296,16 +295,7 @@ def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
         rmx.set_tuning("wgrad_sb", None)
         rmx.set_tuning("wgrad_gz", None)
         rmx.set_tuning("wgrad_nk", None)
-    rmx.set_tuning("wgrad_v4", 0)  # the 4-B-staging single-buffered kernel
-    rmx.set_tuning("wgrad_gz", gz)
-    rmx.set_tuning("wgrad_nk", 0)
-    try:
-        res["v4off"] = grads()
-    finally:
-        rmx.set_tuning("wgrad_v4", None)
-        rmx.set_tuning("wgrad_gz", None)
-        rmx.set_tuning("wgrad_nk", None)
-    for sb in (1, 2, "v4off"):
+    for sb in (1, 2):
         for a, b in zip(res[0], res[sb]):
             assert np.array_equal(a, b)
     assert np.isfinite(res[1][3]).all() and np.abs(res[1][3]).max() > 0
