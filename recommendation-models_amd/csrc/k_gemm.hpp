@@ -62,7 +62,8 @@ __device__ __forceinline__ void vm_wait(int n) {
 
 // Diagnostic builds only (tools/diag_build.sh; never set in librmx.so): 1 = no A split,
 // 2 = no per-step barrier, 4 = no MFMAs in the split GEMM, 32 = no epilogue global stores of the
-// activations.  Results are wrong; timings isolate costs.
+// activations, 512 = no stored-activation epilogue at all (no LDS transpose either).  Results are
+// wrong; timings isolate costs.
 #ifndef RMX_GEMM_DIAG
 #define RMX_GEMM_DIAG 0
 #endif
@@ -1140,6 +1141,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   // Stored activations go through LDS (each wave transposes its rows into a private slab of the
   // now idle stage buffers) so the global stores are whole-row float4s instead of 4-B scatters.
   auto store_rows = [&](float* dst, int ldd) {
+    if constexpr ((RMX_GEMM_DIAG & 512) != 0) return;  // diagnostic: no epilogue transpose, no stores
     using EG = EpiGeom<T, STAGE>;
     constexpr int RW = EG::RW, NTH = EG::NTH, LD = EG::LD;
     float* wbuf = smem + wid * RW * LD;
