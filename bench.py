@@ -655,6 +655,21 @@ def launch_ranks(n, argv, script=None, grace_s=10.0):
     def pump():  # rank 0's stdout, read while it runs (a full pipe would block the rank)
         for line in procs[0].stdout:
             out0.append(line)
+
+    def forward(signum, _frame):  # a launcher stopped by its caller stops (and reaps) its ranks: no orphans
+        for pr in procs:
+            if pr.poll() is None:
+                pr.send_signal(signum)
+        t_end = time.time() + grace_s
+        for pr in procs:
+            try:
+                pr.wait(max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                pr.kill()
+                pr.wait()
+        raise SystemExit(128 + signum)
+    for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP):
+        signal.signal(sig, forward)
     th = threading.Thread(target=pump, daemon=True)
     th.start()
     status = 0

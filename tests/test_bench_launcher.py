@@ -71,3 +71,31 @@ def test_bench_cli_launcher_exit_status(tmp_path):
                         "0", "--no-cpu-baseline", "--settle-ms", "0"], env=env, capture_output=True, timeout=600)
     assert p.returncode != 0
     assert b"exited with status" in p.stderr
+
+
+def test_launcher_forwards_sigterm_to_its_ranks(tmp_path):
+    """A launcher stopped by its caller (the driver's time limit) stops its ranks: none outlives it."""
+    import signal
+    import time
+    script = tmp_path / "rank.py"
+    script.write_text("import os, time\nopen(os.environ['OUTDIR'] + '/pid%s' % os.environ['RANK'], 'w')"
+                      ".write(str(os.getpid()))\ntime.sleep(120)\n")
+    launcher = tmp_path / "launch.py"
+    launcher.write_text("import sys\nsys.path.insert(0, %r)\nimport bench\n"
+                        "raise SystemExit(bench.launch_ranks(2, [], script=%r))\n" % (ROOT, str(script)))
+    env = dict(os.environ, OUTDIR=str(tmp_path))
+    p = subprocess.Popen([sys.executable, str(launcher)], env=env)
+    t0 = time.time()
+    while len(list(tmp_path.glob("pid*"))) < 2 and time.time() - t0 < 60:
+        time.sleep(0.1)
+    pids = [int(f.read_text()) for f in tmp_path.glob("pid*")]
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(30) != 0
+    time.sleep(1.0)
+    for pid in pids:  # gone (or at most a zombie awaiting a reaper other than the launcher)
+        try:
+            state = [ln for ln in open("/proc/%d/status" % pid) if ln.startswith("State:")][0]
+        except (FileNotFoundError, IndexError):
+            continue
+        assert "Z" in state.split()[1], (pid, state)
