@@ -556,7 +556,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
             if "mfma_util" in ent:  # measured matrix-pipe occupancy of the same kernel (profiled run)
                 roof["mfma_util_pmc"] = ent["mfma_util"]
                 roof["mfma_util_source"] = ("rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), "
-                                            "profiles/r02/pmc_%s_summary.txt" % workload)
+                                            "profiles/r03/pmc_%s_summary.txt" % workload)
     roof["kernel"] = dom
     roof["algorithmic_per_launch"] = work
 

@@ -51,21 +51,26 @@ def load(d):
     return vals, dur, stats
 
 
-def stage_of(kernel):
-    """bench.py stage name of a kernel (template signature -> stage)."""
-    m = re.search(r"gemm_kernel<Tile<[^>]*>, (\d+), (\d+), (true|false|\d+)>", kernel)
+def stage_of(kernel, workload=""):
+    """bench.py stage name of a kernel (template signature -> stage).  PNN's layer 1
+    reads the materialised [x | ip] rows (dense A, K = 1,365: the 16-wave 3-deep-ring tile), so it is
+    told from its dense layer 2 by the tile."""
+    m = re.search(r"gemm_kernel<Tile<([^>]*)>, (\d+), (\d+), (true|false|\d+)>", kernel)
     if m:
-        amode, epi = int(m.group(1)), int(m.group(2))
+        tile, amode, epi = m.group(1), int(m.group(2)), int(m.group(3))
         if amode == 3:
             return "cin_layer"
         if amode in (1, 2):
+            return "tower_layer1"
+        if workload.startswith("pnn") and epi == 0 and tile.startswith("1, 13, 8, 2"):
             return "tower_layer1"
         return "tower_layer3" if epi == 1 else "tower_layer2"
     kernel = re.sub(r"^\(anonymous namespace\)::", "", kernel)
     for pat, st in (("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
                     ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
                     ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
-                    ("owner_gather", "shard_exchange")):
+                    ("owner_gather", "shard_exchange"), ("own_rows_kernel", "shard_exchange"),
+                    ("own_gather", "shard_exchange")):
         if kernel.startswith(pat):
             return st
     return None
@@ -130,7 +135,7 @@ def main():
         db = json.load(open(path)) if os.path.exists(path) else {}
         st = {}
         for k, e in out.items():
-            name = stage_of(k)
+            name = stage_of(k, wl)
             if name and "hbm_bytes" in e:
                 st[name] = {"hbm_bytes": round(e["hbm_bytes"]), "fetch_bytes_x2": round(e["fetch_bytes_x2"]),
                             "write_bytes": round(e["write_bytes"]), "kernel": k, "batch": a.batch}
