@@ -906,7 +906,18 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       if (wfuse)
 #pragma unroll
         for (int q = 0; q < kQW; ++q) issue_w(0, q, [&] { return w_id(0, q); });
-    for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
+    if constexpr (FAST) {
+      // always RING - 1 stages (the loop's counted wait assumes RING - 2 younger ones in flight):
+      // with fewer steps than that, the last step's sources fill the spare slots (never read)
+      if (nchunks > 0)
+        for (int c = 0; c < RING - 1; ++c) {
+          const int cs = c < nchunks ? c : nchunks - 1;
+#pragma unroll
+          for (int q = 0; q < IPW; ++q) issue_s3(cs, c % RING, q, [&] { return a_id(cs, q); });
+        }
+    } else {
+      for (int c = 0; c < RING - 1 && c < nchunks; ++c) issue(c);
+    }
     int pend_id = -1;  // kPrecS3: the ring id of the next DMA, read one MFMA group ahead
     if constexpr (RING == 1) {
       // Single-buffered stage, two (or more) blocks per CU: each block loads a step, computes it,

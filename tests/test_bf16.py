@@ -28,6 +28,7 @@ def _model(kind, V):
         "pnn": lambda: (rmx.PNN(V, F, K, [400, 400, 400]), oc.make_model(oc.PNN, F, K, fc=(400, 400, 400))),
         "pnn1": lambda: (rmx.PNN(V, F, K, [64]), oc.make_model(oc.PNN, F, K, fc=(64,))),
         "dnn": lambda: (rmx.DNN(V, F, K, [128, 64]), oc.make_model(oc.DNN, F, K, fc=(128, 64))),
+        "dnn32": lambda: (rmx.DNN(V, F, K, [32, 400, 400]), oc.make_model(oc.DNN, F, K, fc=(32, 400, 400))),
         "deepfm": lambda: (rmx.DeepFM(V, F, K, [400, 400, 400]), oc.make_model(oc.DEEPFM, F, K, fc=(400, 400, 400))),
         "lr": lambda: (rmx.LR(V, F), oc.make_model(oc.LR)),
     }[kind]()
@@ -154,3 +155,43 @@ def test_bf16_bench_batch_matches_bf16_oracle(kind):
         index = np.repeat(np.arange(n, dtype=np.int64), F)
         ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 2)
         assert np.abs(got[r0:r0 + n] - ref).max() <= TOL_BF16
+
+
+
+@pytest.mark.parametrize("kind", ["dcn", "pnn", "dnn32"])
+def test_bf16_fast_ring_variant_bitwise(kind):
+    """tower_variant 6 (the branch-free 3-deep ring tile with two 208-column slices, k_gemm.hpp
+    launch_tower_nt) accumulates each output in the same K-step order as the default 2-deep ring:
+    bitwise-equal predictions at B = 65,536.  dnn32 has a 400-wide layer with K = 32, one K step:
+    fewer steps than the ring's two stages of lead, which the prologue must still fill (the loop's
+    counted wait assumes them)."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 50_003, 65536
+    m, om = _model(kind, V)
+    t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16)
+    t.fill_synthetic(SEED_TAB)
+    mats = oc.round_bf16(m.initMats(SEED_MATS))
+    m.setPrecision(rmx.DTYPE_BF16)
+    m.setMats(mats)
+    m.setBias(0.01)
+    ids_d = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_d)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    got = {}
+    try:
+        for var in (None, 6):
+            rmx.set_tuning("tower_variant", var)
+            m.forward_ids(t, B, ids_d, out)
+            ctx.sync()
+            got[var] = out.numpy().copy()
+    finally:
+        rmx.set_tuning("tower_variant", None)
+    assert np.array_equal(got[6], got[None])
+    wt, et = _rounded_table(V)
+    n = 256
+    ids = oc.gen_ids(SEED_IDS, B - n, n, F, V).astype(np.int64)
+    w, e = oc.gather(wt, et, 1, ids)
+    index = np.repeat(np.arange(n, dtype=np.int64), F)
+    ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 2)
+    assert np.abs(got[6][B - n:] - ref).max() <= TOL_BF16

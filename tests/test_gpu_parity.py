@@ -304,3 +304,4 @@ def test_line_table_forward_bitwise_equals_row_table(kind, B):
         t.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert np.array_equal(outs[0][0], outs[0][1])
+

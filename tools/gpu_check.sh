@@ -88,6 +88,13 @@ for s in $STEPS; do
            run abt_${knob}_${v}_${i}_d 300 python bench.py --workload deepfm_train --steps 60 --warmup 5 --set $knob=$v || exit $?
            run abt_${knob}_${v}_${i}_x 300 python bench.py --workload xdeepfm_train --steps 20 --warmup 3 --set $knob=$v || exit $?
          done ;;
+    abw:*) rest=${s#abw:}   # abw:<workload>:<knob>=<v1>/<v2>/...: each value twice, interleaved, 100 steps
+         wl=${rest%%:*}; kv=${rest#*:}; knob=${kv%%=*}; vals=$(echo ${kv#*=} | tr '/' ' ')
+         for i in 1 2; do
+           for v in $vals; do
+             run abw_${wl}_${knob}_${v}_${i} 300 python bench.py --workload $wl --no-companion --no-cpu-baseline --steps 100 --warmup 10 --set $knob=$v || exit $?
+           done
+         done ;;
     testk:*) k=${s#testk:}
          run pytest_$k 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k $k ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
