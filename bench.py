@@ -60,6 +60,14 @@ def parse():
                     default="deepfm")
     ap.add_argument("--no-companion", action="store_true",
                     help="deepfm: skip the xDeepFM sub-record (BASELINE.json's metric names both models)")
+    ap.add_argument("--no-sharded-companion", action="store_true",
+                    help="deepfm at N > 1 (one GPU per rank): skip the configs[3] sub-record (the 100M-row table "
+                         "hash-sharded over the ranks, RCCL exchange)")
+    ap.add_argument("--sharded-companion", action="store_true",
+                    help="deepfm: add the sharded sub-record at N = 1 too (a rehearsal of the N > 1 path)")
+    ap.add_argument("--companion-timeout", type=float, default=240.0,
+                    help="seconds the sharded sub-record may take before a watchdog aborts its communicator and "
+                         "the line is printed with the sub-record marked as timed out")
     ap.add_argument("--vocab", type=int, default=0, help="table rows (default 1M; 100M for deepfm_sharded)")
     ap.add_argument("--batch", type=int, default=0, help="rows per step per GPU (default per workload)")
     ap.add_argument("--zipf", type=float, default=0.0,
@@ -370,6 +378,9 @@ def max_over_ranks(dist, t):
     return float(x.item())
 
 
+LIVE_SHARDS = []  # sharded tables of this process (the companion watchdog aborts their communicators)
+
+
 def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     """Builds the workload, times K steps after W warm-up steps (max over ranks), then measures the
     per-stage kernel times (HIP events on the launch stream) for the roofline of the dominant kernel."""
@@ -395,6 +406,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
                 dist.broadcast_object_list(box, src=0)
                 uid = box[0]
             table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
+            LIVE_SHARDS.append(table)
         table.set_dedupe(False if args.no_dedupe else (True if args.dedupe_on else "auto"))
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
@@ -824,9 +836,68 @@ def main():
                                    "gbs": round(r["value"] * bpe / 1e9, 1), "peak": PEAK_HBM_GBS,
                                    "frac": round(r["value"] * bpe / 1e9 / PEAK_HBM_GBS, 4),
                                    "note": "compute-bound: the dense tower / CIN, not the gather, sets the rate"}
+    # configs[3] at N > 1 (one GPU per rank): the 100M-row table hash-sharded over the ranks, one RCCL
+    # exchange per batch, as a sub-record of the default line -- so the driver's multi-GPU runs execute
+    # and check the exchange.  A watchdog bounds it: past --companion-timeout it aborts the RCCL
+    # communicator, prints the line with the sub-record marked as timed out and ends the process.
+    if (args.workload == "deepfm" and not args.no_companion and not args.no_sharded_companion and not args.zipf
+            and ((world > 1 and world <= ndev) or args.sharded_companion)):
+        sub = sharded_companion(args, rmx, ctx, rank, world, dist, line if rank == 0 else None)
+        if rank == 0:
+            line.setdefault("models", {})["deepfm_sharded"] = sub
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def sharded_companion(args, rmx, ctx, rank, world, dist, line):
+    """The deepfm_sharded sub-record (rank 0 returns it; every rank takes part): run() on the sharded
+    workload with min(K, 20) / min(W, 5) steps, then every rank's parity on its own rows."""
+    import threading
+    t_lim = args.companion_timeout
+    out_fd = os.dup(1)  # the real stdout: the watchdog may fire inside stdout_to_stderr (RCCL init)
+
+    def expire():
+        sys.stderr.write("bench.py: the sharded sub-record passed %.0f s; aborting its communicator\n" % t_lim)
+        for t in LIVE_SHARDS:
+            try:
+                t.abort()
+            except Exception:
+                pass
+        if line is not None:
+            out = dict(line)
+            out.setdefault("models", {})["deepfm_sharded"] = {
+                "error": "timed out after %.0f s (watchdog aborted the RCCL communicator)" % t_lim}
+            os.write(out_fd, (json.dumps(out) + "\n").encode())
+        os._exit(0)  # the main measurement stands; the line records the failure
+    wd = threading.Timer(t_lim, expire)
+    wd.daemon = True
+    wd.start()
+    try:
+        rs = run(args, "deepfm_sharded", rmx, ctx, rank, world, dist, min(args.steps, 20), min(args.warmup, 5))
+        pc = parity_check("deepfm_sharded", rs["out"], rank * rs["nrows"], vocab=rs["Vw"])
+        pcs = [pc]
+        if dist:
+            pcs = [None] * world
+            dist.all_gather_object(pcs, pc)
+        sub = {"config": config_of("deepfm_sharded", rs, world, 0), "value": round(rs["value"], 1),
+               "unit": "examples/s", "ms_per_step": round(rs["ms_per_step"], 4), "steps": min(args.steps, 20),
+               "warmup": min(args.warmup, 5), "exchange": rs["exchange"], "roofline": rs["roofline"],
+               "stages": rs["stages"], "parity_check_ranks": pcs, "parity_ok": all(p["ok"] for p in pcs)}
+    except Exception as e:  # recorded in the line; the main measurement stands
+        sub = {"error": "%s: %s" % (type(e).__name__, str(e)[:400])}
+        for t in LIVE_SHARDS:  # a failed exchange may leave RCCL kernels waiting on peers
+            try:
+                t.abort()
+            except Exception:
+                pass
+    for t in LIVE_SHARDS:  # (still under the watchdog: destroy synchronises the device)
+        t.close()
+    del LIVE_SHARDS[:]
+    wd.cancel()
+    os.close(out_fd)
+    return sub
 
 
 if __name__ == "__main__":

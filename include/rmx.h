@@ -250,6 +250,11 @@ int rmx_comm_unique_id(void* out, size_t cap);
 int rmx_shard_create(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, int nranks, int rank,
                      const void* unique_id, rmx_shard** out);
 int rmx_shard_destroy(rmx_shard* sh);
+/* Abort the shard's RCCL communicator (ncclCommAbort) from any thread, e.g. a watchdog while an
+ * exchange waits for a peer that never arrives: the pending exchange fails (or its kernels return)
+ * and every later exchange returns RMX_E_COMM; only rmx_shard_destroy may follow.  Takes no lock.
+ * A no-op returning RMX_OK for loopback and group shards. */
+int rmx_shard_abort(rmx_shard* sh);
 /* Owned rows from the same generator as rmx_table_fill_synthetic (bit-identical rows). */
 int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);
 int64_t rmx_shard_local_rows(const rmx_shard* sh);

@@ -39,6 +39,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -92,6 +93,7 @@ struct rmx_shard {
   int k = 0, N = 1, rank = 0;
   bool loopback = false;
   ncclComm_t comm = nullptr;
+  std::atomic<bool> aborted{false};     // rmx_shard_abort ran: the communicator is torn down
   rmx_group* group = nullptr;           // in-process exchange group (or null)
   std::unique_ptr<rmx::Transport> tr;   // RCCL or group transport (null: loopback)
   int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
@@ -780,7 +782,7 @@ int shard_destroy(rmx_shard* sh) {
   (void)hipDeviceSynchronize();  // the exchange may have run on any stream
   sh->tr.reset();
   if (sh->ws_fence) (void)hipEventDestroy(sh->ws_fence);
-  if (sh->comm) ncclCommDestroy(sh->comm);
+  if (sh->comm && !sh->aborted.load()) ncclCommDestroy(sh->comm);
   if (sh->group) {
     {
       std::lock_guard<std::mutex> lk(sh->group->mu);
@@ -932,6 +934,10 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     dedupe_auto(sh, dd, nnz);
     // (the device count also bounds a batch holding ids outside [0, V), which route no row)
     return launch_owner_gather(s, nnz, k, sh.rs, sh.send_ids, sh.part[0], sh.recv_emb, sh.recv_w, cnt);
+  }
+  if (sh.aborted.load()) {
+    set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
+    return RMX_E_COMM;
   }
   Transport& tr = *sh.tr;
   const int me = sh.rank;
@@ -1113,6 +1119,20 @@ extern "C" int rmx_shard_create_group(rmx_ctx* ctx, int64_t num_rows, int embedd
 }
 
 extern "C" int rmx_shard_destroy(rmx_shard* sh) { return shard_destroy(sh); }
+
+extern "C" int rmx_shard_abort(rmx_shard* sh) {
+  if (!sh) {
+    rmx::set_error("rmx_shard_abort: null shard");
+    return RMX_E_INVALID;
+  }
+  if (!sh->comm || sh->aborted.exchange(true)) return RMX_OK;
+  const ncclResult_t r = ncclCommAbort(sh->comm);
+  if (r != ncclSuccess) {
+    rmx::set_error(std::string("rmx_shard_abort: ") + ncclGetErrorString(r));
+    return RMX_E_COMM;
+  }
+  return RMX_OK;
+}
 
 extern "C" int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed) {
   if (!sh) {

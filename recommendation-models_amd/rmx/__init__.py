@@ -319,6 +319,12 @@ class ShardedTable:
         """Collective: rows of ids_dev from their owners (bit-exact copies)."""
         check(_lib.lib.rmx_shard_gather(self.handle, int(n), ids_dev.ptr, w_out.ptr, emb_out.ptr, stream))
 
+    def abort(self):
+        """Tear down the RCCL communicator from any thread (a watchdog over a stuck exchange):
+        later exchanges raise; only close() may follow (rmx_shard_abort)."""
+        if self.handle:
+            check(_lib.lib.rmx_shard_abort(self.handle))
+
     def close(self):
         if self.handle:
             _lib.lib.rmx_shard_destroy(self.handle)

@@ -92,6 +92,7 @@ SIGNATURES = [
     ("rmx_comm_unique_id", c_int, [c_vp, c_sz]),
     ("rmx_shard_create", c_int, [c_vp, c_i64, c_int, c_int, c_int, c_vp, P(c_vp)]),
     ("rmx_shard_destroy", c_int, [c_vp]),
+    ("rmx_shard_abort", c_int, [c_vp]),
     ("rmx_group_create", c_int, [c_int, P(c_vp)]),
     ("rmx_group_destroy", c_int, [c_vp]),
     ("rmx_shard_create_group", c_int, [c_vp, c_i64, c_int, c_vp, c_int, P(c_vp)]),

@@ -241,6 +241,34 @@ def test_rccl_single_rank_shard_matches_replicated():
 
 
 @pytest.mark.gpu
+def test_rccl_shard_abort():
+    """rmx_shard_abort tears the RCCL communicator down without a lock (a watchdog's call): a second
+    abort is a no-op, the one-rank path (no RCCL op) still serves batches bitwise, and destroy
+    afterwards skips the aborted communicator.  A loopback shard has none: abort is a no-op."""
+    import rmx
+    ctx = rmx.default_context()
+    V, B = 200_000, 1024
+    table, ids = _setup(ctx, V, B, seed_row=5)
+    m = rmx.DeepFM(V, F, K, [64, 32])
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    ref = rmx.DeviceArray(ctx, B, np.float32)
+    got = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids, ref)
+    sh = rmx.ShardedTable(ctx, V, K, 1, 0, rmx.comm_unique_id())
+    sh.fill_synthetic(SEED_TAB)
+    sh.abort()
+    sh.abort()
+    m.forward_ids_sharded(sh, B, ids, got)
+    ctx.sync()
+    assert np.array_equal(got.numpy(), ref.numpy())
+    sh.close()
+    lb = rmx.ShardedTable(ctx, V, K, 2, 0)
+    lb.abort()
+    lb.close()
+
+
+@pytest.mark.gpu
 def test_shard_bad_args():
     import rmx
     ctx = rmx.default_context()

@@ -98,6 +98,7 @@ for s in $STEPS; do
     testk:*) k=${s#testk:}
          run pytest_$k 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k $k ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
+    benchsc) run bench_sharded_companion 400 python bench.py --gpus 1 --steps 20 --warmup 5 --sharded-companion ;;
     bench2s) echo "== bench_gpus2_sharded (expects a clean refusal on a 1-GPU box)" | tee -a "$OUT/steps.log"
          timeout -k 10 300 python bench.py --workload deepfm_sharded --gpus 2 --steps 5 --warmup 1 \
             > "$OUT/bench_gpus2_sharded.log" 2>&1
