@@ -477,7 +477,15 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     if args.settle_ms > 0:
         ctx.sync()
         t_s = time.perf_counter()
-        while (time.perf_counter() - t_s) * 1e3 < args.settle_ms:
+        # every sharded step at N > 1 is a collective (the exchange): the ranks must run the same
+        # number of them, so they agree each round on going on (any rank still under the budget)
+        agree = sharded and dist is not None
+        while True:
+            more = (time.perf_counter() - t_s) * 1e3 < args.settle_ms
+            if agree:
+                more = max_over_ranks(dist, 1.0 if more else 0.0) > 0.5
+            if not more:
+                break
             for _ in range(8):
                 step(settle)
                 settle += 1
