@@ -899,6 +899,137 @@ __global__ __launch_bounds__(512, 4) void wgrad_nk_kernel(int rows, int N, int K
     }
 }
 
+// The split dW on a 208 x 208 tile (knob "wgrad_sq", the tower's dW = dPre^T x_in): 13 waves, wave w owns
+// k tile w and all 13 n tiles (13 x 6 MFMAs per 32-row chunk), one block per CU on a double-buffered
+// 156 KiB LDS image.  Against the 128 x 128 tiles, a 400 x 400 dW is 2 x 2 tiles instead of 4 x 4 (416^2
+// instead of 512^2 outputs computed) and every batch row is staged 2 + 2 times instead of 4 + 4 -- the
+// staging (loads, split, LDS stores), not the MFMAs, is what the dW waits on.  Each
+// thread stages one A and one X item (a column's 8-row octet) per chunk; the loads of chunk c + 2 fly
+// during chunk c + 1's MFMAs, and chunk c + 1 is split and stored into the other buffer while chunk c
+// computes.  Per output the chunks and the 6 MFMAs run in the same order as the 128 x 128 kernel; only
+// the row-slice split S can differ.
+constexpr int kSqT = 208, kSqW = kSqT / 16, kSqThr = kSqW * 64;
+// cpart (nullable): the blocks of the first k tile also sum their A columns over their row slice (the
+// bias gradient, sum_b dPre[b][n], fused: the A items pass through registers anyway) into
+// cpart[slice][N], rows in order per staging thread, the 4 row octets added in order at the end.
+__global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, int K, const float* __restrict__ A,
+                                                             int lda, const float* __restrict__ X, int ldx,
+                                                             int rows_per_slice, int tiles, float* __restrict__ part,
+                                                             float* __restrict__ cpart) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) wg_bf16x8 wlds[];
+  // [buf][op: A, X][plane][208 cols][4 slots]
+  auto L = [&](int buf, int op, int pl) { return wlds + ((buf * 2 + op) * 3 + pl) * kSqT * 4; };
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = blockIdx.x, xcd = bid & 7, idx = bid >> 3;
+  const int slice = (idx / tiles) * 8 + xcd, tile = idx % tiles;
+  const int ntn = (N + kSqT - 1) / kSqT;
+  const int n0 = (tile % ntn) * kSqT, k0 = (tile / ntn) * kSqT;
+  const int r_begin = slice * rows_per_slice;
+  const int r_end = min(rows, r_begin + rows_per_slice);
+  const int nch = r_end > r_begin ? (r_end - r_begin + kWgR - 1) / kWgR : 0;
+  // staging item of this thread: column col of A (n0 + col) and of X (k0 + col), row octet h
+  const int col = tid % kSqT, h = tid / kSqT;
+  const bool a_ok = n0 + col < N, x_ok = k0 + col < K;
+  const bool csum_on = cpart != nullptr && k0 == 0;
+  float va[8], vx[8], csum = 0.f;
+  auto gload = [&](int c) {
+    const int r0 = r_begin + c * kWgR + 8 * h;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = r0 + q;
+      const bool ok = r < r_end;
+      va[q] = (ok && a_ok) ? A[(int64_t)r * lda + n0 + col] : 0.f;
+      vx[q] = (ok && x_ok) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
+    }
+  };
+  auto col_sum = [&]() {
+    if (csum_on)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) csum += va[q];
+  };
+  auto sstore = [&](int buf) {
+    const int o = col * 4 + wg_slot(col, h);
+    wg_bf16x8 p0, p1, p2;
+    col_sum();
+    wg_split(va, p0, p1, p2);
+    L(buf, 0, 0)[o] = p0;
+    L(buf, 0, 1)[o] = p1;
+    L(buf, 0, 2)[o] = p2;
+    wg_split(vx, p0, p1, p2);
+    L(buf, 1, 0)[o] = p0;
+    L(buf, 1, 1)[o] = p1;
+    L(buf, 1, 2)[o] = p2;
+  };
+  const int g = lane >> 4, r16 = lane & 15;
+  f32x4 acc[kSqW];
+#pragma unroll
+  for (int a = 0; a < kSqW; ++a) acc[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // stage(c): chunk c + 1 into the other buffer (its last readers, chunk c - 1's MFMAs, passed the
+  // barrier), then chunk c + 2's loads; part 0 = the A item, 1 = the X item and the loads
+  auto stage_part = [&](int c, int part_) {
+    if (c + 1 >= nch) return;
+    const int buf = (c + 1) & 1, o = col * 4 + wg_slot(col, h);
+    wg_bf16x8 p0, p1, p2;
+    if (part_ == 0) col_sum();
+    wg_split(part_ == 0 ? va : vx, p0, p1, p2);
+    L(buf, part_, 0)[o] = p0;
+    L(buf, part_, 1)[o] = p1;
+    L(buf, part_, 2)[o] = p2;
+    if (part_ == 1 && c + 2 < nch) gload(c + 2);
+  };
+  auto compute = [&](int c) {
+    const int cur = c & 1;
+    wg_bf16x8 fx[3], fa[3];
+    const int cx = wid * 16 + r16;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) fx[pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
+#pragma unroll
+    for (int a = 0; a < kSqW; ++a) {
+      const int ca = a * 16 + r16;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fa[pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+      f32x4 d = acc[a];
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fx[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[2], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[1], d, 0, 0, 0);
+      acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[0], d, 0, 0, 0);
+    }
+  };
+  if (nch > 0) {
+    gload(0);
+    sstore(0);
+  }
+  if (nch > 1) gload(1);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    compute(c);
+    // (issuing this staging between the last MFMA tiles instead measured the same: DeepFM training
+    // tower backward 0.2955 vs 0.2975 ms per layer)
+    stage_part(c, 0);
+    stage_part(c, 1);
+    __syncthreads();
+  }
+  float* out = part + (int64_t)slice * N * K;
+  const int k = k0 + wid * 16 + r16;
+#pragma unroll
+  for (int a = 0; a < kSqW; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + a * 16 + 4 * g + r;
+      if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][r];
+    }
+  if (csum_on) {  // block-uniform; the LDS image is free after the loop's last barrier
+    float* red = reinterpret_cast<float*>(wlds);
+    red[h * kSqT + col] = csum;
+    __syncthreads();
+    if (h == 0 && a_ok)
+      cpart[(int64_t)slice * N + n0 + col] = ((red[col] + red[kSqT + col]) + red[2 * kSqT + col]) + red[3 * kSqT + col];
+  }
+}
+
 // out[i] (=, or += when accum) sum_s part[s][i]: a block covers 64 outputs with 4 wave-groups, group
 // q summing slices q, q + 4, ...; the 4 group sums are added in fixed order (deterministic).
 __global__ __launch_bounds__(256) void slice_reduce_kernel(int S, int64_t n, const float* __restrict__ part,
@@ -953,8 +1084,11 @@ int ensure_part(TrainState& T, int64_t n) {
 // only, wgrad_z_ok): X is the CIN outer product generated from x0 / up instead of read
 bool wgrad_z_ok() { return f32_split_enabled() && tuning_get("wgrad_s3", 2) != 0; }
 
+// bias (nullable): also bias[n] = sum_b A[b][n] when the kernel can fuse it (the 208 x 208 tile); *bias_done
+// says whether it did (else the caller runs colsum)
 int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, int lda, const float* X, int ldx,
-          float* out, bool accum, const WgZ* zg = nullptr) {
+          float* out, bool accum, const WgZ* zg = nullptr, float* bias = nullptr, bool* bias_done = nullptr) {
+  if (bias_done) *bias_done = false;
   if (rows <= 0 || N <= 0 || K <= 0) return RMX_OK;
   // knob "wgrad_s3": 0 = the f32 MFMA kernel, 1 = split GEMM with 64 x 64 tiles, 2 = 128 x 128 tiles
   // default 2 since the single-buffered kernel (wgrad_sb): DeepFM training at B = 65,536 2.25 ->
@@ -973,15 +1107,66 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   // (the tower's 400 x 400 / 624 dW ran slower on it: DeepFM training 1.95 -> 2.19 ms), 0 off
   const int nkv = tuning_get("wgrad_nk", 1);
   const bool nk = var == 2 && (nkv == 2 || (nkv == 1 && zg));
+  // knob "wgrad_sq": 1 (default) the 208 x 208 tile for a read (not generated) X, 0 off (DeepFM
+  // training at B = 65,536: tower backward 0.346 / 0.346 / 0.445 -> 0.300 / 0.300 / 0.423 ms per layer,
+  // 33.4 -> 35.4 M examples/s, profiles/r03/ab_wgrad_sq.txt)
+  // (one block per CU: at small batches -- xDeepFM training, B = 4,096 -- the 128 x 128 tiles' two blocks
+  // per CU win: tower layer-1 backward 0.083 vs 0.104 ms)
+  const bool sq = var == 2 && !zg && !nk && tuning_get("wgrad_sq", 1) != 0 && rows >= 32768;
   const int TT = var == 2 ? 128 : kWgT;
-  const int tiles = nk ? ((N + kNkN - 1) / kNkN) * ((K + kNkK - 1) / kNkK) : ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
+  const int tiles = sq   ? ((N + kSqT - 1) / kSqT) * ((K + kSqT - 1) / kSqT)
+                    : nk ? ((N + kNkN - 1) / kNkN) * ((K + kNkK - 1) / kNkK)
+                         : ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
   // slices of ~1024 rows (one slice of both operands, (N + K) * 4 KiB, stays in an XCD's 4 MiB L2),
   // at least ~1024 blocks in flight, S a multiple of the 8 XCDs
   int S = std::max((rows + 1023) / 1024, std::min((1024 + tiles - 1) / tiles, std::max(1, rows / 64)));
   S = round_up(std::min(S, 512), 8);
+  if (sq) {
+    // one block per CU: the S (a multiple of 8) with the fewest rounds x chunks per block
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      RMX_HIP(hipGetDevice(&dev));
+      RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      ncu = std::max(ncu, 1);
+    }
+    int64_t best = -1;
+    for (int s8 = 8; s8 <= 512; s8 += 8) {
+      const int64_t chunks = round_up((rows + s8 - 1) / s8, kWgR) / kWgR;
+      const int64_t cost = ((int64_t)tiles * s8 + ncu - 1) / ncu * chunks;
+      if (best < 0 || cost < best) {
+        best = cost;
+        S = s8;
+      }
+      if (chunks <= 1) break;
+    }
+  }
   const int rps = round_up((rows + S - 1) / S, var ? kWgR : 16);
-  int st = ensure_part(T, (int64_t)S * N * K);
+  const bool fuse_bias = sq && bias && tuning_get("wgrad_bias", 1) != 0;
+  int st = ensure_part(T, (int64_t)S * N * K + (fuse_bias ? (int64_t)S * N : 0));
   if (st) return st;
+  if (sq) {
+    const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * kSqT * 4;  // 156 KiB
+    static bool attr = false;
+    if (!attr) {
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      attr = true;
+    }
+    float* cpart = fuse_bias ? T.part2 + (int64_t)S * N * K : nullptr;
+    hipLaunchKernelGGL(wgrad_sq_kernel, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps, tiles,
+                       T.part2, cpart);
+    RMX_HIP(hipGetLastError());
+    hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)N * K + 63) / 64)), dim3(256), 0, s, S,
+                       (int64_t)N * K, T.part2, out, accum ? 1 : 0);
+    RMX_HIP(hipGetLastError());
+    if (fuse_bias) {
+      hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, S, (int64_t)N, cpart,
+                         bias, 0);
+      RMX_HIP(hipGetLastError());
+      *bias_done = true;
+    }
+    return RMX_OK;
+  }
   // knob "wgrad_sb": 1 (default) the single-buffered kernel on the 128 x 128 tiles (two blocks per CU),
   // 2 also on the 64 x 64 tiles, 0 off
   if (nk) {
@@ -1351,11 +1536,15 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     // below fused as a mask; otherwise gemm_f32_kernel + relu_back_kernel
     const float* mask = l > 0 ? T.h[l - 1] : nullptr;
     const int ldmask = l > 0 ? m.layers[l - 1].Npad : 0;
-    bool masked = false;
+    bool masked = false, bias_done = false;
     for (int q = 0; q < nb; ++q) {
       const Blk& bk = blks[q];
-      if (o.g_mats && (st = wgrad(T, s, B, N, bk.K, dpre, L.Npad, xin + bk.c0, ldin, o.g_mats + bk.w, false)))
+      // (the bias gradient rides along with the first block's dW when the kernel fuses it)
+      bool bd = false;
+      if (o.g_mats && (st = wgrad(T, s, B, N, bk.K, dpre, L.Npad, xin + bk.c0, ldin, o.g_mats + bk.w, false, nullptr,
+                                  (q == 0 && L.bias_mode == 1) ? o.g_mats + L.b_off : nullptr, &bd)))
         return st;
+      bias_done = bias_done || bd;
       if (!need_dx) continue;
       if (nb == 1 && m.precision == kF32 && dx_s3_usable(L, ldin) && (!mask || L.NTpad <= ldmask)) {
         if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, dxin + bk.c0, ldin, mask, ldmask))) return st;
@@ -1366,7 +1555,8 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
           return st;
       }
     }
-    if (o.g_mats && L.bias_mode == 1 && (st = colsum(T, s, B, N, dpre, L.Npad, nullptr, o.g_mats + L.b_off, false)))
+    if (o.g_mats && L.bias_mode == 1 && !bias_done &&
+        (st = colsum(T, s, B, N, dpre, L.Npad, nullptr, o.g_mats + L.b_off, false)))
       return st;
     if (o.g_mats && L.bias_mode == 2) {  // one CAdd(1) scalar over all outputs
       if ((st = colsum(T, s, B, N, dpre, L.Npad, nullptr, T.tmp, false))) return st;

@@ -302,6 +302,58 @@ def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "dcn", "pnn"])
+def test_backward_wgrad_sq_tile(kind):
+    """The 208 x 208 dW tile (wgrad_sq 1, default at >= 32,768 rows), with and without the bias
+    gradient fused into it (wgrad_bias), against the 128 x 128 tiles + colsum_kernel (wgrad_sq 0, the
+    kernels the oracle tests pin at small B): the same per-output chunk / MFMA order over a different
+    row-slice split, so within 2e-5 relative of it.  B = 32,768 + 7 (a ragged last chunk); PNN's
+    layer 1 has two Linear blocks (K = 624 and 741)."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K, fc, B = 20_000, 39, 16, (400, 400, 400), 32775
+    m = _gpu_model(rmx, kind, V, F, K, fc)
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 3, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(5).random(B) > 0.7).astype(np.float32))
+    ml = len(mats)
+
+    def grads():
+        out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, ml, 1)]
+        m.backward_ids(t, B, ids, targets, *out)
+        ctx.sync()
+        return [o.numpy().copy() for o in out]
+
+    res = {}
+    try:
+        for sq, bias in ((0, 1), (1, 1), (1, 0)):  # wgrad_bias 1: the bias gradient fused into the dW
+            rmx.set_tuning("wgrad_sq", sq)
+            rmx.set_tuning("wgrad_bias", bias)
+            res[sq, bias] = grads()
+    finally:
+        rmx.set_tuning("wgrad_sq", None)
+        rmx.set_tuning("wgrad_bias", None)
+    for key in ((1, 1), (1, 0)):
+        for a, b in zip(res[0, 1], res[key]):
+            assert np.abs(a - b).max() <= 2e-5 * max(np.abs(a).max(), 1e-30), key
+    # every getMatsSize block on its own scale (the biases: fused column sums vs colsum_kernel)
+    sizes = list(m.getMatsSize())
+    off = 0
+    for i in range(0, len(sizes), 2):
+        n = sizes[i] * sizes[i + 1]
+        a, b = res[0, 1][3][off:off + n], res[1, 1][3][off:off + n]
+        assert np.abs(a - b).max() <= 2e-5 * max(np.abs(a).max(), 1e-30), (i // 2, sizes[i], sizes[i + 1])
+        off += n
+    assert np.isfinite(res[1, 1][3]).all() and np.abs(res[1, 1][3]).max() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", GPU_KINDS)
 def test_backward_host_arrays_in_place(kind):
     """L-A RecModel.backward: the caller's arrays come back holding the gradients."""
