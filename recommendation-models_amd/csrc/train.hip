@@ -912,10 +912,12 @@ constexpr int kSqT = 208, kSqW = kSqT / 16, kSqThr = kSqW * 64;
 // cpart (nullable): the blocks of the first k tile also sum their A columns over their row slice (the
 // bias gradient, sum_b dPre[b][n], fused: the A items pass through registers anyway) into
 // cpart[slice][N], rows in order per staging thread, the 4 row octets added in order at the end.
+// GZ: X is the CIN outer product z = x0 (x) up generated while staged (as wgrad_s3_kernel / wgrad_nk_kernel).
+template <bool GZ>
 __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, int K, const float* __restrict__ A,
                                                              int lda, const float* __restrict__ X, int ldx,
                                                              int rows_per_slice, int tiles, float* __restrict__ part,
-                                                             float* __restrict__ cpart) {
+                                                             float* __restrict__ cpart, WgZ zg) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) wg_bf16x8 wlds[];
   // [buf][op: A, X][plane][208 cols][4 slots]
@@ -932,6 +934,7 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
   const int col = tid % kSqT, h = tid / kSqT;
   const bool a_ok = n0 + col < N, x_ok = k0 + col < K;
   const bool csum_on = cpart != nullptr && k0 == 0;
+  const int zf = GZ ? (k0 + col) / zg.Hp : 0, zh = GZ ? k0 + col - zf * zg.Hp : 0;  // (f, h) of column k
   float va[8], vx[8], csum = 0.f;
   auto gload = [&](int c) {
     const int r0 = r_begin + c * kWgR + 8 * h;
@@ -940,7 +943,10 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
       const int r = r0 + q;
       const bool ok = r < r_end;
       va[q] = (ok && a_ok) ? A[(int64_t)r * lda + n0 + col] : 0.f;
-      vx[q] = (ok && x_ok) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
+      if constexpr (GZ)
+        vx[q] = (ok && x_ok) ? zg.x0[(int64_t)r * zg.F + zf] * zg.up[(int64_t)r * zg.ldup + zh] : 0.f;
+      else
+        vx[q] = (ok && x_ok) ? X[(int64_t)r * ldx + k0 + col] : 0.f;
     }
   };
   auto col_sum = [&]() {
@@ -1112,10 +1118,12 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   // 33.4 -> 35.4 M examples/s, profiles/r03/ab_wgrad_sq.txt)
   // (one block per CU: at small batches -- xDeepFM training, B = 4,096 -- the 128 x 128 tiles' two blocks
   // per CU win: tower layer-1 backward 0.083 vs 0.104 ms)
-  const bool sq = var == 2 && !zg && !nk && tuning_get("wgrad_sq", 1) != 0 && rows >= 32768;
+  // knob "wgrad_sq_gz": 1 the 208 x 208 tile also for the CIN's generated operand (else the 208 x 128 one)
+  const bool sq_gz = zg && var == 2 && tuning_get("wgrad_sq_gz", 0) != 0 && rows >= 32768;
+  const bool sq = sq_gz || (var == 2 && !zg && !nk && tuning_get("wgrad_sq", 1) != 0 && rows >= 32768);
   const int TT = var == 2 ? 128 : kWgT;
-  const int tiles = sq   ? ((N + kSqT - 1) / kSqT) * ((K + kSqT - 1) / kSqT)
-                    : nk ? ((N + kNkN - 1) / kNkN) * ((K + kNkK - 1) / kNkK)
+  const int tiles = sq ? ((N + kSqT - 1) / kSqT) * ((K + kSqT - 1) / kSqT)
+                  : nk ?  ((N + kNkN - 1) / kNkN) * ((K + kNkK - 1) / kNkK)
                          : ((N + TT - 1) / TT) * ((K + TT - 1) / TT);
   // slices of ~1024 rows (one slice of both operands, (N + K) * 4 KiB, stays in an XCD's 4 MiB L2),
   // at least ~1024 blocks in flight, S a multiple of the 8 XCDs
@@ -1149,12 +1157,19 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * kSqT * 4;  // 156 KiB
     static bool attr = false;
     if (!attr) {
-      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
       attr = true;
     }
     float* cpart = fuse_bias ? T.part2 + (int64_t)S * N * K : nullptr;
-    hipLaunchKernelGGL(wgrad_sq_kernel, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps, tiles,
-                       T.part2, cpart);
+    if (zg)
+      hipLaunchKernelGGL(wgrad_sq_kernel<true>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
+                         tiles, T.part2, cpart, z);
+    else
+      hipLaunchKernelGGL(wgrad_sq_kernel<false>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
+                         tiles, T.part2, cpart, z);
     RMX_HIP(hipGetLastError());
     hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)N * K + 63) / 64)), dim3(256), 0, s, S,
                        (int64_t)N * K, T.part2, out, accum ? 1 : 0);

@@ -302,6 +302,44 @@ def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
 
 
 @pytest.mark.gpu
+def test_backward_wgrad_sq_tile_cin():
+    """The CIN's generated-operand dW on the 208 x 208 tile (wgrad_sq_gz 1) against the 208 x 128 one
+    (the default): rows = B k = 65,584 (a ragged chunk), within 2e-5 relative per mats block."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K, B = 20_000, 39, 16, 4099
+    m = _gpu_model(rmx, "xdeepfm", V, F, K, (400, 400, 400))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 9, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(3).random(B) > 0.7).astype(np.float32))
+    res = {}
+    try:
+        for v in (0, 1):
+            rmx.set_tuning("wgrad_sq_gz", v)
+            out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, len(mats), 1)]
+            m.backward_ids(t, B, ids, targets, *out)
+            ctx.sync()
+            res[v] = [o.numpy().copy() for o in out]
+    finally:
+        rmx.set_tuning("wgrad_sq_gz", None)
+    sizes = list(m.getMatsSize())
+    off = 0
+    for i in range(0, len(sizes), 2):
+        n = sizes[i] * sizes[i + 1]
+        a, b = res[0][3][off:off + n], res[1][3][off:off + n]
+        assert np.abs(a - b).max() <= 2e-5 * max(np.abs(a).max(), 1e-30), (i // 2, sizes[i], sizes[i + 1])
+        off += n
+    for a, b in zip(res[0][:3], res[1][:3]):
+        assert np.array_equal(a, b)  # the dW does not feed the other gradients
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["deepfm", "dcn", "pnn"])
 def test_backward_wgrad_sq_tile(kind):
     """The 208 x 208 dW tile (wgrad_sq 1, default at >= 32,768 rows), with and without the bias
