@@ -1131,13 +1131,10 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   S = round_up(std::min(S, 512), 8);
   if (sq) {
     // one block per CU: the S (a multiple of 8) with the fewest rounds x chunks per block
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      RMX_HIP(hipGetDevice(&dev));
-      RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      ncu = std::max(ncu, 1);
-    }
+    int ncu = 0, dev = 0;
+    RMX_HIP(hipGetDevice(&dev));
+    RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    ncu = std::max(ncu, 1);
     int64_t best = -1;
     for (int s8 = 8; s8 <= 512; s8 += 8) {
       const int64_t chunks = round_up((rows + s8 - 1) / s8, kWgR) / kWgR;
@@ -1155,14 +1152,9 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   if (st) return st;
   if (sq) {
     const size_t lds = sizeof(wg_bf16x8) * 2 * 2 * 3 * kSqT * 4;  // 156 KiB
-    static bool attr = false;
-    if (!attr) {
-      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
-      attr = true;
-    }
+    // (set at every launch, as launch_cfg does: a process may drive several devices)
+    RMX_HIP(hipFuncSetAttribute(zg ? (const void*)wgrad_sq_kernel<true> : (const void*)wgrad_sq_kernel<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     float* cpart = fuse_bias ? T.part2 + (int64_t)S * N * K : nullptr;
     if (zg)
       hipLaunchKernelGGL(wgrad_sq_kernel<true>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
