@@ -103,6 +103,10 @@ def stage_work(workload, stage, B, direct=False):
         return "byte", B * (F * 4 + F * es + F * K * es + 4)
     if stage == "first_order":
         return "byte", B * (F * 4 + F * es + 4)
+    if stage == "encoder_fm_x":  # training: the same reads + the gathered rows stored as fp32 x
+        return "byte", B * (F * 4 + F * es + F * K * es + 4 + D * 4)
+    if stage == "first_order_x":  # training: ids + w + rows + y + x
+        return "byte", B * (F * 4 + F * es + F * K * es + 4 + D * 4)
     if stage == "cross":  # ids + rows + pre2
         return "byte", B * (F * 4 + F * K * es + 4)
     if stage == "product":  # ids + rows + the [x | ip] row written

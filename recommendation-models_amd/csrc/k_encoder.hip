@@ -24,18 +24,24 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 //       3 = y += y2 (L-A path with an irregular COO index: y already holds y1 from the CSR kernel).
 // k = 16 fast path: 4 lanes per sample (one float4 of the 64-B row each), 16 samples per wave,
 // all F row loads of a lane independent (ids staged in registers first).
+// xo (nullable, MODE 0 / 1 / 3): also store the gathered rows as the fp32 x = [B][F * 16] (row stride F * 16):
+// the training forward's tower input, written from the same loads (float4 per lane, 64 B per field)
 template <int MODE, class T>
 __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* __restrict__ ids,
                                                           const T* __restrict__ table,
                                                           const T* __restrict__ wtab, int F,
                                                           float* __restrict__ y, float beta,
-                                                          float* __restrict__ prob, int ld, int wld) {
+                                                          float* __restrict__ prob, int ld, int wld,
+                                                          float* __restrict__ xo) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int s = lane >> 2, c = lane & 3;
   const int b = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + s;
   const bool valid = b < M;
   const int bb = valid ? b : 0;
+  constexpr bool FM = MODE == 1 || MODE == 3;
+  const bool rows = FM || (MODE == 0 && xo != nullptr);  // the rows are loaded
+  float4* xr = xo && valid ? reinterpret_cast<float4*>(xo + (int64_t)b * F * 16) + c : nullptr;
   float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = s4;
   float y1 = 0.f;
   int f = 0;
@@ -47,25 +53,29 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
     float wv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if (MODE == 1 || MODE == 3) v[u] = load4(table + (int64_t)id[u] * ld + c * 4);
+      if (rows) v[u] = load4(table + (int64_t)id[u] * ld + c * 4);
       if (MODE != 3) wv[u] = (c == 0) ? ld1(wtab + (int64_t)id[u] * wld) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      if (MODE == 1 || MODE == 3) {
+      if (FM) {
         s4.x += v[u].x; s4.y += v[u].y; s4.z += v[u].z; s4.w += v[u].w;
         q4.x += v[u].x * v[u].x; q4.y += v[u].y * v[u].y;
         q4.z += v[u].z * v[u].z; q4.w += v[u].w * v[u].w;
       }
       if (MODE != 3) y1 += wv[u];
+      if (xr) xr[(f + u) * 4] = v[u];
     }
   }
   for (; f < F; ++f) {
     const int id = ids ? ids[(int64_t)bb * F + f] : bb * F + f;
-    if (MODE == 1 || MODE == 3) {
+    if (rows) {
       const float4 v = load4(table + (int64_t)id * ld + c * 4);
-      s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
-      q4.x += v.x * v.x; q4.y += v.y * v.y; q4.z += v.z * v.z; q4.w += v.w * v.w;
+      if (FM) {
+        s4.x += v.x; s4.y += v.y; s4.z += v.z; s4.w += v.w;
+        q4.x += v.x * v.x; q4.y += v.y * v.y; q4.z += v.z * v.z; q4.w += v.w * v.w;
+      }
+      if (xr) xr[f * 4] = v;
     }
     if (MODE != 3 && c == 0) y1 += ld1(wtab + (int64_t)id * wld);
   }
@@ -131,14 +141,14 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
 
 template <class T>
 static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids, const T* table, const T* wtab, int F,
-                             int k, float* y, float bt, float* prob, int ld, int wld) {
+                             int k, float* y, float bt, float* prob, int ld, int wld, float* xo) {
   if (k == 16 || mode == 2) {  // LR (mode 2) never reads the table: any k takes the 4-lane path
     dim3 grid((M + 63) / 64);
     switch (mode) {
-      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
-      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
-      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
-      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld); break;
+      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo); break;
+      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo); break;
+      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, nullptr); break;
+      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo); break;
     }
   } else {
     dim3 grid((M + 255) / 256);
@@ -151,15 +161,19 @@ static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids,
 }
 
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table, const void* wtab, int dt,
-                   int F, int k, float* y, const float* beta, float* prob, int ld, int wld) {
+                   int F, int k, float* y, const float* beta, float* prob, int ld, int wld, float* xo) {
   if (M <= 0) return RMX_OK;
+  if (xo && (k != 16 || mode == 2)) {
+    set_error("encoder: the gathered-row output needs k = 16 and a table-reading mode");
+    return RMX_E_INVALID;
+  }
   const float bt = beta ? *beta : 0.f;
   ld = ld > 0 ? ld : (k == 16 || mode == 2 ? 16 : k);
   wld = wld > 0 ? wld : 1;
   if (dt == kBF16)
-    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob, ld, wld);
+    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob, ld, wld, xo);
   else
-    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob, ld, wld);
+    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob, ld, wld, xo);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -127,10 +127,11 @@ bool tower_wring(const DenseLayer& L, int M, const AGatherArgs* ga);
 
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
-// ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1)
+// ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1); xo (k = 16,
+// modes 0 / 1 / 3): also write the gathered rows as fp32 x [M][F * 16] (the training forward's tower input)
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table,
                    const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob, int ld = 0,
-                   int wld = 0);
+                   int wld = 0, float* xo = nullptr);
 int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y);
 int launch_sigmoid_out(hipStream_t s, int B, const float* y, float beta, float* out);
 int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids);

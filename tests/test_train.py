@@ -302,6 +302,40 @@ def test_backward_wgrad_single_buffer_bitwise(kind, gz, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn"])
+def test_backward_fused_x_bitwise(kind):
+    """train_fuse_x: the encoder kernel storing the gathered rows as the tower input x (1: DeepFM, the
+    default; 2: the first-order models too) gives bitwise the gradients and loss of encoder + gather_x (0):
+    x is a copy either way and the first order / FM arithmetic is unchanged."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K, B = 20_000, 39, 16, 777
+    m = _gpu_model(rmx, kind, V, F, K, (32, 16))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 21, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(2).random(B) > 0.7).astype(np.float32))
+    res = {}
+    try:
+        for v in (0, 1, 2):
+            rmx.set_tuning("train_fuse_x", v)
+            out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, len(mats), 1)]
+            m.backward_ids(t, B, ids, targets, *out)
+            ctx.sync()
+            res[v] = [o.numpy().copy() for o in out]
+    finally:
+        rmx.set_tuning("train_fuse_x", None)
+    for v in (1, 2):
+        for a, b in zip(res[0], res[v]):
+            assert np.array_equal(a, b), v
+
+
+@pytest.mark.gpu
 def test_backward_wgrad_sq_tile_cin():
     """The CIN's generated-operand dW on the 208 x 208 tile (wgrad_sq_gz 1) against the 208 x 128 one
     (the default): rows = B k = 65,584 (a ragged chunk), within 2e-5 relative per mats block."""
