@@ -130,6 +130,8 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * FC[0] * FC[1]
     if stage == "tower_layer3":
         return "flop", 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
+    if stage == "tower_tail":  # bf16: layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip)
+        return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
     if stage.startswith("cin_layer"):
         idx = {"cin_layer1": 0, "cin_layer2": 1, "cin_layer3+": 2}[stage]
         hp = F if idx == 0 else CIN[idx - 1]

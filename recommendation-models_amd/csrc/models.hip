@@ -801,6 +801,12 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   for (size_t i = 0; i < m.layers.size(); ++i) {
     const bool last = i + 1 == m.layers.size();
     const DenseLayer& L = m.layers[i];
+    // bf16: the last hidden layer and the output layer in one persistent kernel (k_tail.hip)
+    if (i >= 1 && i + 2 == m.layers.size() && m.precision == kBF16 &&
+        tower_tail_usable(L, m.layers[i + 1], B, lda)) {
+      StageTimer t(m, s, "tower_tail");
+      return launch_tower_tail_bf16(s, L, m.layers[i + 1], B, reinterpret_cast<const bf16_t*>(A), lda, oa);
+    }
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
     XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};

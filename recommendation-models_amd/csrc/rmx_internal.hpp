@@ -125,6 +125,11 @@ bool tower_fm_fusable(const DenseLayer& L, int M, const AGatherArgs* gather, boo
 // (k_gemm.hpp kWRing): the first order is then summed from LDS at no cost
 bool tower_wring(const DenseLayer& L, int M, const AGatherArgs* ga);
 
+// bf16 tower tail (k_tail.hip): ReLU(H L2) -> ReLU(. L3) . wo -> head, one persistent launch, when
+// both layers are bf16 with Npad = Kpad = 416; H [M][lda] bf16
+bool tower_tail_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda);
+int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const bf16_t* H, int lda,
+                           const OutArgs& oa);
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
 // ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1); xo (k = 16,

@@ -180,6 +180,7 @@ def test_bf16_fast_ring_variant_bitwise(kind):
     out = rmx.DeviceArray(ctx, B, np.float32)
     got = {}
     try:
+        rmx.set_tuning("bf16_tail", 0)  # the engine's layers 2 / 3 (the tail kernel has its own test)
         for var in (None, 6):
             rmx.set_tuning("tower_variant", var)
             m.forward_ids(t, B, ids_d, out)
@@ -187,6 +188,7 @@ def test_bf16_fast_ring_variant_bitwise(kind):
             got[var] = out.numpy().copy()
     finally:
         rmx.set_tuning("tower_variant", None)
+        rmx.set_tuning("bf16_tail", None)
     assert np.array_equal(got[6], got[None])
     wt, et = _rounded_table(V)
     n = 256
@@ -195,3 +197,53 @@ def test_bf16_fast_ring_variant_bitwise(kind):
     index = np.repeat(np.arange(n, dtype=np.int64), F)
     ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 2)
     assert np.abs(got[6][B - n:] - ref).max() <= TOL_BF16
+
+
+@pytest.mark.parametrize("kind,B", [("dcn", 65536), ("pnn", 65536), ("dcn", 37), ("pnn", 1000),
+                                    ("dcn", 300 * 64 + 17), ("dnn32", 4099)])
+def test_bf16_tower_tail_matches_unfused(kind, B):
+    """The bf16 tower tail (csrc/k_tail.hip: the last hidden layer + the output layer in one persistent
+    launch, h2 kept in LDS) against the same model with the tail off (two engine launches, h2 through
+    HBM) and against the bf16 oracle.  B covers one partial row block (37), a ragged last block
+    (1000), more row blocks than CUs (several per block: 19,217 and 65,536).  dnn32 has no tail
+    (its 400-wide layer has K = 32): the fallback must be taken, bitwise."""
+    import rmx
+    ctx = rmx.default_context()
+    V = 50_003
+    m, om = _model(kind, V)
+    t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16)
+    t.fill_synthetic(SEED_TAB)
+    mats = oc.round_bf16(m.initMats(SEED_MATS))
+    m.setPrecision(rmx.DTYPE_BF16)
+    m.setMats(mats)
+    m.setBias(0.01)
+    ids_d = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_d)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    got = {}
+    try:
+        for tail in (0, 1):
+            rmx.set_tuning("bf16_tail", tail)
+            m.set_timing(True)
+            m.forward_ids(t, B, ids_d, out)
+            ctx.sync()
+            stages, _ = m.get_timing()
+            m.set_timing(False)
+            got[tail] = out.numpy().copy()
+            assert ("tower_tail" in stages) == (tail == 1 and kind != "dnn32"), stages
+    finally:
+        rmx.set_tuning("bf16_tail", None)
+    diff = float(np.abs(got[1] - got[0]).max())
+    print("%s B=%d: max|p_tail - p_unfused| = %.3g" % (kind, B, diff))
+    if kind == "dnn32":
+        assert np.array_equal(got[1], got[0])
+    else:
+        # h2 is the same bf16 of the same fp32 sums; only the logit's summation order differs
+        assert diff <= 5e-5
+    wt, et = _rounded_table(V)
+    for r0, n in ((0, min(B, 256)), (max(0, B - 100), min(B, 100))):
+        ids = oc.gen_ids(SEED_IDS, r0, n, F, V).astype(np.int64)
+        w, e = oc.gather(wt, et, 1, ids)
+        index = np.repeat(np.arange(n, dtype=np.int64), F)
+        ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 2)
+        assert np.abs(got[1][r0:r0 + n] - ref).max() <= TOL_BF16
