@@ -37,22 +37,44 @@
 namespace rmx {
 namespace {
 
-constexpr int kTBM = 64;                   // rows per row block
-constexpr int kTNT = 26;                   // 16-column tiles: Npad = 416 (N <= 416)
+constexpr int kTBM = 128;                  // rows per row block
+constexpr int kTMT = kTBM / 16;            // row tiles
+constexpr int kTNT = 25;                   // computed 16-column tiles (N <= 400)
+constexpr int kTN = 416;                   // Npad: packed rows of W per K step
 constexpr int kTKS = 13;                   // 32-wide K steps: Kpad = 416
-constexpr int kTN = kTNT * 16;
-constexpr int kTCW = 12;                   // compute waves
-constexpr int kTLW = 4;                    // loader waves
+constexpr int kTCW = 13;                   // compute waves: w < 12 own tiles w, w + 12; wave 12 tile 24
+constexpr int kTLW = 3;                    // loader waves (13, 14, 15)
 constexpr int kTThreads = (kTCW + kTLW) * 64;
-constexpr int kTImg = kTKS * kTBM * 64;    // bytes of one h tile image [step][row][64 B] (53,248)
-constexpr int kTIns = kTImg / 1024;        // 1-KiB DMA instructions per image (52)
-// weight fragments are loaded PF K steps ahead: 2 for the two-tile waves, 1 for the three-tile ones
-// (2 spills there at the 128-VGPR budget of 4 waves per SIMD)
-template <int NTW>
-constexpr int kTPF = NTW >= 3 ? 1 : 2;
-constexpr size_t kTLds = 2 * kTImg + sizeof(float) * kTCW * kTBM;
+constexpr int kTImg = kTKS * kTBM * 64;    // bytes of the h tile image [step][row][64 B] (106,496)
+constexpr int kTH1 = 7;                    // K steps in the image's first half
+constexpr int kTInsA = kTH1 * kTBM * 64 / 1024;            // 1-KiB DMA instructions, first half (56)
+constexpr int kTInsB = (kTKS - kTH1) * kTBM * 64 / 1024;   // second half (48)
+constexpr int kTPerB = kTInsB / kTLW;                      // 16 per loader (the counted wait below)
+constexpr int kTPF = 2;                    // weight fragments loaded this many K steps ahead
+constexpr int kTPrm = 3 * kTN;              // b2, b3, wo staged in LDS (fp32)
+constexpr size_t kTLds = kTImg + sizeof(float) * (kTCW * kTBM + kTPrm);
 
-static_assert(kTIns % kTLW == 0, "every loader issues the same DMAs");
+static_assert(kTInsB % kTLW == 0 && kTPerB == 16, "the loaders' counted vmcnt wait assumes 16 second-half DMAs each");
+
+// Diagnostic builds only (timing probes, wrong results; never set in librmx.so): 1 = no weight loads
+// in the K loops (the prologue's fragments reused), 4 = no h1 prefetch after the first tile, 8 = no
+// head (the finish of each row block)
+#ifndef RMX_TAIL_DIAG
+#define RMX_TAIL_DIAG 0
+#endif
+// 16: s_memtime stamps of block 0's waves 0, 2, 12 (compute) and 13 (loader 0) at every barrier of
+// its row blocks (tools/diag_tail_stamps.py reads them through rmx_diag_tail)
+#if RMX_TAIL_DIAG & 16
+__device__ unsigned long long g_tail_t[4][40];
+#define TS(k)                                                                              \
+  do {                                                                                     \
+    if (dslot >= 0 && (k) < 40) g_tail_t[dslot][k] = __builtin_amdgcn_s_memtime();       \
+  } while (0)
+#else
+#define TS(k) \
+  do {        \
+  } while (0)
+#endif
 
 struct TailArgs {
   int M, nblk;
@@ -70,147 +92,111 @@ __device__ __forceinline__ void bar_lds() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
-
-// weight fragment of K step c, the wave's column tile j: Wl = this lane's element of the wave's
-// first tile (W + ((w * 16 + r16) * 32 + g * 8)); tile j is 12 tiles further: 1 KiB per wave
-__device__ __forceinline__ f32x4 ldw(const bf16_t* Wl, int c, int j) {
-  return *reinterpret_cast<const f32x4*>(Wl + (c * kTN + j * kTCW * 16) * 32);
-}
-// the lane's base of ldw, opaque to the optimiser so that the 13 x NTW fragment addresses are formed
-// step by step instead of being hoisted out of the row-block loop (which spilled)
-__device__ __forceinline__ const bf16_t* wlane(const bf16_t* W, int w, int lane) {
-  const bf16_t* Wl = W + ((w * 16 + (lane & 15)) * 32 + (lane >> 4) * 8);
-  asm volatile("" : "+v"(Wl));
-  return Wl;
-}
-// h fragment of K step c for tile row `row`, k slot g, from a swizzled image
-__device__ __forceinline__ f32x4 ldh(const char* img, int c, int row, int g) {
-  return *reinterpret_cast<const f32x4*>(img + ((c * kTBM + row) * 4 + swz_slot(row, g)) * 16);
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
-// one layer's K loop: acc[i][j] (tile row i, column tile j) += W_j h_i^T over the 13 steps; wb holds
-// the prologue's fragments of steps 0 .. kTPF - 1 on entry
-template <int NTW>
-__device__ __forceinline__ void tail_layer(const bf16_t* Wl, const char* img, int lane,
-                                           f32x4 (&acc)[4][NTW], f32x4 (&wb)[kTPF<NTW> + 1][NTW]) {
-  const int g = lane >> 4, r16 = lane & 15;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < kTKS; ++c) {
-    if (c + kTPF<NTW> < kTKS)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) wb[(c + kTPF<NTW>) % (kTPF<NTW> + 1)][j] = ldw(Wl, c + kTPF<NTW>, j);
-    f32x4 a[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = ldh(img, c, 16 * i + r16, g);
-    __builtin_amdgcn_sched_barrier(0);  // one step's loads at a time (hoisting them all spills)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb[c % (kTPF<NTW> + 1)][j]),
-                                                            __builtin_bit_cast(bf16x8, a[i]), acc[i][j], 0, 0, 0);
-  }
+// weight fragment of K step c, the wave's column tile j: lane offset wo = this lane's element of the
+// wave's first tile ((w * 16 + r16) * 32 + g * 8); tile j is 12 tiles further: 1 KiB per wave.  W stays
+// a kernel-argument pointer (global address space: global_load, counted by vmcnt only; a laundered
+// pointer would become a flat load, which also counts in lgkmcnt and made every LDS wait a full drain)
+__device__ __forceinline__ f32x4 ldw(const bf16_t* __restrict__ W, int wo, int c, int j) {
+  return *reinterpret_cast<const f32x4*>(W + wo + (c * kTN + j * 12 * 16) * 32);
+}
+// the lane's offset for ldw, opaque to the optimiser so that the fragment addresses are formed step
+// by step instead of being hoisted out of the row-block loop (which spilled)
+__device__ __forceinline__ int wlane(int w, int lane) {
+  int wo = (w * 16 + (lane & 15)) * 32 + (lane >> 4) * 8;
+  asm volatile("" : "+v"(wo));
+  return wo;
+}
+// h fragment of K step c, row tile i, from the swizzled image.  The swizzle key of row 16 i + r16 is
+// that of r16 ((row >> 2) & 3 drops the 16 i), so a lane's fragments sit at one per-lane base hb =
+// (r16 * 4 + swz_slot(r16, g)) * 16 plus compile-time offsets (ds_read immediates); hb is opaque so
+// the 13 x 8 addresses are not formed up front (they spilled)
+__device__ __forceinline__ int hbase(int lane) {
+  int hb = ((lane & 15) * 4 + swz_slot(lane & 15, lane >> 4)) * 16;
+  asm volatile("" : "+v"(hb));
+  return hb;
+}
+__device__ __forceinline__ f32x4 ldh(const char* img, int hb, int c, int i) {
+  return *reinterpret_cast<const f32x4*>(img + hb + (c * kTBM + 16 * i) * 64);
 }
 
-template <int NTW>
-__device__ __forceinline__ void tail_prologue(const bf16_t* Wl, f32x4 (&wb)[kTPF<NTW> + 1][NTW]) {
+// K steps [C0, C1) of a layer: acc[i][j] (row tile i, column tile j) += W_j h_i^T; wb holds the
+// fragments of steps C0 .. C0 + kTPF - 1 on entry (ring slot c % (kTPF + 1))
+template <int NTW, int C0, int C1>
+__device__ __forceinline__ void tail_steps(const bf16_t* __restrict__ W, int wo, const char* img, int lane, f32x4 (&acc)[kTMT][NTW],
+                                           f32x4 (&wb)[kTPF + 1][NTW]) {
+  const int hb = hbase(lane);
 #pragma unroll
-  for (int c = 0; c < kTPF<NTW>; ++c)
+  for (int c = C0; c < C1; ++c) {
+    if (c + kTPF < kTKS && !(RMX_TAIL_DIAG & 1)) {
+      int wc = wo + (c + kTPF) * kTN * 32;
+      asm volatile("" : "+v"(wc));  // formed here, not all 13 at the layer's start
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) wb[c][j] = ldw(Wl, c, j);
-}
-
-template <int NTW>
-__device__ void tail_compute(const TailArgs& p, char* smem, int w, int lane, int nit) {
-  const int g = lane >> 4, r16 = lane & 15;
-  float* red = reinterpret_cast<float*>(smem + 2 * kTImg);  // [kTCW][kTBM] partial logits
-  f32x4 acc[4][NTW];
-  f32x4 wb[kTPF<NTW> + 1][NTW];
-  tail_prologue<NTW>(wlane(p.W2, w, lane), wb);
-  for (int it = 0; it < nit; ++it) {
-    const int rb = blockIdx.x + it * gridDim.x;
-    char* img = smem + (it & 1) * kTImg;
-    __builtin_amdgcn_s_barrier();  // B0: the loaders' DMAs of this tile have landed
-    asm volatile("" ::: "memory");
-    tail_layer<NTW>(wlane(p.W2, w, lane), img, lane, acc, wb);
-    tail_prologue<NTW>(wlane(p.W3, w, lane), wb);  // in flight across the epilogue
-    bar_lds();                              // B1: every wave has read the tile
-    // h2 = bf16(ReLU(acc + b2)) into the same image: lane holds n = 16 t + 4 g .. + 3 of row 16 i + r16
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int n0 = 16 * (w + kTCW * j) + 4 * g;
-      const f32x4 bb = p.b2 ? *reinterpret_cast<const f32x4*>(p.b2 + n0) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const int c = n0 >> 5, slot = (n0 & 31) >> 3, half = (n0 >> 2) & 1;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 16 * i + r16;
-        f32x4 v = acc[i][j] + bb;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-        *reinterpret_cast<bf16x4*>(img + ((c * kTBM + row) * 4 + swz_slot(row, slot)) * 16 + half * 8) =
-            __builtin_convertvector(v, bf16x4);
-      }
+      for (int j = 0; j < NTW; ++j) wb[(c + kTPF) % (kTPF + 1)][j] = ldw(W, wc, 0, j);
     }
-    bar_lds();  // B2: h2 complete
-    tail_layer<NTW>(wlane(p.W3, w, lane), img, lane, acc, wb);
-    if (it + 1 < nit) tail_prologue<NTW>(wlane(p.W2, w, lane), wb);
-    // output dot: part[i] = sum over this lane's n of ReLU(acc + b3)[n] * wo[n], then over the 4 lane groups
-    float part[4] = {0.f, 0.f, 0.f, 0.f};
+    // two groups of four row tiles: each group's four fragments, then its MFMAs (all eight at
+    // once would hold 32 more registers)
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int n0 = 16 * (w + kTCW * j) + 4 * g;
-      const f32x4 bb = p.b3 ? *reinterpret_cast<const f32x4*>(p.b3 + n0) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 wv = *reinterpret_cast<const f32x4*>(p.oa.wo + n0);
+    for (int h = 0; h < 2; ++h) {
+      f32x4 a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = ldh(img, hb, c, 4 * h + i);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[i][j][r] + bb[r];
-          v = v > 0.f ? v : 0.f;
-          part[i] += v * wv[r];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      part[i] += __shfl_xor(part[i], 16);
-      part[i] += __shfl_xor(part[i], 32);
-      if (g == 0) red[w * kTBM + 16 * i + r16] = part[i];
-    }
-    bar_lds();  // B3: partial logits complete
-    if (w == 0) {
-      const int m = rb * kTBM + lane;
-      if (m < p.M) {
-        const OutArgs& oa = p.oa;
-        float y = red[lane];
-#pragma unroll
-        for (int q = 1; q < kTCW; ++q) y += red[q * kTBM + lane];
-        if (oa.has_bo) y = y + oa.bo;
-        if (oa.rowsum) {
-          float rs = 0.f;
-          for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
-          y = rs + y;
-        }
-        if (oa.pre2) y = oa.pre2[m] + y;
-        float t = oa.pre ? oa.pre[m] + y : y;
-        t = t + oa.beta;
-        oa.out[m] = 1.0f / (1.0f + expf(-t));
-      }
+        for (int j = 0; j < NTW; ++j)
+          acc[4 * h + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, wb[c % (kTPF + 1)][j]), __builtin_bit_cast(bf16x8, a[i]), acc[4 * h + i][j], 0, 0, 0);
     }
   }
 }
 
-// loader wave lw: its share (13 of the 52 1-KiB instructions) of row block rb's h tile into image
-// `img`; lane L of instruction ins fills image row R = 16 ins + L / 4 (R = step * 64 + row) at
-// physical slot L & 3, i.e. loads logical slot swz_slot(row, L & 3) (the swizzle is an involution)
-__device__ void tail_issue(const TailArgs& p, char* img, int rb, int lw, int lane, const float* zero16) {
-  const int m0 = rb * kTBM;
+template <int NTW>
+__device__ __forceinline__ void tail_prologue(const bf16_t* __restrict__ W, int wo, f32x4 (&wb)[kTPF + 1][NTW]) {
 #pragma unroll
-  for (int q = 0; q < kTIns / kTLW; ++q) {
-    const int ins = lw + kTLW * q;
+  for (int c = 0; c < kTPF; ++c)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) wb[c][j] = ldw(W, wo, c, j);
+}
+
+template <int NTW>
+__device__ __forceinline__ void tail_zero(f32x4 (&acc)[kTMT][NTW]) {
+#pragma unroll
+  for (int i = 0; i < kTMT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// h2 columns n0 .. n0 + 3 of rows 16 i + r16 go to per-lane base pbase(n0) + 1 KiB * i (same key
+// argument as hbase) as one bf16x4 (8 B)
+__device__ __forceinline__ int pbase(int lane, int n0) {
+  const int r16 = lane & 15, c = n0 >> 5, slot = (n0 & 31) >> 3, half = (n0 >> 2) & 1;
+  int pb = ((c * kTBM + r16) * 4 + swz_slot(r16, slot)) * 16 + half * 8;
+  asm volatile("" : "+v"(pb));
+  return pb;
+}
+__device__ __forceinline__ void put_h2(char* img, int pb, int i, const f32x4& v) {
+  *reinterpret_cast<bf16x4*>(img + pb + i * 1024) = __builtin_convertvector(v, bf16x4);
+}
+
+// issuing wave idx of nidx: its share of one half of row block rb's h1 image (half 0: K steps 0 .. 6,
+// DMA instructions 0 .. 55; half 1: steps 7 .. 12, instructions 56 .. 103).  Lane L of instruction ins
+// fills image row R = 16 ins + L / 4 (R = step * 128 + row) at physical slot L & 3, i.e. loads
+// logical slot swz_slot(row, L & 3) (the swizzle is an involution).
+template <int HALF>
+__device__ __forceinline__ void tail_issue(const TailArgs& p, char* img, int rb, int idx, int nidx, int lane,
+                                           const float* zero16) {
+  constexpr int ins0 = HALF ? kTInsA : 0, nins = HALF ? kTInsB : kTInsA;
+  const int m0 = rb * kTBM;
+  // a rolled loop: unrolled, the 104 per-lane sources / LDS bases were formed up front and spilled
+#pragma unroll 1
+  for (int k = idx; k < nins; k += nidx) {
+    const int ins = ins0 + k;
     const int R = ins * 16 + (lane >> 2);
     const int c = R / kTBM, row = R - c * kTBM;
     const int m = m0 + row, kk = c * 32 + swz_slot(row, lane & 3) * 8;
@@ -219,44 +205,219 @@ __device__ void tail_issue(const TailArgs& p, char* img, int rb, int lw, int lan
   }
 }
 
+// Compute wave with first column tile w (NTW tiles: w, w + 12; the last compute wave w = 24, one
+// tile): barriers B0, BM2, B1, B2, BM3, B3 per row block, the same six as the loaders
+template <int NTW>
+__device__ void tail_compute(const TailArgs& p, char* img, float* red, const float* prm, int w, int lane, int nit,
+                             const float* zero16) {
+  const int g = lane >> 4, r16 = lane & 15;
+#if RMX_TAIL_DIAG & 16
+  const int dslot = (blockIdx.x == 0 && lane == 0) ? (w == 0 ? 0 : (w == 2 ? 1 : (w == 24 ? 2 : -1))) : -1;
+#endif
+  TS(0);
+  f32x4 acc[kTMT][NTW];
+  f32x4 wb[kTPF + 1][NTW];
+  // the first row block's first half: every wave of the block issues its DMAs (issue, not HBM, limits
+  // a start from an empty ring), then the weight prologue
+  if (nit > 0) tail_issue<0>(p, img, blockIdx.x, w < 12 ? w : kTCW - 1, 16, lane, zero16);
+  tail_prologue<NTW>(p.W2, wlane(w, lane), wb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int it = 0; it < nit; ++it) {
+    bar();  // B0: the first half of this row block's h1 image has landed
+    TS(1 + 10 * it);
+    {
+      const int wo = wlane(w, lane);
+      tail_zero<NTW>(acc);
+      tail_steps<NTW, 0, kTH1>(p.W2, wo, img, lane, acc, wb);
+      TS(2 + 10 * it);
+      bar();  // BM2: the second half has landed
+      TS(3 + 10 * it);
+      tail_steps<NTW, kTH1, kTKS>(p.W2, wo, img, lane, acc, wb);
+    }
+    tail_prologue<NTW>(p.W3, wlane(w, lane), wb);  // in flight across the epilogue
+    TS(4 + 10 * it);
+    bar_lds();                                      // B1: every wave has read the h1 image
+    TS(5 + 10 * it);
+    // h2 = bf16(ReLU(acc + b2)) into the same image; lane holds n = 16 t + 4 g .. + 3 of row 16 i + r16
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n0 = 16 * (w + 12 * j) + 4 * g;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(prm + n0);
+      const int pb = pbase(lane, n0);
+#pragma unroll
+      for (int i = 0; i < kTMT; ++i) {
+        f32x4 v = acc[i][j] + bb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+        put_h2(img, pb, i, v);
+      }
+    }
+    if (w == 2 * 12) {  // columns 400 .. 415 (not computed) read as zeros by the next layer
+      const int pb = pbase(lane, 16 * kTNT + 4 * g);
+#pragma unroll
+      for (int i = 0; i < kTMT; ++i) put_h2(img, pb, i, f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+    bar_lds();  // B2: h2 complete
+    TS(6 + 10 * it);
+    {
+      const int wo = wlane(w, lane);
+      tail_zero<NTW>(acc);
+      tail_steps<NTW, 0, kTH1>(p.W3, wo, img, lane, acc, wb);
+      TS(7 + 10 * it);
+      bar_lds();  // BM3: steps 0 .. 6 read by every wave: the loaders refill them with the next block
+      TS(8 + 10 * it);
+      tail_steps<NTW, kTH1, kTKS>(p.W3, wo, img, lane, acc, wb);
+    }
+    if (it + 1 < nit) tail_prologue<NTW>(p.W2, wlane(w, lane), wb);
+    // output dot: part[i] = sum over this lane's n of ReLU(acc + b3)[n] * wo[n], then over the 4 lane groups
+    float part[kTMT];
+#pragma unroll
+    for (int i = 0; i < kTMT; ++i) part[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n0 = 16 * (w + 12 * j) + 4 * g;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(prm + kTN + n0);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(prm + 2 * kTN + n0);
+#pragma unroll
+      for (int i = 0; i < kTMT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] + bb[r];
+          v = v > 0.f ? v : 0.f;
+          part[i] += v * wv[r];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kTMT; ++i) {
+      part[i] += __shfl_xor(part[i], 16);
+      part[i] += __shfl_xor(part[i], 32);
+      if (g == 0) red[(w < 12 ? w : kTCW - 1) * kTBM + 16 * i + r16] = part[i];
+    }
+    TS(9 + 10 * it);
+    bar_lds();  // B3: partial logits complete, the image is free
+    TS(10 + 10 * it);
+  }
+}
+
 __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs p) {
   extern __shared__ __attribute__((aligned(16))) char tsmem[];
+  char* img = tsmem;
+  float* red = reinterpret_cast<float*>(tsmem + kTImg);  // [kTCW][kTBM] partial logits
+  float* prm = red + kTCW * kTBM;                         // b2 | b3 | wo, kTN each
   const float* zero16 = g_rmx_zero16;
   asm volatile("" : "+s"(zero16));
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nit = blockIdx.x < p.nblk ? (p.nblk - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  if (w < 2) {
-    tail_compute<3>(p, tsmem, w, lane, nit);
-  } else if (w < kTCW) {
-    tail_compute<2>(p, tsmem, w, lane, nit);
+  if (w < kTCW - 1) {
+    tail_compute<2>(p, img, red, prm, w, lane, nit, zero16);
+  } else if (w == kTCW - 1) {
+    tail_compute<1>(p, img, red, prm, 2 * 12, lane, nit, zero16);
   } else {
-    // loaders: tile it + 1 streams in while the compute waves run tile it; every wave passes the
-    // same four barriers per tile (B0 .. B3)
+    // loaders.  Row block it + 1's first half streams in behind layer 3's second half of block it, its
+    // second half behind layer 2's first half of block it + 1 (issued after B0, so B0 waits for no
+    // issue).  Loader 0 also runs the head of block it - 1 after B0 (its inputs loaded a block early;
+    // red[] is rewritten only after BM3).
     const int lw = w - kTCW;
-    if (nit > 0) tail_issue(p, tsmem, blockIdx.x, lw, lane, zero16);
-    for (int it = 0; it < nit; ++it) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // B0
-      if (it + 1 < nit) tail_issue(p, tsmem + ((it + 1) & 1) * kTImg, blockIdx.x + (it + 1) * gridDim.x, lw, lane, zero16);
-      __builtin_amdgcn_s_barrier();  // B1
-      __builtin_amdgcn_s_barrier();  // B2
-      __builtin_amdgcn_s_barrier();  // B3
+    const OutArgs& oa = p.oa;
+#if RMX_TAIL_DIAG & 16
+    const int dslot = (blockIdx.x == 0 && lane == 0 && lw == 0) ? 3 : -1;
+#endif
+    TS(0);
+    if (nit > 0) tail_issue<0>(p, img, blockIdx.x, kTCW + lw, 16, lane, zero16);
+    {  // the epilogue parameters into LDS (read after B1 / BM3 by the compute waves)
+      float v[(kTPrm + kTLW * 64 - 1) / (kTLW * 64)];
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(v) / sizeof(float)); ++q) {
+        const int i = lw * 64 + lane + q * kTLW * 64;
+        const int a = i / kTN, n = i - a * kTN;
+        const float* src = a == 0 ? p.b2 : (a == 1 ? p.b3 : oa.wo);
+        v[q] = (i < kTPrm && src) ? src[n] : 0.f;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and this loader's first-half DMAs: B0 needs them)
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(v) / sizeof(float)); ++q) {
+        const int i = lw * 64 + lane + q * kTLW * 64;
+        if (i < kTPrm) prm[i] = v[q];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    if (nit > 0) tail_issue<1>(p, img, blockIdx.x, lw, kTLW, lane, zero16);
+    float hin[2] = {0.f, 0.f}, hpre[2] = {0.f, 0.f};    // the head's inputs of rows lane, lane + 64
+    float pin[2] = {0.f, 0.f}, ppre[2] = {0.f, 0.f};    // ... of the previous row block
+    auto head = [&](int rb, const float* in2, const float* pr) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = lane + 64 * h, m = rb * kTBM + row;
+        if (m < p.M) {
+          float y = red[row];
+#pragma unroll
+          for (int q = 1; q < kTCW; ++q) y += red[q * kTBM + row];
+          if (oa.has_bo) y = y + oa.bo;
+          if (oa.rowsum || oa.pre2) y = in2[h] + y;
+          float t = oa.pre ? pr[h] + y : y;
+          t = t + oa.beta;
+          oa.out[m] = 1.0f / (1.0f + expf(-t));
+        }
+      }
+    };
+    for (int it = 0; it < nit; ++it) {
+      const int rb = blockIdx.x + it * gridDim.x;
+      if (it > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // first half landed
+      TS(1 + 10 * it);
+      bar();  // B0
+      if (it > 0) {
+        if (!(RMX_TAIL_DIAG & 4)) tail_issue<1>(p, img, rb, lw, kTLW, lane, zero16);
+        if (lw == 0 && !(RMX_TAIL_DIAG & 8)) head(rb - (int)gridDim.x, pin, ppre);
+      }
+      if (lw == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int m = rb * kTBM + lane + 64 * h;
+          if (m < p.M) {
+            float rs = 0.f;
+            if (oa.rowsum)
+              for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
+            hin[h] = oa.rowsum ? rs : (oa.pre2 ? oa.pre2[m] : 0.f);  // (rowsum and pre2 never together)
+            hpre[h] = oa.pre ? oa.pre[m] : 0.f;
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // second half landed
+      TS(2 + 10 * it);
+      bar();                                              // BM2
+      bar();                                              // B1
+      bar();                                              // B2
+      bar();                                              // BM3
+      if (it + 1 < nit && !(RMX_TAIL_DIAG & 4)) tail_issue<0>(p, img, rb + gridDim.x, lw, kTLW, lane, zero16);
+      bar();  // B3
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        pin[h] = hin[h];
+        ppre[h] = hpre[h];
+      }
+    }
+    if (lw == 0 && nit > 0 && !(RMX_TAIL_DIAG & 8)) head(blockIdx.x + (nit - 1) * gridDim.x, pin, ppre);
   }
 }
 
 }  // namespace
 
+#if RMX_TAIL_DIAG & 16
+extern "C" int rmx_diag_tail(unsigned long long* out160) {
+  return hipMemcpyFromSymbol(out160, HIP_SYMBOL(g_tail_t), sizeof(unsigned long long) * 160) == hipSuccess ? 0 : -5;
+}
+#endif
+
 bool tower_tail_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda) {
   return tuning_get("bf16_tail", 1) != 0 && M > 0 && L2.W16 && L3.W16 && L2.Npad == kTN && L3.Npad == kTN &&
-         L2.Kpad == kTKS * 32 && L3.Kpad == kTKS * 32 && L3.K <= L2.Npad && lda >= L2.K && lda % 8 == 0 &&
-         L2.N1 < 0 && L3.N1 < 0;
+         L2.N <= 16 * kTNT && L3.N <= 16 * kTNT && L2.Kpad == kTKS * 32 && L3.Kpad == kTKS * 32 &&
+         L3.K <= 16 * kTNT && lda >= L2.K && lda % 8 == 0 && L2.N1 < 0 && L3.N1 < 0;
 }
 
 int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const bf16_t* H, int lda,
                            const OutArgs& oa) {
-  if (!tower_tail_usable(L2, L3, M, lda) || !oa.wo || !oa.out) {
-    set_error("tower tail: needs two bf16 layers of Npad = Kpad = 416 and an output head");
+  if (!tower_tail_usable(L2, L3, M, lda) || !oa.wo || !oa.out || (oa.rowsum && oa.pre2)) {
+    set_error("tower tail: needs two bf16 layers of N <= 400 (Npad = Kpad = 416) and an output head");
     return RMX_E_INVALID;
   }
   int dev = 0, ncu = 0;

@@ -162,6 +162,12 @@ int alloc_wt(DenseLayer& L) {
 // the GEMM gathers 16-B slots straight from table rows: k must be a multiple of 4 fp32 / 8 bf16
 bool needs_gather_x(const rmx_model& m) { return m.k % (m.precision == kBF16 ? 8 : 4) != 0; }
 
+// row stride (elements) of the materialised layer-1 input xbuf (PNN [x | ip], generic-k x): Kpad
+// rounded up to whole 128-B lines, so no row of the GEMM's A operand straddles a line boundary
+// (PNN bf16: 1,376 -> 1,408 elements; fp32 rows of 1,376 are already 43 lines)
+int xbuf_ld_max(const rmx_model& m) { return round_up(m.layers[0].Kpad, m.precision == kBF16 ? 64 : 32); }
+int xbuf_ld(const rmx_model& m) { return tuning_get("x_line_pad", 1) ? xbuf_ld_max(m) : m.layers[0].Kpad; }
+
 }  // namespace
 
 int model_build(rmx_model& m) {
@@ -601,7 +607,7 @@ int ensure_ws(rmx_model& m, int B) {
   if ((st = dev_alloc(&m.pre2, B))) return st;
   if (m.dcn_fused && (st = dev_alloc(&m.xcol, (size_t)B * (m.cross_depth + 1)))) return st;
   if (m.type == RMX_MODEL_PNN || (m.type != RMX_MODEL_LR && needs_gather_x(m))) {
-    if ((st = dev_alloc(&m.xbuf, (size_t)B * m.layers[0].Kpad))) return st;
+    if ((st = dev_alloc(&m.xbuf, (size_t)B * xbuf_ld_max(m)))) return st;
   }
   if (!m.cin_layers.empty()) {
     int maxH = 16;
@@ -782,18 +788,18 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   } else if (m.type == RMX_MODEL_PNN) {
     StageTimer t(m, s, "product");
     if ((st = launch_product(s, B, F, k, in.ids, in.table, in.dtype, m.pairs, F * (F - 1) / 2, m.xbuf, m.precision,
-                              m.layers[0].Kpad)))
+                              xbuf_ld(m))))
       return st;
     A = m.xbuf;
-    lda = m.layers[0].Kpad;
+    lda = xbuf_ld(m);
     gather_first = false;
   }
   if (m.type != RMX_MODEL_PNN && !gather_first) {
     StageTimer t(m, s, "gather_x");
-    if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, in.dtype, m.xbuf, m.precision, m.layers[0].Kpad)))
+    if ((st = launch_gather_x(s, B, F, k, in.ids, in.table, in.dtype, m.xbuf, m.precision, xbuf_ld(m))))
       return st;
     A = m.xbuf;
-    lda = m.layers[0].Kpad;
+    lda = xbuf_ld(m);
   }
 
   // 3. tower (the last layer runs the output head: dot + bias + CAddTable + Sigmoid)
