@@ -125,6 +125,7 @@ struct GemmArgs {
   float* xcol;         // kEpiRelu: raw extra columns n >= xn_main -> xcol[m * xld + n - xn_main] (DCN cross)
   int xn_main, xld;
   int prio;            // 1: the first half of the block's waves issue at raised priority (s_setprio)
+  int nt_store;        // 1: stored activations use non-temporal stores (knob "gemm_nt_store")
   // DeepFM first order + FM fused into tower layer 1 (kGatherK16 + kPrecS3, column slice 0): the A
   // tiles that stream through LDS are the gathered field rows, so the FM sums ride along and
   // fm_y[m] = y1 + y2 (bit-identical to encoder_k16_kernel<1>: same fp32 order, no contraction).
@@ -1185,6 +1186,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
           }
           if constexpr (BF)
             *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(dst) + o) = __builtin_convertvector(v, bf16x4);
+          else if (p.nt_store)
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(dst + o));
           else
             *reinterpret_cast<f32x4*>(dst + o) = v;
         }

@@ -192,6 +192,7 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   }
   const int var = tuning_get("s3_tower", 1);
   p.prio = tuning_get("gemm_prio", 0);
+  p.nt_store = tuning_get("gemm_nt_store", 0);
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
   // 3: 16-row waves, a single-buffered 57 KiB stage, two blocks per CU (4 waves / SIMD)
   if (var == 3) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 4, 1>, kPrecS3>(s, p, amode, epi);
@@ -232,6 +233,7 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 int launch_cin_s3(hipStream_t s, GemmArgs& p) {
   const int var = tuning_get("s3_cin", 2);
   p.prio = tuning_get("gemm_prio", 0);
+  p.nt_store = tuning_get("gemm_nt_store", 0);
   if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   if (var == 2) {
     if (tuning_get("s3_stagger", 1) == 2)

@@ -113,18 +113,149 @@ __global__ __launch_bounds__(kRedThreads) void bce_kernel(int B, const float* __
   }
 }
 
-// loss = sum(part_l) / B; every non-null target of the bias gradient = sum(part_g)
-__global__ void bce_finish_kernel(int nparts, int B, const double* __restrict__ part, float* __restrict__ loss,
-                                  float* __restrict__ gbias, float* __restrict__ gbias2) {
-  if (threadIdx.x != 0) return;
+// loss = sum(part_l) / B; every non-null target of the bias gradient = sum(part_g).  256 threads: thread t
+// sums parts t, t + 256, ... in order, then a fixed tree (one thread over 1,024 parts was a chain of
+// dependent L2 loads: ~0.1 ms)
+__global__ __launch_bounds__(256) void bce_finish_kernel(int nparts, int B, const double* __restrict__ part,
+                                                         float* __restrict__ loss, float* __restrict__ gbias,
+                                                         float* __restrict__ gbias2) {
+  __shared__ double sl[256], sg[256];
   double l = 0.0, g = 0.0;
-  for (int i = 0; i < nparts; ++i) {
+  for (int i = threadIdx.x; i < nparts; i += 256) {
     l += part[i];
     g += part[kMaxParts + i];
   }
-  if (loss) *loss = (float)(l / B);
-  if (gbias) *gbias = (float)g;
-  if (gbias2) *gbias2 = (float)g;
+  sl[threadIdx.x] = l;
+  sg[threadIdx.x] = g;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sl[threadIdx.x] += sl[threadIdx.x + o];
+      sg[threadIdx.x] += sg[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  if (loss) *loss = (float)(sl[0] / B);
+  if (gbias) *gbias = (float)sg[0];
+  if (gbias2) *gbias2 = (float)sg[0];
+}
+
+// The training head in one pass over the last hidden activations h (knob "train_head_fused", default
+// on): per row (one wave), the logit and p exactly as tower_head_kernel (same products, same order:
+// bitwise the same p), BigDL BCECriterion + Sigmoid backward as bce_kernel (dz = dL/dlogit), the output
+// layer's dPre = dz * wo masked by ReLU (h > 0) as head_back4_kernel, and per-block partial sums of the
+// loss, of dz (bias gradients) and of dz * h[:, n] (dW_out, reduced over blocks by slice_reduce_kernel).
+// One read of h instead of three (tower_head, head_back, colsum) and no launches in between:
+// DeepFM B = 65,536: tower_head + bce + head_back 0.036 + 0.024 + 0.085 ms.
+constexpr int kHeadCols = 8;  // columns per lane: N <= 512
+__global__ __launch_bounds__(256) void head_train_kernel(int B, int N, const float* __restrict__ h, int ldh, OutArgs oa,
+                                                         const float* __restrict__ targets, float* __restrict__ dz,
+                                                         float* __restrict__ g, int ldg, int per_block,
+                                                         double* __restrict__ part, float* __restrict__ cpart) {
+  __shared__ double sl[4], sg[4];
+  __shared__ float cs[4][kHeadCols * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float eps = 1e-12f, norm = 1.0f / (float)B;
+  const int b0 = blockIdx.x * per_block, b1 = min(B, b0 + per_block);
+  float col[kHeadCols];
+#pragma unroll
+  for (int q = 0; q < kHeadCols; ++q) col[q] = 0.f;
+  double l = 0.0, gsum = 0.0;
+  // the BCE loss terms (two fp64 logs per row) run 64 rows at a time, one row per lane: row i of the
+  // wave parks its p / target in lane i & 63 (computed by one lane per row inside the row loop they cost
+  // ~1.5 k cycles of the whole wave's issue per row)
+  float px = 0.5f, pt = 0.f;
+  int npend = 0;
+  auto flush = [&]() {
+    if (lane < npend) l += -((double)pt * log((double)px + eps) + (1.0 - pt) * log(1.0 - (double)px + eps));
+    npend = 0;
+  };
+  float wv4[kHeadCols];
+#pragma unroll
+  for (int q = 0; q < kHeadCols; ++q) wv4[q] = lane + 64 * q < N ? oa.wo[lane + 64 * q] : 0.f;
+  // the wave's rows b0 + wv, b0 + wv + 4, ... in groups of kHeadRows whose h rows are loaded together
+  // (row by row, each row's load latency was exposed: 0.197 vs 0.143 ms for the three kernels)
+  constexpr int kHeadRows = 4;
+  for (int m0 = b0 + wv; m0 < b1; m0 += 4 * kHeadRows) {
+    float hv[kHeadRows][kHeadCols], pre_r[kHeadRows], pre2_r[kHeadRows], tg_r[kHeadRows], rs_r[kHeadRows];
+#pragma unroll
+    for (int r = 0; r < kHeadRows; ++r) {
+      const int m = m0 + 4 * r;
+      const bool ok = m < b1;
+#pragma unroll
+      for (int q = 0; q < kHeadCols; ++q) {
+        const int n = lane + 64 * q;
+        hv[r][q] = (ok && n < N) ? h[(int64_t)m * ldh + n] : 0.f;
+      }
+      // the row's scalars with its h (loaded after the logit's reduction, each cost a full latency)
+      pre_r[r] = (ok && oa.pre) ? oa.pre[m] : 0.f;
+      pre2_r[r] = (ok && oa.pre2) ? oa.pre2[m] : 0.f;
+      tg_r[r] = ok ? targets[m] : 0.f;
+      rs_r[r] = 0.f;  // xDeepFM: the CIN's per-row partials, in tower_head_kernel's order
+      if (ok && oa.rowsum)
+        for (int j = 0; j < oa.rowsum_k; ++j) rs_r[r] += oa.rowsum[(int64_t)m * oa.rowsum_k + j];
+    }
+#pragma unroll
+    for (int r = 0; r < kHeadRows; ++r) {
+      const int m = m0 + 4 * r;
+      if (m >= b1) break;
+      float p = 0.f;
+#pragma unroll
+      for (int q = 0; q < kHeadCols; ++q)
+        if (lane + 64 * q < N) p += hv[r][q] * wv4[q];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+      float y = p;
+      if (oa.has_bo) y = y + oa.bo;
+      if (oa.rowsum) y = rs_r[r] + y;
+      if (oa.pre2) y = pre2_r[r] + y;
+      float t = oa.pre ? pre_r[r] + y : y;
+      t = t + oa.beta;
+      const float x = 1.0f / (1.0f + expf(-t));
+      const float tg = tg_r[r] > 0.f ? 1.f : 0.f;  // DeepFM.scala:106
+      const float gp = -(tg - x) * norm / ((1.f - x + eps) * (x + eps));
+      const float gz = gp * (1.f - x) * x;
+      if (lane == 0) {
+        oa.out[m] = x;
+        dz[m] = gz;
+      }
+      if (lane == npend) {
+        px = x;
+        pt = tg;
+        gsum += gz;
+      }
+      if (++npend == 64) flush();
+#pragma unroll
+      for (int q = 0; q < kHeadCols; ++q) {
+        const int n = lane + 64 * q;
+        if (n < N) {
+          g[(int64_t)m * ldg + n] = hv[r][q] > 0.f ? gz * wv4[q] : 0.f;
+          col[q] += gz * hv[r][q];
+        }
+      }
+    }
+  }
+  flush();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    l += __shfl_xor(l, o);
+    gsum += __shfl_xor(gsum, o);
+  }
+  if (lane == 0) {
+    sl[wv] = l;
+    sg[wv] = gsum;
+  }
+#pragma unroll
+  for (int q = 0; q < kHeadCols; ++q) cs[wv][lane + 64 * q] = col[q];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = ((sl[0] + sl[1]) + sl[2]) + sl[3];
+    part[kMaxParts + blockIdx.x] = ((sg[0] + sg[1]) + sg[2]) + sg[3];
+  }
+  if (cpart)
+    for (int n = threadIdx.x; n < N; n += 256)
+      cpart[(int64_t)blockIdx.x * N + n] = ((cs[0][n] + cs[1][n]) + cs[2][n]) + cs[3][n];
 }
 
 // dPre of the last hidden layer: g[b][n] = dz[b] * wo[n] masked by ReLU (h > 0)
@@ -1407,6 +1538,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   const int F = m.F, k = m.k, D = F * k, Lc = m.cross_depth;
 
   // ---- forward with stored activations ----
+  bool head_fused = false;  // the head, the BCE and the output layer's backward ran as head_train_kernel
   if (t == RMX_MODEL_LR) {
     StageTimer tm(m, s, "first_order_sigmoid");
     if (in.y1) st = launch_sigmoid_out(s, B, in.y1, in.beta, T.p);
@@ -1493,19 +1625,56 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     oa.pre = pre;
     oa.beta = in.beta;
     oa.out = T.p;
-    StageTimer tm(m, s, "tower_head");
-    if ((st = launch_tower_head(s, B, eff_n(m.layers.back()), A, lda, oa))) return st;
+    const int Nh = eff_n(m.layers.back());
+    head_fused = tuning_get("train_head_fused", 1) != 0 && Nh <= kHeadCols * 64;
+    if (head_fused) {
+      // logit + p + BCE + the output layer's dPre / dW_out in one pass over h (head_train_kernel)
+      StageTimer tm(m, s, "head_bce");
+      const int nparts = std::min(kMaxParts, (B + 15) / 16);  // >= 16 rows per block; 64 at B = 65,536
+      const int per = (B + nparts - 1) / nparts;
+      const int np = (B + per - 1) / per;
+      float* cp = nullptr;
+      // dW_out partials: np slices reduced in two fixed-order passes when np is a multiple of 16 (np / 16
+      // slices of 16 * Nh, then 16 slices of Nh): a single pass over 1,024 slices ran on 7 blocks
+      const int G = (np % 16 == 0 && np >= 64) ? 16 : 1;
+      if (o.g_mats) {
+        if ((st = ensure_part(T, (int64_t)np * Nh + (int64_t)G * Nh))) return st;
+        cp = T.part2;
+      }
+      hipLaunchKernelGGL(head_train_kernel, dim3(np), dim3(256), 0, s, B, Nh, A, lda, oa, o.targets, T.dz, T.g[0],
+                         m.layers.back().Npad, per, T.part, cp);
+      RMX_HIP(hipGetLastError());
+      float* gbo = (m.has_bo && o.g_mats) ? o.g_mats + m.bo_off : nullptr;
+      hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(256), 0, s, np, B, T.part, o.loss, o.g_bias, gbo);
+      RMX_HIP(hipGetLastError());
+      if (cp && G > 1) {
+        float* cp2 = cp + (int64_t)np * Nh;
+        hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)G * Nh + 63) / 64)), dim3(256), 0, s, np / G,
+                           (int64_t)G * Nh, cp, cp2, 0);
+        RMX_HIP(hipGetLastError());
+        hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((Nh + 63) / 64)), dim3(256), 0, s, G, (int64_t)Nh, cp2,
+                           o.g_mats + m.wo_off, 0);
+        RMX_HIP(hipGetLastError());
+      } else if (cp) {
+        hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((Nh + 63) / 64)), dim3(256), 0, s, np, (int64_t)Nh, cp,
+                           o.g_mats + m.wo_off, 0);
+        RMX_HIP(hipGetLastError());
+      }
+    } else {
+      StageTimer tm(m, s, "tower_head");
+      if ((st = launch_tower_head(s, B, Nh, A, lda, oa))) return st;
+    }
   }
 
   // ---- loss, dL/dz, bias gradient ----
-  {
+  if (!head_fused) {
     StageTimer tm(m, s, "bce");
     const int nparts = std::min(kMaxParts, (B + kRedThreads - 1) / kRedThreads);
     const int per = (B + nparts - 1) / nparts;
     hipLaunchKernelGGL(bce_kernel, dim3(nparts), dim3(kRedThreads), 0, s, B, T.p, o.targets, T.dz, per, T.part);
     RMX_HIP(hipGetLastError());
     float* gbo = (m.has_bo && o.g_mats) ? o.g_mats + m.bo_off : nullptr;  // output Linear bias: same sum
-    hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(64), 0, s, nparts, B, T.part, o.loss, o.g_bias, gbo);
+    hipLaunchKernelGGL(bce_finish_kernel, dim3(1), dim3(256), 0, s, nparts, B, T.part, o.loss, o.g_bias, gbo);
     RMX_HIP(hipGetLastError());
   }
   if (o.g_w && t != RMX_MODEL_DNN && o.nnz > 0) {
@@ -1516,7 +1685,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
 
   // ---- tower backward ----
   const int nl = (int)m.layers.size();
-  {
+  if (!head_fused) {
     const DenseLayer& last = m.layers.back();
     const int N = eff_n(last);
     StageTimer tm(m, s, "head_back");
