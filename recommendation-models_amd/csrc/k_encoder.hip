@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
                                                           const T* __restrict__ wtab, int F,
                                                           float* __restrict__ y, float beta,
                                                           float* __restrict__ prob, int ld, int wld,
-                                                          float* __restrict__ xo) {
+                                                          float* __restrict__ xo, float* __restrict__ so) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int s = lane >> 2, c = lane & 3;
@@ -79,6 +79,9 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
     }
     if (MODE != 3 && c == 0) y1 += ld1(wtab + (int64_t)id * wld);
   }
+  // so (nullable, FM modes): the FM sums s_j = sum_f e_fj (field order from 0) as [B][16], read by the
+  // training backward's fused embedding gradient (k_gemm.hpp store_rows, emb_grad_kernel's s)
+  if (FM && so && valid) reinterpret_cast<float4*>(so + (int64_t)b * 16)[c] = s4;
   float y2 = 0.f;
   if (MODE == 1 || MODE == 3) {
     // d_j = s_j^2 - q_j for j = 4c..4c+3; lane c==0 sums j = 0..15 sequentially.
@@ -141,14 +144,14 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
 
 template <class T>
 static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids, const T* table, const T* wtab, int F,
-                             int k, float* y, float bt, float* prob, int ld, int wld, float* xo) {
+                             int k, float* y, float bt, float* prob, int ld, int wld, float* xo, float* so) {
   if (k == 16 || mode == 2) {  // LR (mode 2) never reads the table: any k takes the 4-lane path
     dim3 grid((M + 63) / 64);
     switch (mode) {
-      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo); break;
-      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo); break;
-      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, nullptr); break;
-      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo); break;
+      case 0: hipLaunchKernelGGL((encoder_k16_kernel<0, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo, so); break;
+      case 1: hipLaunchKernelGGL((encoder_k16_kernel<1, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo, so); break;
+      case 2: hipLaunchKernelGGL((encoder_k16_kernel<2, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, nullptr, nullptr); break;
+      default: hipLaunchKernelGGL((encoder_k16_kernel<3, T>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld, xo, so); break;
     }
   } else {
     dim3 grid((M + 255) / 256);
@@ -161,8 +164,12 @@ static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids,
 }
 
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table, const void* wtab, int dt,
-                   int F, int k, float* y, const float* beta, float* prob, int ld, int wld, float* xo) {
+                   int F, int k, float* y, const float* beta, float* prob, int ld, int wld, float* xo, float* so) {
   if (M <= 0) return RMX_OK;
+  if (so && (k != 16 || (mode != 1 && mode != 3))) {
+    set_error("encoder: the FM-sum output needs k = 16 and an FM mode");
+    return RMX_E_INVALID;
+  }
   if (xo && (k != 16 || mode == 2)) {
     set_error("encoder: the gathered-row output needs k = 16 and a table-reading mode");
     return RMX_E_INVALID;
@@ -171,9 +178,9 @@ int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const voi
   ld = ld > 0 ? ld : (k == 16 || mode == 2 ? 16 : k);
   wld = wld > 0 ? wld : 1;
   if (dt == kBF16)
-    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob, ld, wld, xo);
+    encoder_launch_t(s, mode, M, ids, (const bf16_t*)table, (const bf16_t*)wtab, F, k, y, bt, prob, ld, wld, xo, so);
   else
-    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob, ld, wld, xo);
+    encoder_launch_t(s, mode, M, ids, (const float*)table, (const float*)wtab, F, k, y, bt, prob, ld, wld, xo, so);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -142,6 +142,13 @@ struct GemmArgs {
   int raw;
   const float* mask;
   int ldmask;
+  // DeepFM training, dX of tower layer 1 written straight as the embedding gradient (train.hip): the
+  // stored value becomes dx + dz[m] * (s[m][j] - x[m][n]) / 16 (emb_grad_kernel's FM term, same
+  // arithmetic; j = n mod 16), with x [M][eg_ldx] the gathered rows and s [M][16] the FM sums
+  const float* eg_x;
+  const float* eg_s;
+  const float* eg_dz;
+  int eg_ldx;
 };
 
 template <int V>
@@ -1183,6 +1190,16 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
             const f32x4 h = *reinterpret_cast<const f32x4*>(p.mask + (int64_t)m * p.ldmask + n0 + (bt0 + j0) * 16 + c4 * 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = h[e] > 0.f ? v[e] : 0.f;
+          }
+          if constexpr (!BF) {
+            if (p.eg_x) {
+              const int n = n0 + (bt0 + j0) * 16 + c4 * 4;
+              const f32x4 xv = *reinterpret_cast<const f32x4*>(p.eg_x + (int64_t)m * p.eg_ldx + n);
+              const f32x4 sv = *reinterpret_cast<const f32x4*>(p.eg_s + (int64_t)m * 16 + (n & 15));
+              const float gz = p.eg_dz[m];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += gz * (sv[e] - xv[e]) / 16.0f;
+            }
           }
           if constexpr (BF)
             *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16_t*>(dst) + o) = __builtin_convertvector(v, bf16x4);

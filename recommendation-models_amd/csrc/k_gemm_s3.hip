@@ -116,7 +116,7 @@ bool dx_s3_usable(const DenseLayer& L, int ldx) {
 }
 
 int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, int lda, float* dx, int ldx,
-                 const float* mask, int ldmask) {
+                 const float* mask, int ldmask, const EmbGradArgs* eg) {
   if (!dx_s3_usable(L, ldx) || (mask && L.NTpad > ldmask)) {
     set_error("dx: no split-GEMM W^T for this layer");
     return RMX_E_INVALID;
@@ -136,6 +136,16 @@ int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, i
   p.raw = 1;
   p.mask = mask;
   p.ldmask = ldmask;
+  if (eg) {
+    if (ldx != L.K || L.K % 16 || ldx % 4 || eg->ldx % 4) {
+      set_error("dx: the fused embedding gradient needs [B][F * 16] rows");
+      return RMX_E_INVALID;
+    }
+    p.eg_x = eg->x;
+    p.eg_s = eg->s;
+    p.eg_dz = eg->dz;
+    p.eg_ldx = eg->ldx;
+  }
   return launch_tower_s3(s, p, kDenseA, Epi::kReluStore);
 }
 

@@ -133,10 +133,11 @@ int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
 // ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1); xo (k = 16,
-// modes 0 / 1 / 3): also write the gathered rows as fp32 x [M][F * 16] (the training forward's tower input)
+// modes 0 / 1 / 3): also write the gathered rows as fp32 x [M][F * 16] (the training forward's tower input);
+// so (k = 16, modes 1 / 3): also write the FM sums s_j = sum_f e_fj as [M][16]
 int launch_encoder(hipStream_t s, int mode, int M, const int32_t* ids, const void* table,
                    const void* wtab, int dt, int F, int k, float* y, const float* beta, float* prob, int ld = 0,
-                   int wld = 0, float* xo = nullptr);
+                   int wld = 0, float* xo = nullptr, float* so = nullptr);
 int launch_first_order_csr(hipStream_t s, int B, const int64_t* row_ptr, const float* w, float* y);
 int launch_sigmoid_out(hipStream_t s, int B, const float* y, float beta, float* out);
 int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int64_t V, int32_t* ids);
@@ -152,8 +153,15 @@ int launch_pack_linear(hipStream_t s, const float* mats_dev, DenseLayer& L);
 int launch_pack_linear_t(hipStream_t s, const float* mats_dev, DenseLayer& L);
 // dX[B][ldx] = dPre[B][lda] W (+ mask: dX *= (mask > 0)), on the split GEMM; RMX_E_INVALID when the
 // layer has no W^T planes (the caller then uses its library GEMM)
+// DeepFM: write dX of tower layer 1 as the embedding gradient (GemmArgs::eg_*)
+struct EmbGradArgs {
+  const float* x;   // [B][ldx] gathered rows
+  const float* s;   // [B][16] FM sums
+  const float* dz;  // [B] dL/dlogit
+  int ldx;
+};
 int launch_dx_s3(hipStream_t s, const DenseLayer& L, int B, const float* dpre, int lda, float* dx, int ldx,
-                 const float* mask, int ldmask);
+                 const float* mask, int ldmask, const EmbGradArgs* eg = nullptr);
 bool dx_s3_usable(const DenseLayer& L, int ldx);
 // fp32 packed [n16][Npad][16] -> the three bf16 planes of the split GEMM (k_gemm_s3.hip)
 int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3);

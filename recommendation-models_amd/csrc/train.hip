@@ -55,6 +55,8 @@ struct TrainState {
   int rc = 0;                   // rows per chunk (a multiple of k)
   float* part2 = nullptr;       // [cap_part] slice partials of wgrad / colsum
   int64_t cap_part = 0;
+  float* fms = nullptr;         // DeepFM, k = 16: [B][16] FM sums s_j of the forward (fused embedding gradient)
+  bool fms_valid = false;       // this step's forward wrote fms
 };
 
 namespace {
@@ -1404,6 +1406,7 @@ int ensure_train(rmx_model& m, int B) {
   T.h.clear();
   tfree(T.g[0]);
   tfree(T.g[1]);
+  tfree(T.fms);
   tfree(T.p);
   tfree(T.dz);
   tfree(T.ones);
@@ -1441,6 +1444,7 @@ int ensure_train(rmx_model& m, int B) {
     if ((st = talloc(&T.g[1], (size_t)B * maxld))) return st;
   }
   if ((st = talloc(&T.p, B)) || (st = talloc(&T.dz, B)) || (st = talloc(&T.ones, B))) return st;
+  if (m.type == RMX_MODEL_DEEPFM && m.k == 16 && (st = talloc(&T.fms, (size_t)B * 16))) return st;
   if ((st = talloc(&T.tmp, std::max(maxld, 2 * m.cross_depth + 1)))) return st;
   if (m.type == RMX_MODEL_XDEEPFM) {
     const int64_t R = (int64_t)B * m.k;
@@ -1490,6 +1494,7 @@ void train_release(rmx_model& m) {
   for (auto& p : T.h) tfree(p);
   tfree(T.g[0]);
   tfree(T.g[1]);
+  tfree(T.fms);
   tfree(T.p);
   tfree(T.dz);
   tfree(T.ones);
@@ -1558,8 +1563,10 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     float* xo = fuse_x ? T.x : nullptr;
     if (t == RMX_MODEL_DEEPFM) {
       StageTimer tm(m, s, fuse_x ? "encoder_fm_x" : "encoder_fm");
+      // the FM sums for the fused embedding gradient (knob "train_emb_fused", default on)
+      T.fms_valid = T.fms && k == 16 && tuning_get("train_emb_fused", 1) != 0;
       if ((st = launch_encoder(s, in.y1 ? 3 : 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr,
-                               nullptr, 0, 0, xo)))
+                               nullptr, 0, 0, xo, T.fms_valid ? T.fms : nullptr)))
         return st;
       pre = m.y12;
     } else if (t != RMX_MODEL_DNN) {
@@ -1700,6 +1707,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     RMX_HIP(hipGetLastError());
   }
   int cur = 0;
+  bool emb_fused = false;  // layer 1's dX epilogue wrote the embedding gradient (DeepFM)
   static const char* bnames[] = {"tower_back1", "tower_back2", "tower_back3", "tower_back4+"};
   for (int l = nl - 1; l >= 0; --l) {
     const DenseLayer& L = m.layers[l];
@@ -1734,7 +1742,15 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       bias_done = bias_done || bd;
       if (!need_dx) continue;
       if (nb == 1 && m.precision == kF32 && dx_s3_usable(L, ldin) && (!mask || L.NTpad <= ldmask)) {
-        if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, dxin + bk.c0, ldin, mask, ldmask))) return st;
+        // DeepFM layer 1: dX + the FM term written straight as the embedding gradient (emb_grad_kernel's
+        // arithmetic in the dX epilogue: dX is never stored and reread)
+        emb_fused = l == 0 && t == RMX_MODEL_DEEPFM && T.fms_valid && o.g_emb && ldin == D && L.K == D;
+        if (emb_fused) {
+          const EmbGradArgs eg{T.x, T.fms, T.dz, T.ldx};
+          if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, o.g_emb, D, nullptr, 0, &eg))) return st;
+        } else if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, dxin + bk.c0, ldin, mask, ldmask))) {
+          return st;
+        }
         masked = mask != nullptr;
       } else {
         if ((st = launch_gemm_f32(s, false, false, B, bk.K, N, dpre, L.Npad, m.mats_dev + bk.w, bk.K, dxin + bk.c0,
@@ -1856,7 +1872,7 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
   }
 
   // ---- embedding gradients ----
-  if (o.g_emb) {
+  if (o.g_emb && !emb_fused) {
     StageTimer tm(m, s, "emb_grad");
     if (t == RMX_MODEL_PNN)
       hipLaunchKernelGGL(pnn_emb_grad_kernel, dim3(nblk((int64_t)B * D)), dim3(256), 0, s, B, F, k, T.x, T.ldx, dX,

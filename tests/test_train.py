@@ -336,6 +336,48 @@ def test_backward_fused_x_bitwise(kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fc,B", [((32, 16), 777), ((400, 400, 400), 4099)])
+def test_backward_fused_head_and_emb_grad(fc, B):
+    """train_emb_fused: DeepFM's layer-1 dX epilogue writes the embedding gradient itself (dX + the FM
+    term with emb_grad_kernel's arithmetic, the forward's FM sums) -- bitwise the two-kernel result.
+    train_head_fused: logit + BCE + the output layer's backward in one kernel -- p, dz and everything fed
+    by them bitwise (g_w, g_emb); the batch sums (loss, bias gradient, dW_out) only change summation
+    order: 1e-6 relative."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K = 20_000, 39, 16
+    m = _gpu_model(rmx, "deepfm", V, F, K, fc)
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 33, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(3).random(B) > 0.7).astype(np.float32))
+    res = {}
+    try:
+        for eg, hd in ((0, 0), (1, 0), (1, 1)):
+            rmx.set_tuning("train_emb_fused", eg)
+            rmx.set_tuning("train_head_fused", hd)
+            out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, len(mats), 1)]
+            m.backward_ids(t, B, ids, targets, *out)
+            ctx.sync()
+            res[(eg, hd)] = [o.numpy().copy() for o in out]
+    finally:
+        rmx.set_tuning("train_emb_fused", None)
+        rmx.set_tuning("train_head_fused", None)
+    for a, b in zip(res[(0, 0)], res[(1, 0)]):
+        assert np.array_equal(a, b)
+    loss0, gw0, ge0, gm0, gb0 = res[(1, 0)]
+    loss1, gw1, ge1, gm1, gb1 = res[(1, 1)]
+    assert np.array_equal(gw0, gw1) and np.array_equal(ge0, ge1)
+    for a, b in ((loss0, loss1), (gb0, gb1), (gm0, gm1)):
+        assert np.allclose(a, b, rtol=1e-6, atol=1e-9 * max(1.0, float(np.abs(a).max())))
+
+
+@pytest.mark.gpu
 def test_backward_wgrad_sq_tile_cin():
     """The CIN's generated-operand dW on the 208 x 208 tile (wgrad_sq_gz 1) against the 208 x 128 one
     (the default): rows = B k = 65,584 (a ragged chunk), within 2e-5 relative per mats block."""

@@ -70,7 +70,7 @@ def stage_of(kernel, workload=""):
                     ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
                     ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
                     ("owner_gather", "shard_exchange"), ("own_rows_kernel", "shard_exchange"),
-                    ("own_gather", "shard_exchange")):
+                    ("own_gather", "shard_exchange"), ("tower_tail_bf16_kernel", "tower_tail")):
         if kernel.startswith(pat):
             return st
     return None
