@@ -21,7 +21,7 @@
 //     waves 0-1 three tiles, 2-11 two, i.e. 7 / 7 / 6 / 6 tiles per SIMD (waves w and w + 4 share
 //     a SIMD);
 //   - the weights (W2, W3: [13 steps][416][32] bf16, 338 KiB each, L2-resident) go straight from
-//     global memory into registers, two K steps ahead: each fragment is 1 KiB contiguous per wave
+//     global memory into registers, one K step ahead: each fragment is 1 KiB contiguous per wave
 //     and exactly one wave of the block reads it, so staging it through LDS would buy no reuse;
 //   - the MFMA runs with the operands swapped (D = W h^T: v_mfma_f32_16x16x32_bf16 with the weight
 //     fragment as A), so a lane ends up holding 4 consecutive outputs n of one sample, which is
@@ -50,7 +50,9 @@ constexpr int kTH1 = 7;                    // K steps in the image's first half
 constexpr int kTInsA = kTH1 * kTBM * 64 / 1024;            // 1-KiB DMA instructions, first half (56)
 constexpr int kTInsB = (kTKS - kTH1) * kTBM * 64 / 1024;   // second half (48)
 constexpr int kTPerB = kTInsB / kTLW;                      // 16 per loader (the counted wait below)
-constexpr int kTPF = 2;                    // weight fragments loaded this many K steps ahead
+// weight fragments loaded this many K steps ahead: 1 (2 spilled 14 registers at the 128-VGPR budget of
+// 16 waves: tail 0.0463 vs 0.0443 ms, 11.3 vs 5.0 MB of scratch writes per launch)
+constexpr int kTPF = 1;
 constexpr int kTPrm = 3 * kTN;              // b2, b3, wo staged in LDS (fp32)
 constexpr size_t kTLds = kTImg + sizeof(float) * (kTCW * kTBM + kTPrm);
 
