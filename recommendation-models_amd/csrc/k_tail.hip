@@ -45,18 +45,44 @@ constexpr int kTKS = 13;                   // 32-wide K steps: Kpad = 416
 constexpr int kTCW = 13;                   // compute waves: w < 12 own tiles w, w + 12; wave 12 tile 24
 constexpr int kTLW = 3;                    // loader waves (13, 14, 15)
 constexpr int kTThreads = (kTCW + kTLW) * 64;
-constexpr int kTImg = kTKS * kTBM * 64;    // bytes of the h tile image [step][row][64 B] (106,496)
-constexpr int kTH1 = 7;                    // K steps in the image's first half
-constexpr int kTInsA = kTH1 * kTBM * 64 / 1024;            // 1-KiB DMA instructions, first half (56)
-constexpr int kTInsB = (kTKS - kTH1) * kTBM * 64 / 1024;   // second half (48)
-constexpr int kTPerB = kTInsB / kTLW;                      // 16 per loader (the counted wait below)
+constexpr int kTStep = kTBM * 64;         // bytes of one K step of a row block's h tile (8 KiB)
+constexpr int kTSlots = 18;                // LDS step slots: 13 of the current row block + 5 spare
+constexpr int kTImg = kTSlots * kTStep;    // 147,456 B
+constexpr int kTE = 5;                     // "early" K steps of a row block (loaded a whole row block ahead)
+constexpr int kTL3 = kTKS - kTE;           // layer-3 steps read before the slots of the next block's late steps free up (8)
+constexpr int kTInsE = kTE * kTStep / 1024;            // 1-KiB DMA instructions: early steps (40)
+constexpr int kTInsL = (kTKS - kTE) * kTStep / 1024;   // late steps (64)
 // weight fragments loaded this many K steps ahead: 1 (2 spilled 14 registers at the 128-VGPR budget of
 // 16 waves: tail 0.0463 vs 0.0443 ms, 11.3 vs 5.0 MB of scratch writes per launch)
 constexpr int kTPF = 1;
 constexpr int kTPrm = 3 * kTN;              // b2, b3, wo staged in LDS (fp32)
 constexpr size_t kTLds = kTImg + sizeof(float) * (kTCW * kTBM + kTPrm);
 
-static_assert(kTInsB % kTLW == 0 && kTPerB == 16, "the loaders' counted vmcnt wait assumes 16 second-half DMAs each");
+static_assert(kTLds <= 160 * 1024, "LDS budget");
+static_assert(kTSlots == kTKS + kTE && kTL3 == kTKS - kTE, "the slot rotation below");
+
+// The 18 step slots rotate between row blocks: block t holds its K step c in slot S_t[c].  Block t + 1's
+// early steps go to the 5 slots block t does not use (loadable any time during block t), its late steps
+// (5 .. 12) to block t's steps 0 .. 7, free once layer 3 of block t has read them:
+//   S_{t+1}[0..4] = F_t,  S_{t+1}[5..12] = S_t[0..7],  F_{t+1} = S_t[8..12];  S_0 = 0..12, F_0 = 13..17.
+// S_t ++ F_t is then [0..17] rotated right by 5 t, i.e. S_t[c] = (c + base_t) mod 18 with base_0 = 0 and
+// base_{t+1} = base_t + 13 mod 18: one wave-uniform integer per block (a table of 18 slots per block was
+// kept in scratch by the compiler).  The early steps have a whole row block of lead and the late ones
+// layer 3's last 5 steps + layer 2's first 5 (the previous two-half image gave each half about half a
+// layer, and layer 2 waited at its mid barrier).
+struct SlotMap {
+  int base;
+};
+__device__ __forceinline__ SlotMap slots_first() { return SlotMap{0}; }
+__device__ __forceinline__ SlotMap slots_next(const SlotMap& m) {
+  const int b = m.base + kTKS;
+  return SlotMap{b >= kTSlots ? b - kTSlots : b};
+}
+// slot of step c (c < 13, wave-uniform)
+__device__ __forceinline__ int slot_at(const SlotMap& m, int c) {
+  const int s = c + m.base;
+  return s >= kTSlots ? s - kTSlots : s;
+}
 
 // Diagnostic builds only (timing probes, wrong results; never set in librmx.so): 1 = no weight loads
 // in the K loops (the prologue's fragments reused), 4 = no h1 prefetch after the first tile, 8 = no
@@ -122,15 +148,15 @@ __device__ __forceinline__ int hbase(int lane) {
   asm volatile("" : "+v"(hb));
   return hb;
 }
-__device__ __forceinline__ f32x4 ldh(const char* img, int hb, int c, int i) {
-  return *reinterpret_cast<const f32x4*>(img + hb + (c * kTBM + 16 * i) * 64);
+__device__ __forceinline__ f32x4 ldh(const char* img, int hb, int slot, int i) {
+  return *reinterpret_cast<const f32x4*>(img + slot * kTStep + hb + i * 1024);
 }
 
 // K steps [C0, C1) of a layer: acc[i][j] (row tile i, column tile j) += W_j h_i^T; wb holds the
 // fragments of steps C0 .. C0 + kTPF - 1 on entry (ring slot c % (kTPF + 1))
 template <int NTW, int C0, int C1>
-__device__ __forceinline__ void tail_steps(const bf16_t* __restrict__ W, int wo, const char* img, int lane, f32x4 (&acc)[kTMT][NTW],
-                                           f32x4 (&wb)[kTPF + 1][NTW]) {
+__device__ __forceinline__ void tail_steps(const bf16_t* __restrict__ W, int wo, const char* img, const SlotMap& sm,
+                                           int lane, f32x4 (&acc)[kTMT][NTW], f32x4 (&wb)[kTPF + 1][NTW]) {
   const int hb = hbase(lane);
 #pragma unroll
   for (int c = C0; c < C1; ++c) {
@@ -146,7 +172,7 @@ __device__ __forceinline__ void tail_steps(const bf16_t* __restrict__ W, int wo,
     for (int h = 0; h < 2; ++h) {
       f32x4 a[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = ldh(img, hb, c, 4 * h + i);
+      for (int i = 0; i < 4; ++i) a[i] = ldh(img, hb, slot_at(sm, c), 4 * h + i);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -176,9 +202,10 @@ __device__ __forceinline__ void tail_zero(f32x4 (&acc)[kTMT][NTW]) {
 
 // h2 columns n0 .. n0 + 3 of rows 16 i + r16 go to per-lane base pbase(n0) + 1 KiB * i (same key
 // argument as hbase) as one bf16x4 (8 B)
-__device__ __forceinline__ int pbase(int lane, int n0) {
-  const int r16 = lane & 15, c = n0 >> 5, slot = (n0 & 31) >> 3, half = (n0 >> 2) & 1;
-  int pb = ((c * kTBM + r16) * 4 + swz_slot(r16, slot)) * 16 + half * 8;
+// (the K step n0 >> 5 of a column tile is wave-uniform: its step slot goes into the base)
+__device__ __forceinline__ int pbase(int lane, int n0, const SlotMap& sm) {
+  const int r16 = lane & 15, c = n0 >> 5, q = (n0 & 31) >> 3, half = (n0 >> 2) & 1;
+  int pb = slot_at(sm, __builtin_amdgcn_readfirstlane(c)) * kTStep + (r16 * 4 + swz_slot(r16, q)) * 16 + half * 8;
   asm volatile("" : "+v"(pb));
   return pb;
 }
@@ -186,24 +213,24 @@ __device__ __forceinline__ void put_h2(char* img, int pb, int i, const f32x4& v)
   *reinterpret_cast<bf16x4*>(img + pb + i * 1024) = __builtin_convertvector(v, bf16x4);
 }
 
-// issuing wave idx of nidx: its share of one half of row block rb's h1 image (half 0: K steps 0 .. 6,
-// DMA instructions 0 .. 55; half 1: steps 7 .. 12, instructions 56 .. 103).  Lane L of instruction ins
-// fills image row R = 16 ins + L / 4 (R = step * 128 + row) at physical slot L & 3, i.e. loads
-// logical slot swz_slot(row, L & 3) (the swizzle is an involution).
-template <int HALF>
-__device__ __forceinline__ void tail_issue(const TailArgs& p, char* img, int rb, int idx, int nidx, int lane,
-                                           const float* zero16) {
-  constexpr int ins0 = HALF ? kTInsA : 0, nins = HALF ? kTInsB : kTInsA;
+// issuing wave idx of nidx: its share of K steps [C0, C1) of row block rb's h1 tile into the step slots
+// of map sm (8 1-KiB DMA instructions per step).  Lane L of instruction q of a step fills tile row
+// 16 q + L / 4 at physical 16-B slot L & 3, i.e. loads logical slot swz_slot(row, L & 3) (the swizzle is
+// an involution).
+template <int C0, int C1>
+__device__ __forceinline__ void tail_issue(const TailArgs& p, char* img, const SlotMap& sm, int rb, int idx, int nidx,
+                                           int lane, const float* zero16) {
+  constexpr int nins = (C1 - C0) * kTStep / 1024;
   const int m0 = rb * kTBM;
-  // a rolled loop: unrolled, the 104 per-lane sources / LDS bases were formed up front and spilled
+  // a rolled loop: unrolled, the per-lane sources / LDS bases were formed up front and spilled
 #pragma unroll 1
   for (int k = idx; k < nins; k += nidx) {
-    const int ins = ins0 + k;
-    const int R = ins * 16 + (lane >> 2);
-    const int c = R / kTBM, row = R - c * kTBM;
+    const int c = C0 + (k >> 3), q = k & 7;
+    const int row = q * 16 + (lane >> 2);
     const int m = m0 + row, kk = c * 32 + swz_slot(row, lane & 3) * 8;
     const void* src = (m < p.M && kk < p.K2) ? (const void*)(p.H + (int64_t)m * p.lda + kk) : (const void*)zero16;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + ins * 1024), 16, 0, 0);
+    char* dst = img + slot_at(sm, c) * kTStep + q * 1024;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   }
 }
 
@@ -219,33 +246,34 @@ __device__ void tail_compute(const TailArgs& p, char* img, float* red, const flo
   TS(0);
   f32x4 acc[kTMT][NTW];
   f32x4 wb[kTPF + 1][NTW];
-  // the first row block's first half: every wave of the block issues its DMAs (issue, not HBM, limits
-  // a start from an empty ring), then the weight prologue
-  if (nit > 0) tail_issue<0>(p, img, blockIdx.x, w < 12 ? w : kTCW - 1, 16, lane, zero16);
+  SlotMap sm = slots_first();
+  // the first row block's early steps: every wave of the block issues its DMAs (issue, not HBM, limits a
+  // start from an empty image), then the weight prologue
+  if (nit > 0) tail_issue<0, kTE>(p, img, sm, blockIdx.x, w < 12 ? w : kTCW - 1, 16, lane, zero16);
   tail_prologue<NTW>(p.W2, wlane(w, lane), wb);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   for (int it = 0; it < nit; ++it) {
-    bar();  // B0: the first half of this row block's h1 image has landed
+    bar();  // B0: this row block's early steps have landed
     TS(1 + 10 * it);
     {
       const int wo = wlane(w, lane);
       tail_zero<NTW>(acc);
-      tail_steps<NTW, 0, kTH1>(p.W2, wo, img, lane, acc, wb);
+      tail_steps<NTW, 0, kTE>(p.W2, wo, img, sm, lane, acc, wb);
       TS(2 + 10 * it);
-      bar();  // BM2: the second half has landed
+      bar();  // BM2: its late steps have landed
       TS(3 + 10 * it);
-      tail_steps<NTW, kTH1, kTKS>(p.W2, wo, img, lane, acc, wb);
+      tail_steps<NTW, kTE, kTKS>(p.W2, wo, img, sm, lane, acc, wb);
     }
     tail_prologue<NTW>(p.W3, wlane(w, lane), wb);  // in flight across the epilogue
     TS(4 + 10 * it);
-    bar_lds();                                      // B1: every wave has read the h1 image
+    bar_lds();                                      // B1: every wave has read the h1 tile
     TS(5 + 10 * it);
-    // h2 = bf16(ReLU(acc + b2)) into the same image; lane holds n = 16 t + 4 g .. + 3 of row 16 i + r16
+    // h2 = bf16(ReLU(acc + b2)) into the same slots; lane holds n = 16 t + 4 g .. + 3 of row 16 i + r16
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int n0 = 16 * (w + 12 * j) + 4 * g;
       const f32x4 bb = *reinterpret_cast<const f32x4*>(prm + n0);
-      const int pb = pbase(lane, n0);
+      const int pb = pbase(lane, n0, sm);
 #pragma unroll
       for (int i = 0; i < kTMT; ++i) {
         f32x4 v = acc[i][j] + bb;
@@ -255,7 +283,7 @@ __device__ void tail_compute(const TailArgs& p, char* img, float* red, const flo
       }
     }
     if (w == 2 * 12) {  // columns 400 .. 415 (not computed) read as zeros by the next layer
-      const int pb = pbase(lane, 16 * kTNT + 4 * g);
+      const int pb = pbase(lane, 16 * kTNT + 4 * g, sm);
 #pragma unroll
       for (int i = 0; i < kTMT; ++i) put_h2(img, pb, i, f32x4{0.f, 0.f, 0.f, 0.f});
     }
@@ -264,11 +292,11 @@ __device__ void tail_compute(const TailArgs& p, char* img, float* red, const flo
     {
       const int wo = wlane(w, lane);
       tail_zero<NTW>(acc);
-      tail_steps<NTW, 0, kTH1>(p.W3, wo, img, lane, acc, wb);
+      tail_steps<NTW, 0, kTL3>(p.W3, wo, img, sm, lane, acc, wb);
       TS(7 + 10 * it);
-      bar_lds();  // BM3: steps 0 .. 6 read by every wave: the loaders refill them with the next block
+      bar_lds();  // BM3: steps 0 .. 7 read by every wave: the loaders refill them with the next block
       TS(8 + 10 * it);
-      tail_steps<NTW, kTH1, kTKS>(p.W3, wo, img, lane, acc, wb);
+      tail_steps<NTW, kTL3, kTKS>(p.W3, wo, img, sm, lane, acc, wb);
     }
     if (it + 1 < nit) tail_prologue<NTW>(p.W2, wlane(w, lane), wb);
     // output dot: part[i] = sum over this lane's n of ReLU(acc + b3)[n] * wo[n], then over the 4 lane groups
@@ -296,8 +324,9 @@ __device__ void tail_compute(const TailArgs& p, char* img, float* red, const flo
       if (g == 0) red[(w < 12 ? w : kTCW - 1) * kTBM + 16 * i + r16] = part[i];
     }
     TS(9 + 10 * it);
-    bar_lds();  // B3: partial logits complete, the image is free
+    bar_lds();  // B3: partial logits complete
     TS(10 + 10 * it);
+    sm = slots_next(sm);
   }
 }
 
@@ -315,17 +344,18 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
   } else if (w == kTCW - 1) {
     tail_compute<1>(p, img, red, prm, 2 * 12, lane, nit, zero16);
   } else {
-    // loaders.  Row block it + 1's first half streams in behind layer 3's second half of block it, its
-    // second half behind layer 2's first half of block it + 1 (issued after B0, so B0 waits for no
-    // issue).  Loader 0 also runs the head of block it - 1 after B0 (its inputs loaded a block early;
-    // red[] is rewritten only after BM3).
+    // loaders.  Row block t + 1's early steps stream in behind row block t from BM2 on (a whole block of
+    // lead), its late steps behind layer 3's last 5 steps and layer 2's first 5 of block t + 1.  Loader 0
+    // also runs the head of block t - 1 after B0 (its inputs loaded a block early; red[] is rewritten
+    // only after the next BM3).
     const int lw = w - kTCW;
     const OutArgs& oa = p.oa;
 #if RMX_TAIL_DIAG & 16
     const int dslot = (blockIdx.x == 0 && lane == 0 && lw == 0) ? 3 : -1;
 #endif
     TS(0);
-    if (nit > 0) tail_issue<0>(p, img, blockIdx.x, kTCW + lw, 16, lane, zero16);
+    SlotMap sm = slots_first();
+    if (nit > 0) tail_issue<0, kTE>(p, img, sm, blockIdx.x, kTCW + lw, 16, lane, zero16);
     {  // the epilogue parameters into LDS (read after B1 / BM3 by the compute waves)
       float v[(kTPrm + kTLW * 64 - 1) / (kTLW * 64)];
 #pragma unroll
@@ -335,7 +365,7 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
         const float* src = a == 0 ? p.b2 : (a == 1 ? p.b3 : oa.wo);
         v[q] = (i < kTPrm && src) ? src[n] : 0.f;
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and this loader's first-half DMAs: B0 needs them)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and this loader's early-step DMAs: B0 needs them)
 #pragma unroll
       for (int q = 0; q < (int)(sizeof(v) / sizeof(float)); ++q) {
         const int i = lw * 64 + lane + q * kTLW * 64;
@@ -343,7 +373,7 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    if (nit > 0) tail_issue<1>(p, img, blockIdx.x, lw, kTLW, lane, zero16);
+    if (nit > 0) tail_issue<kTE, kTKS>(p, img, sm, blockIdx.x, lw, kTLW, lane, zero16);
     float hin[2] = {0.f, 0.f}, hpre[2] = {0.f, 0.f};    // the head's inputs of rows lane, lane + 64
     float pin[2] = {0.f, 0.f}, ppre[2] = {0.f, 0.f};    // ... of the previous row block
     auto head = [&](int rb, const float* in2, const float* pr) {
@@ -364,13 +394,18 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
     };
     for (int it = 0; it < nit; ++it) {
       const int rb = blockIdx.x + it * gridDim.x;
-      if (it > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // first half landed
+      const SlotMap nx = slots_next(sm);
+      // early steps of block it landed: only the late-step DMAs of this loader (issued after them) may be
+      // in flight -- 22 for loader 0, 21 for the others (64 instructions over 3 loaders)
+      if (it > 0) {
+        if (lw == 0)
+          asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+      }
       TS(1 + 10 * it);
       bar();  // B0
-      if (it > 0) {
-        if (!(RMX_TAIL_DIAG & 4)) tail_issue<1>(p, img, rb, lw, kTLW, lane, zero16);
-        if (lw == 0 && !(RMX_TAIL_DIAG & 8)) head(rb - (int)gridDim.x, pin, ppre);
-      }
+      if (it > 0 && lw == 0 && !(RMX_TAIL_DIAG & 8)) head(rb - (int)gridDim.x, pin, ppre);
       if (lw == 0) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -384,19 +419,23 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
           }
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // second half landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // late steps landed
       TS(2 + 10 * it);
-      bar();                                              // BM2
-      bar();                                              // B1
-      bar();                                              // B2
-      bar();                                              // BM3
-      if (it + 1 < nit && !(RMX_TAIL_DIAG & 4)) tail_issue<0>(p, img, rb + gridDim.x, lw, kTLW, lane, zero16);
+      bar();  // BM2
+      // the next block's early steps into the 5 slots this block does not use
+      if (it + 1 < nit && !(RMX_TAIL_DIAG & 4)) tail_issue<0, kTE>(p, img, nx, rb + gridDim.x, lw, kTLW, lane, zero16);
+      bar();  // B1
+      bar();  // B2
+      bar();  // BM3
+      // its late steps into this block's steps 0 .. 7, just read by layer 3
+      if (it + 1 < nit && !(RMX_TAIL_DIAG & 4)) tail_issue<kTE, kTKS>(p, img, nx, rb + gridDim.x, lw, kTLW, lane, zero16);
       bar();  // B3
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         pin[h] = hin[h];
         ppre[h] = hpre[h];
       }
+      sm = nx;
     }
     if (lw == 0 && nit > 0 && !(RMX_TAIL_DIAG & 8)) head(blockIdx.x + (nit - 1) * gridDim.x, pin, ppre);
   }
