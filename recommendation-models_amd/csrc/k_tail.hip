@@ -4,7 +4,7 @@
 // The last hidden Linear + ReLU and the output Linear + head of a bf16 tower
 // (model/encoder/HigherOrderEncoder.scala:34-59: Linear(400 -> 400) + ReLU, then the last
 // Linear(400 -> 400) + ReLU whose output feeds Linear(400 -> 1); the heads of DCN.scala /
-// PNN.scala: CAddTable + Sigmoid) as ONE launch over row blocks of 64 samples:
+// PNN.scala: CAddTable + Sigmoid) as ONE launch over row blocks of 128 samples:
 //   h2 = bf16(ReLU(h1 W2^T + b2))        kept in LDS, never written to HBM
 //   y  = sum_n ReLU(h2 W3^T + b3)[n] wo[n] (+ bo) ; p = sigmoid(pre + (pre2 + y) + beta)
 // Why: run as two launches, each layer reads 52 MB and the first writes 52 MB at B = 65,536, with
@@ -13,22 +13,21 @@
 // Here the only HBM traffic is h1 (read once) and p.
 //
 // Block = 16 waves on one CU (persistent: grid = min(row blocks, CUs)):
-//   - 4 loader waves (one per SIMD) DMA the NEXT row block's h1 tile (64 rows x 416 bf16 = 52 KiB,
-//     global_load_lds) into the idle half of a double-buffered LDS image while the 12 compute waves
-//     run the current one, so the tile's HBM latency hides behind two layers of MFMAs (a loader's
-//     vmcnt wait stalls only the loader: every wave has its own counter);
-//   - compute wave w owns column tiles w, w + 12, w + 24 (< 26) of both layers for all 64 rows:
-//     waves 0-1 three tiles, 2-11 two, i.e. 7 / 7 / 6 / 6 tiles per SIMD (waves w and w + 4 share
-//     a SIMD);
+//   - 3 loader waves DMA the NEXT row block's h1 tile (128 rows x 416 bf16 = 104 KiB, global_load_lds)
+//     into rotating LDS step slots while the 13 compute waves run the current one (slot map and
+//     schedule below), so the tile's HBM latency hides behind the MFMAs (a loader's vmcnt wait stalls
+//     only the loader: every wave has its own counter); loader 0 also runs each block's head;
+//   - compute wave w < 12 owns column tiles w, w + 12 of both layers for all 128 rows, wave 12 tile 24
+//     (the 25 tiles of N = 400): 7 / 6 / 6 / 6 tiles per SIMD (waves w and w + 4 share a SIMD);
 //   - the weights (W2, W3: [13 steps][416][32] bf16, 338 KiB each, L2-resident) go straight from
 //     global memory into registers, one K step ahead: each fragment is 1 KiB contiguous per wave
 //     and exactly one wave of the block reads it, so staging it through LDS would buy no reuse;
 //   - the MFMA runs with the operands swapped (D = W h^T: v_mfma_f32_16x16x32_bf16 with the weight
 //     fragment as A), so a lane ends up holding 4 consecutive outputs n of one sample, which is
-//     what the epilogue needs: h2 goes back into the tile's own LDS image as one 8-B bf16x4 write
+//     what the epilogue needs: h2 goes back into the block's own LDS slots as one 8-B bf16x4 write
 //     per (tile, row tile), and the output dot sums along the lane first.
-// Per K step a compute wave reads 4 A fragments (4 KiB) from LDS and issues 4 x NTW MFMAs; per SIMD
-// that is 28 MFMAs x 16 cycles against 16 KiB of LDS reads (128 cycles at 128 B/clk): MFMA-bound.
+// Per K step a compute wave reads 8 h fragments (8 KiB) from LDS and issues 8 x NTW MFMAs: each weight
+// fragment feeds 8 MFMAs (at 64 rows per block the weight stream was half the kernel's time).
 // The sums are the unfused kernels' up to the order of the final logit reduction: h2 is the same
 // bf16 (RNE) of the same fp32 accumulations (K steps in order), so parity is held to the same bar
 // against the oracle's bf16 emulation (tests/test_bf16.py).
