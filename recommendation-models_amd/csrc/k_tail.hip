@@ -112,6 +112,11 @@ struct TailArgs {
   const bf16_t* W3;
   const float* b3;
   OutArgs oa;        // wo [416], bo, pre, pre2, rowsum, beta, out
+  // first order computed here instead of read from oa.pre (PNN: its own kernel otherwise): y1[m] =
+  // sum_f w[ids[m * F + f] * wld] in field order (encoder_k16_kernel<0>'s sum), null = off
+  const int32_t* fo_ids;
+  const bf16_t* fo_w;
+  int fo_F, fo_wld;
 };
 
 __device__ __forceinline__ void bar_lds() {
@@ -210,6 +215,37 @@ __device__ __forceinline__ int pbase(int lane, int n0, const SlotMap& sm) {
 }
 __device__ __forceinline__ void put_h2(char* img, int pb, int i, const f32x4& v) {
   *reinterpret_cast<bf16x4*>(img + pb + i * 1024) = __builtin_convertvector(v, bf16x4);
+}
+
+// the fused first order of row m: all F ids, then all F weights in flight (two latency rounds), summed in
+// field order from 0 (encoder_k16_kernel<0>'s y1, bitwise).  FF compile-time (no per-field conditions:
+// with a runtime F they became 40 scalar masks and spilled); fo_sum_any: 8 fields at a time
+template <int FF>
+__device__ __forceinline__ float fo_sum(const TailArgs& p, int m) {
+  int idv[FF];
+#pragma unroll
+  for (int f = 0; f < FF; ++f) idv[f] = p.fo_ids[(int64_t)m * FF + f];
+  float wv[FF];
+#pragma unroll
+  for (int f = 0; f < FF; ++f) wv[f] = (float)p.fo_w[(int64_t)idv[f] * p.fo_wld];
+  float y1 = 0.f;
+#pragma unroll
+  for (int f = 0; f < FF; ++f) y1 += wv[f];
+  return y1;
+}
+__device__ __forceinline__ float fo_sum_any(const TailArgs& p, int m) {
+  float y1 = 0.f;
+#pragma unroll 1
+  for (int f0 = 0; f0 < p.fo_F; f0 += 8) {
+    float wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      wv[u] = f0 + u < p.fo_F ? (float)p.fo_w[(int64_t)p.fo_ids[(int64_t)m * p.fo_F + f0 + u] * p.fo_wld] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (f0 + u < p.fo_F) y1 += wv[u];
+  }
+  return y1;
 }
 
 // issuing wave idx of nidx: its share of K steps [C0, C1) of row block rb's h1 tile into the step slots
@@ -373,22 +409,23 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (nit > 0) tail_issue<kTE, kTKS>(p, img, sm, blockIdx.x, lw, kTLW, lane, zero16);
-    float hin[2] = {0.f, 0.f}, hpre[2] = {0.f, 0.f};    // the head's inputs of rows lane, lane + 64
-    float pin[2] = {0.f, 0.f}, ppre[2] = {0.f, 0.f};    // ... of the previous row block
-    auto head = [&](int rb, const float* in2, const float* pr) {
+    // the head: loaders 0 and 1, one row each per lane (row = 64 lw + lane); its inputs are loaded a block
+    // early (hin: pre2 or the CIN partials, hpre: pre or the fused first order)
+    const bool hl = lw < 2;
+    const int hrow = lw * 64 + lane;
+    const bool has_pre = oa.pre || p.fo_ids;
+    float hin = 0.f, hpre = 0.f, pin = 0.f, ppre = 0.f;
+    auto head = [&](int rb, float in2, float pr) {
+      const int m = rb * kTBM + hrow;
+      if (m < p.M) {
+        float y = red[hrow];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int row = lane + 64 * h, m = rb * kTBM + row;
-        if (m < p.M) {
-          float y = red[row];
-#pragma unroll
-          for (int q = 1; q < kTCW; ++q) y += red[q * kTBM + row];
-          if (oa.has_bo) y = y + oa.bo;
-          if (oa.rowsum || oa.pre2) y = in2[h] + y;
-          float t = oa.pre ? pr[h] + y : y;
-          t = t + oa.beta;
-          oa.out[m] = 1.0f / (1.0f + expf(-t));
-        }
+        for (int q = 1; q < kTCW; ++q) y += red[q * kTBM + hrow];
+        if (oa.has_bo) y = y + oa.bo;
+        if (oa.rowsum || oa.pre2) y = in2 + y;
+        float t = has_pre ? pr + y : y;
+        t = t + oa.beta;
+        oa.out[m] = 1.0f / (1.0f + expf(-t));
       }
     };
     for (int it = 0; it < nit; ++it) {
@@ -404,17 +441,18 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
       }
       TS(1 + 10 * it);
       bar();  // B0
-      if (it > 0 && lw == 0 && !(RMX_TAIL_DIAG & 8)) head(rb - (int)gridDim.x, pin, ppre);
-      if (lw == 0) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int m = rb * kTBM + lane + 64 * h;
-          if (m < p.M) {
-            float rs = 0.f;
-            if (oa.rowsum)
-              for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
-            hin[h] = oa.rowsum ? rs : (oa.pre2 ? oa.pre2[m] : 0.f);  // (rowsum and pre2 never together)
-            hpre[h] = oa.pre ? oa.pre[m] : 0.f;
+      if (it > 0 && hl && !(RMX_TAIL_DIAG & 8)) head(rb - (int)gridDim.x, pin, ppre);
+      if (hl) {
+        const int m = rb * kTBM + hrow;
+        if (m < p.M) {
+          float rs = 0.f;
+          if (oa.rowsum)
+            for (int jj = 0; jj < oa.rowsum_k; ++jj) rs += oa.rowsum[(int64_t)m * oa.rowsum_k + jj];
+          hin = oa.rowsum ? rs : (oa.pre2 ? oa.pre2[m] : 0.f);  // (rowsum and pre2 never together)
+          if (p.fo_ids) {
+            hpre = p.fo_F == 39 ? fo_sum<39>(p, m) : fo_sum_any(p, m);  // (F = 39: the Criteo shape)
+          } else {
+            hpre = oa.pre ? oa.pre[m] : 0.f;
           }
         }
       }
@@ -429,14 +467,11 @@ __global__ __launch_bounds__(kTThreads, 1) void tower_tail_bf16_kernel(TailArgs 
       // its late steps into this block's steps 0 .. 7, just read by layer 3
       if (it + 1 < nit && !(RMX_TAIL_DIAG & 4)) tail_issue<kTE, kTKS>(p, img, nx, rb + gridDim.x, lw, kTLW, lane, zero16);
       bar();  // B3
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        pin[h] = hin[h];
-        ppre[h] = hpre[h];
-      }
+      pin = hin;
+      ppre = hpre;
       sm = nx;
     }
-    if (lw == 0 && nit > 0 && !(RMX_TAIL_DIAG & 8)) head(blockIdx.x + (nit - 1) * gridDim.x, pin, ppre);
+    if (hl && nit > 0 && !(RMX_TAIL_DIAG & 8)) head(blockIdx.x + (nit - 1) * gridDim.x, pin, ppre);
   }
 }
 
@@ -455,7 +490,7 @@ bool tower_tail_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int ld
 }
 
 int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const bf16_t* H, int lda,
-                           const OutArgs& oa) {
+                           const OutArgs& oa, const TailFirstOrder* fo) {
   if (!tower_tail_usable(L2, L3, M, lda) || !oa.wo || !oa.out || (oa.rowsum && oa.pre2)) {
     set_error("tower tail: needs two bf16 layers of N <= 400 (Npad = Kpad = 416) and an output head");
     return RMX_E_INVALID;
@@ -476,6 +511,16 @@ int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer
   p.W3 = L3.W16;
   p.b3 = L3.b;
   p.oa = oa;
+  if (fo) {
+    if (fo->F > 40 || fo->F <= 0 || !fo->ids || !fo->w || oa.pre) {
+      set_error("tower tail: the fused first order needs 1 <= F <= 40 and no precomputed pre");
+      return RMX_E_INVALID;
+    }
+    p.fo_ids = fo->ids;
+    p.fo_w = fo->w;
+    p.fo_F = fo->F;
+    p.fo_wld = fo->wld > 0 ? fo->wld : 1;
+  }
   const int grid = std::min(p.nblk, std::max(ncu, 1));
   hipLaunchKernelGGL(tower_tail_bf16_kernel, dim3(grid), dim3(kTThreads), kTLds, s, p);
   RMX_HIP(hipGetLastError());

@@ -728,6 +728,12 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // fm_y1: 0 = first-order kernel, 1 = layer 1's epilogue gathers, 2 (default) = summed from the
   // ring's weight DMAs when layer 1 runs a w-ring tile (free), else the first-order kernel
   const int fm_y1 = tuning_get("fm_y1", 2);
+  // PNN bf16: its first order (a kernel of its own otherwise: nothing else gathers the weights) summed by
+  // the tower tail's head (knob "tail_fo", default on)
+  const size_t nl = m.layers.size();
+  const bool tail_fo = m.type == RMX_MODEL_PNN && m.precision == kBF16 && in.dtype == kBF16 && in.ids && !in.y1 &&
+                       F <= 40 && nl >= 3 && tuning_get("tail_fo", 1) != 0 &&
+                       tower_tail_usable(m.layers[nl - 2], m.layers[nl - 1], B, m.layers[nl - 3].Npad);
   const bool fm_add = fm_fused && deepfm &&
                       (fm_y1 == 0 || (fm_y1 == 2 && !tower_wring(m.layers[0], B, &ga)));
   if (fm_add) {
@@ -744,11 +750,11 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
                         in.wld);
     pre = m.y12;
   } else if (m.type != RMX_MODEL_DNN) {
-    if (!in.y1) {
+    if (!in.y1 && !tail_fo) {
       StageTimer t(m, s, "first_order");
       st = launch_encoder(s, 0, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr, in.ld, in.wld);
     }
-    pre = m.y12;  // (the L-A irregular path already wrote y1 here)
+    pre = tail_fo ? nullptr : m.y12;  // (the L-A irregular path already wrote y1 here)
   }
   if (st) return st;
 
@@ -811,7 +817,9 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     if (i >= 1 && i + 2 == m.layers.size() && m.precision == kBF16 &&
         tower_tail_usable(L, m.layers[i + 1], B, lda)) {
       StageTimer t(m, s, "tower_tail");
-      return launch_tower_tail_bf16(s, L, m.layers[i + 1], B, reinterpret_cast<const bf16_t*>(A), lda, oa);
+      const TailFirstOrder fo{in.ids, reinterpret_cast<const bf16_t*>(in.wtab), F, in.wld};
+      return launch_tower_tail_bf16(s, L, m.layers[i + 1], B, reinterpret_cast<const bf16_t*>(A), lda, oa,
+                                    tail_fo ? &fo : nullptr);
     }
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);

@@ -128,8 +128,13 @@ bool tower_wring(const DenseLayer& L, int M, const AGatherArgs* ga);
 // bf16 tower tail (k_tail.hip): ReLU(H L2) -> ReLU(. L3) . wo -> head, one persistent launch, when
 // both layers are bf16 with Npad = Kpad = 416; H [M][lda] bf16
 bool tower_tail_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda);
+struct TailFirstOrder {  // the first order summed by the tail itself (bf16 weights)
+  const int32_t* ids;    // [M][F]
+  const bf16_t* w;       // weight of id at w[id * wld]
+  int F, wld;
+};
 int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const bf16_t* H, int lda,
-                           const OutArgs& oa);
+                           const OutArgs& oa, const TailFirstOrder* fo = nullptr);
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
 // ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1); xo (k = 16,

@@ -247,3 +247,35 @@ def test_bf16_tower_tail_matches_unfused(kind, B):
         index = np.repeat(np.arange(n, dtype=np.int64), F)
         ref = oc.forward(om, n, index, np.array([0.01], np.float32), w, e, mats, 2)
         assert np.abs(got[1][r0:r0 + n] - ref).max() <= TOL_BF16
+
+
+@pytest.mark.parametrize("B", [1000, 65536])
+def test_bf16_tail_first_order_bitwise(B):
+    """PNN bf16: the tower tail's head sums the first order itself (tail_fo, default on: field order from
+    0, encoder_k16_kernel<0>'s arithmetic) -- bitwise the predictions of the first-order kernel path."""
+    import rmx
+    ctx = rmx.default_context()
+    V = 50_003
+    m, _ = _model("pnn", V)
+    t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16)
+    t.fill_synthetic(SEED_TAB)
+    m.setPrecision(rmx.DTYPE_BF16)
+    m.setMats(oc.round_bf16(m.initMats(SEED_MATS)))
+    m.setBias(0.01)
+    ids_d = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_d)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    got = {}
+    try:
+        for fo in (0, 1):
+            rmx.set_tuning("tail_fo", fo)
+            m.set_timing(True)
+            m.forward_ids(t, B, ids_d, out)
+            ctx.sync()
+            stages, _ = m.get_timing()
+            m.set_timing(False)
+            got[fo] = out.numpy().copy()
+            assert ("first_order" in stages) == (fo == 0), stages
+    finally:
+        rmx.set_tuning("tail_fo", None)
+    assert np.array_equal(got[0], got[1])
