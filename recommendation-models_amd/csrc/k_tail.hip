@@ -59,6 +59,8 @@ constexpr size_t kTLds = kTImg + sizeof(float) * (kTCW * kTBM + kTPrm);
 
 static_assert(kTLds <= 160 * 1024, "LDS budget");
 static_assert(kTSlots == kTKS + kTE && kTL3 == kTKS - kTE, "the slot rotation below");
+static_assert(kTInsE == 40 && kTInsL == 64 && kTLW == 3,
+              "the loaders' counted vmcnt waits: 40 early-step DMAs (14 / 13 / 13), 64 late ones (22 / 21 / 21)");
 
 // The 18 step slots rotate between row blocks: block t holds its K step c in slot S_t[c].  Block t + 1's
 // early steps go to the 5 slots block t does not use (loadable any time during block t), its late steps
