@@ -47,7 +47,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 PEAK_S3_TFLOPS = PEAK_BF16_TFLOPS / 6
 # stages whose GEMMs run on the split (f32_split on): priced against its peak.  The backward stages
 # (dW and dX on the split; the CIN backward's rocBLAS part is fp32) take the higher peak too.
-S3_STAGES = ("tower_layer", "cin_layer", "tower_back", "cin_back")
+S3_STAGES = ("tower_layer", "tower_tail", "cin_layer", "tower_back", "cin_back")
 
 
 def parse():
@@ -130,7 +130,7 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * FC[0] * FC[1]
     if stage == "tower_layer3":
         return "flop", 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
-    if stage == "tower_tail":  # bf16: layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip)
+    if stage == "tower_tail":  # layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip, k_tail_s3.hip)
         return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
     if stage.startswith("cin_layer"):
         idx = {"cin_layer1": 0, "cin_layer2": 1, "cin_layer3+": 2}[stage]

@@ -821,6 +821,11 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
       return launch_tower_tail_bf16(s, L, m.layers[i + 1], B, reinterpret_cast<const bf16_t*>(A), lda, oa,
                                     tail_fo ? &fo : nullptr);
     }
+    // fp32: the same pair on the split GEMM with h2 in registers (k_tail_s3.hip)
+    if (i >= 1 && i + 2 == m.layers.size() && m.precision == kF32 && tower_tail_s3_usable(L, m.layers[i + 1], B, lda)) {
+      StageTimer t(m, s, "tower_tail");
+      return launch_tower_tail_s3(s, L, m.layers[i + 1], B, A, lda, oa);
+    }
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
     XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};

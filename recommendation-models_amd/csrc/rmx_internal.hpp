@@ -135,6 +135,11 @@ struct TailFirstOrder {  // the first order summed by the tail itself (bf16 weig
 };
 int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const bf16_t* H, int lda,
                            const OutArgs& oa, const TailFirstOrder* fo = nullptr);
+// fp32 tower tail (k_tail_s3.hip): ReLU(H L2) -> ReLU(. L3) . wo -> head on the split GEMM, one persistent
+// launch, h2 in registers; both layers 400 x 400 with split planes; H [M][lda] fp32
+bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda);
+int launch_tower_tail_s3(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const float* H, int lda,
+                         const OutArgs& oa);
 // logit / sigmoid head over stored last-hidden activations h[M][ldh] (one wave per row)
 int launch_tower_head(hipStream_t s, int M, int N, const float* h, int ldh, const OutArgs& oa);
 // ld: row stride of the table in elements (0 = k); wld: stride of the weights (0 = 1); xo (k = 16,
