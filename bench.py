@@ -872,19 +872,24 @@ def sharded_companion(args, rmx, ctx, rank, world, dist, line):
     t_lim = args.companion_timeout
     out_fd = os.dup(1)  # the real stdout: the watchdog may fire inside stdout_to_stderr (RCCL init)
 
+    closing = threading.Event()  # set before the shards are closed: the watchdog then only exits
+
     def expire():
         sys.stderr.write("bench.py: the sharded sub-record passed %.0f s; aborting its communicator\n" % t_lim)
-        for t in LIVE_SHARDS:
-            try:
-                t.abort()
-            except Exception:
-                pass
+        if not closing.is_set():  # (ShardedTable.abort / close are also ordered by the table's lock)
+            for t in list(LIVE_SHARDS):
+                try:
+                    t.abort()
+                except Exception:
+                    pass
         if line is not None:
             out = dict(line)
             out.setdefault("models", {})["deepfm_sharded"] = {
                 "error": "timed out after %.0f s (watchdog aborted the RCCL communicator)" % t_lim}
             os.write(out_fd, (json.dumps(out) + "\n").encode())
-        os._exit(0)  # the main measurement stands; the line records the failure
+        # the line (with the main measurement) is out; the non-zero status tells launch_ranks and the
+        # driver that the multi-GPU exchange hung
+        os._exit(124)
     wd = threading.Timer(t_lim, expire)
     wd.daemon = True
     wd.start()
@@ -906,6 +911,7 @@ def sharded_companion(args, rmx, ctx, rank, world, dist, line):
                 t.abort()
             except Exception:
                 pass
+    closing.set()
     for t in LIVE_SHARDS:  # (still under the watchdog: destroy synchronises the device)
         t.close()
     del LIVE_SHARDS[:]

@@ -241,6 +241,15 @@ int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32
  * :165-199).  owner(id) = p(id) mod nranks, local row = p(id) div nranks, p the keyed permutation of
  * rmx_shard_set_owner_hash (default key RMX_OWNER_HASH_DEFAULT).  One exchange per batch over
  * RCCL (grouped send/recv = all-to-all over xGMI): ids to owners, rows back.
+ * At nranks > 1 the exchange has fixed-capacity buckets (~1.1 x ids / nranks per peer): every message
+ * size is known on the host, so the exchange makes no host sync; ids past a bucket's capacity get their
+ * rows in a second, counted round that every rank runs when any rank overflowed (each rank's header
+ * carries its overflow flag).  The overflow check is made when the slot is consumed (or, for
+ * rmx_forward_ids_sharded / rmx_shard_gather, after the forward / copy is queued, which then runs again).
+ * An id outside [0, num_rows) reads a zero row on every path.
+ * CONTRACT CHANGE (round 3): the default owner function is the keyed permutation below, no longer
+ * id mod nranks.  A caller that pre-partitions ids or rows must use rmx_owner_hash (or
+ * rmx_shard_set_owner_hash(sh, 0) for id mod nranks). 
  * rmx_comm_unique_id: rank 0 creates the RCCL id (RMX_UNIQUE_ID_BYTES bytes) and the caller
  * broadcasts it (e.g. torch.distributed / MPI / Spark broadcast).  unique_id == NULL creates a
  * LOOPBACK shard: all nranks partitions live in this process on ctx's GPU and the exchange is
@@ -276,6 +285,9 @@ int64_t rmx_owner_hash(uint64_t key, int64_t num_rows, int nranks, int64_t id, i
 int rmx_shard_set_dedupe(rmx_shard* sh, int on);
 /* Ids this rank sent to owners in its last exchange (the distinct ids when deduplicating). */
 int64_t rmx_shard_last_sent(const rmx_shard* sh);
+/* Overflow rounds this shard has run (fixed-capacity exchange at nranks > 1: an id past its bucket's
+ * capacity on any rank); -1 for a NULL shard. */
+int64_t rmx_shard_overflow_rounds(const rmx_shard* sh);
 /* Collective (every rank calls it): d_w[i] = w[ids[i]], d_emb[i*k+j] = emb[ids[i]][j] gathered
  * from the owners (makeWeights / makeEmbeddings through the exchange).  Bit-exact copies. */
 int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,

@@ -67,6 +67,10 @@ static_assert(kQQ == 5 && kQIns == 39, "the static vmcnt counts below assume 5 D
 #ifndef RMX_QTAIL_DIAG
 #define RMX_QTAIL_DIAG 0
 #endif
+// weight-fragment prefetch depth (column tiles) of the layer-3 units, where h2's 100 registers are live
+#ifndef RMX_QTAIL_PF3
+#define RMX_QTAIL_PF3 1
+#endif
 
 // a zero h1 row: the load source of rows past M (every lane issues the same loads at every K offset)
 __device__ __attribute__((aligned(16))) float g_qzero_row[kQN];
@@ -119,10 +123,9 @@ __device__ __forceinline__ int q_fbase(int lane) {
 // One unit: NT column tiles (local tiles 0 .. NT - 1 of the unit's half) of one K step.  acc[T0 + t] +=
 // W_t h^T on the split planes (ah, am, al) of this wave's 16 rows; dma(q) issues the wave's q-th DMA of
 // unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.
-template <int NT, int T0, int NA>
+template <int NT, int T0, int NA, int PF = 2>
 __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                        f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo) {
-  constexpr int PF = 2;
   f32x4 bq[PF + 1][3];
   int fbu = fb;
   asm volatile("" : "+v"(fbu));
@@ -179,8 +182,12 @@ __device__ __forceinline__ void q_h1_dma(const TailS3Args& p, const float* zrow,
   for (int i = 0; i < 2; ++i) {
     int r = 8 * i + (lane >> 3), j = (lane & 7) ^ ((lane >> 3) & 7);
     asm volatile("" : "+v"(r), "+v"(j));  // formed here (not hoisted)
+    // branch-free (an exec-masked address branch split the unit into basic blocks): rows past M
+    // read the zero row at the same column offset (M * lda < 2^31: launch check)
     const int m = rb * kQBM + w * 16 + r;
-    const float* row = (rb < p.nblk && m < p.M) ? p.H + (int64_t)m * p.lda : zrow;
+    const uint32_t ok = (rb < p.nblk && m < p.M) ? 1u : 0u;
+    const uintptr_t base = (uintptr_t)zrow + (uintptr_t)ok * ((uintptr_t)p.H - (uintptr_t)zrow);
+    const float* row = reinterpret_cast<const float*>(base) + (uint32_t)(m * (int)ok) * (uint32_t)p.lda;
     __builtin_amdgcn_global_load_lds(row + 32 * c + 4 * j,
                                      (__attribute__((address_space(3))) void*)(hlds + ds * 2048 + i * 1024), 16, 0,
                                      0);
@@ -233,9 +240,9 @@ __device__ __forceinline__ void q_layer3(const TailS3Args& p, char* lds, const f
     const int dslot = slot == 0 ? 2 : slot - 1;  // (slot + 2) mod 3
     const char* ub = lds + slot * kQUnit;
     if constexpr (HF == 0)
-      q_unit<kQUT, 0>(ub, fb, ah, am, al, acc, q_unit_src(p, u2), lds, dslot, w, lo);
+      q_unit<kQUT, 0, kQUT, RMX_QTAIL_PF3>(ub, fb, ah, am, al, acc, q_unit_src(p, u2), lds, dslot, w, lo);
     else
-      q_unit<kQUT - 1, 0>(ub, fb, ah, am, al, acc, q_unit_src(p, u2), lds, dslot, w, lo);
+      q_unit<kQUT - 1, 0, kQUT, RMX_QTAIL_PF3>(ub, fb, ah, am, al, acc, q_unit_src(p, u2), lds, dslot, w, lo);
     slot = q_next(slot);
   }
   // the output dot over this half's columns: ReLU(acc + b3)[n] * wo[n], n = 16 (13 HF + t) + 4 g + q

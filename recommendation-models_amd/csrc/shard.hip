@@ -93,7 +93,10 @@ struct rmx_shard {
   int k = 0, N = 1, rank = 0;
   bool loopback = false;
   ncclComm_t comm = nullptr;
-  std::atomic<bool> aborted{false};     // rmx_shard_abort ran: the communicator is torn down
+  // the communicator's life: 0 live, 1 aborted (rmx_shard_abort tore it down), 2 destroyed.  Abort and
+  // destroy each claim it by compare-exchange from 0, so exactly one of ncclCommAbort / ncclCommDestroy
+  // runs; the RCCL transport checks it before every call (nothing is posted on a torn-down comm)
+  std::atomic<int> comm_state{0};
   rmx_group* group = nullptr;           // in-process exchange group (or null)
   std::unique_ptr<rmx::Transport> tr;   // RCCL or group transport (null: loopback)
   int64_t rows_per = 0;                 // ceil(V / N) local rows per partition
@@ -104,7 +107,9 @@ struct rmx_shard {
                                         // extra row stays zero (the row of an out-of-range id read in place)
   // per-batch buffers (grow only)
   int64_t cap_send = 0, cap_recv = 0;
-  int64_t cap_slot[2] = {0, 0};         // ids each pull slot's buffers hold (grown one slot at a time)
+  int64_t cap_slot[2] = {0, 0};         // ids each pull slot's perm holds (grown one slot at a time)
+  int64_t cap_rows[2] = {0, 0};         // rows each pull slot's recv_emb / recv_w hold
+  int64_t cap_sfix = 0;                 // send_ids elements (max(nnz, N * cap))
   int32_t* counts = nullptr;            // [4N]: send counts, recv counts, cursors, scratch
   int32_t* h_counts = nullptr;          // pinned host [2N]
   int32_t* send_ids = nullptr;          // [nnz] local rows, bucketed by owner
@@ -137,8 +142,37 @@ struct rmx_shard {
   int32_t* hslot = nullptr;             // [nnz] set slot of id n
   mutable int64_t last_sent = 0;        // ids sent by the last exchange (distinct ids when deduped)
   mutable bool last_sent_dev = false;   // one rank: last_sent is still on the device (counts[0])
+  mutable int last_fixed = -1;          // >= 0: last_sent is the summary of that slot's fixed exchange (pinned)
   int32_t* bcnt = nullptr;              // [N][tiles] per-tile owner counts -> tile start offsets
   int64_t cap_tiles = 0;
+  // Fixed-capacity exchange (N > 1 through a transport; knob "shard_fixed", default on): every peer bucket
+  // has the host-known capacity cap (cap_of: ~1.1 nnz / N), so every message size is fixed and no count
+  // has to reach the host before the rows move.  The first cap ids of bucket o go in send_ids[o][cap],
+  // the rest (overflow) in send_ovf; each rank's header tells every peer its count and whether it
+  // overflowed anywhere, so all ranks learn the same "any overflow" and agree on running a second,
+  // counted round for the overflow ids (shard_resolve) -- never a different number of collectives.
+  int64_t cap_fix = 0;                  // N * cap held by recv_fix / srow_*
+  // The capacity must be the same on every rank (the message sizes pair up) without a host round trip,
+  // so it comes from the PREVIOUS exchange: ~1.1 x the largest routed total of any rank there / N (every
+  // rank reads the same maximum from its summary).  The first exchange has cap 0: every id goes through
+  // the counted overflow round.
+  int64_t cap_next = 0;
+  int32_t* send_ovf = nullptr;          // [cap_send] overflow ids in bucket order
+  int32_t* recv_fix = nullptr;          // [N][cap] ids requested by the peers
+  float* srow_emb = nullptr;            // [N][cap][k] rows gathered for the peers
+  float* srow_w = nullptr;              // [N][cap]
+  int32_t* hdr = nullptr;               // device: headers sent [N][3] | received [N][3] | summary [2N + 2]
+  int32_t* h_hdr_s[2] = {nullptr, nullptr};   // pinned per pull slot: the summary (counts sent, received, any, max total)
+  hipEvent_t hdr_ev[2] = {nullptr, nullptr};  // the slot's summary has reached the host
+  bool unresolved[2] = {false, false};  // a fixed exchange whose overflow check is pending
+  hipStream_t slot_stream[2] = {nullptr, nullptr};  // its stream (the overflow round runs there)
+  int64_t slot_cap[2] = {0, 0}, slot_n[2] = {0, 0};
+  bool slot_dd[2] = {false, false};
+  int64_t rounds2 = 0;                  // overflow rounds run so far
+  int64_t cap_ovf = 0;                  // owner side of the overflow round (grown on demand)
+  int32_t* recv_ovf = nullptr;
+  float* ovf_emb = nullptr;
+  float* ovf_w = nullptr;
   // one exchange at a time per shard; the per-batch buffers are ordered across streams like a
   // model's workspace (rmx::ModelUse)
   std::mutex mu;
@@ -298,20 +332,29 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(int nb, int32_t* __res
   if (t == 1023) counts[blockIdx.x] = part[1023];
 }
 
-// slot of id n = owner offset + tile start for o + rank in the tile
+// Position of id n in its owner's bucket = tile start for o + rank in the tile.  Dense layout (cap < 0):
+// slot = owner offset + position.  Fixed layout (cap >= 0): slot o * cap + position while position < cap,
+// else the overflow list: send_ovf[q] with q = (overflow of the buckets before o) + position - cap, and
+// the row slot N * cap + q.  An id with no owner (outside [0, V), or an empty dedupe slot) gets zslot,
+// a row that stays zero.
 __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nnz, int N, int nb,
                                                                      const int32_t* __restrict__ ids,
                                                                      const int32_t* __restrict__ counts,
                                                                      const int32_t* __restrict__ bstart,
                                                                      int32_t* __restrict__ send_ids,
-                                                                     int32_t* __restrict__ perm, OwnerPerm op) {
-  __shared__ int h[kMaxRanks], start[kMaxRanks];
+                                                                     int32_t* __restrict__ perm, OwnerPerm op,
+                                                                     int32_t cap, int32_t zslot,
+                                                                     int32_t* __restrict__ send_ovf) {
+  __shared__ int h[kMaxRanks], start[kMaxRanks], ovs[kMaxRanks];
   if (threadIdx.x == 0) {
-    int s = 0;
+    int s = 0, so = 0;
     for (int o = 0; o < N; ++o) {
-      start[o] = s + bstart[(int64_t)o * nb + blockIdx.x];
+      const int b = bstart[(int64_t)o * nb + blockIdx.x];
+      start[o] = cap >= 0 ? b : s + b;  // fixed: the position inside the bucket
+      ovs[o] = so;
       h[o] = 0;
       s += counts[o];
+      so += cap >= 0 && counts[o] > cap ? counts[o] - cap : 0;
     }
   }
   __syncthreads();
@@ -325,11 +368,20 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(int64_t nn
     const int rk = wave_reserve(own[u], h);
     const int64_t n = base + u * kRouteThreads + threadIdx.x;
     if (own[u] >= 0) {
-      const int slot = start[own[u]] + rk;
-      send_ids[slot] = loc[u];
-      perm[n] = slot;
+      const int pos = start[own[u]] + rk;
+      if (cap < 0) {
+        send_ids[pos] = loc[u];
+        perm[n] = pos;
+      } else if (pos < cap) {
+        send_ids[own[u] * cap + pos] = loc[u];
+        perm[n] = own[u] * cap + pos;
+      } else {
+        const int q = ovs[own[u]] + pos - cap;
+        send_ovf[q] = loc[u];
+        perm[n] = N * cap + q;
+      }
     } else if (n < nnz) {
-      perm[n] = 0;  // no owner: a defined in-range slot, never an out-of-bounds read downstream
+      perm[n] = zslot;  // no owner: the zero row
     }
   }
 }
@@ -362,6 +414,76 @@ __global__ __launch_bounds__(256) void owner_gather_kernel(int64_t n, const int3
   const float* row = part + (int64_t)rows[t] * rs;
   for (int j = 0; j < k; ++j) out_emb[t * k + j] = row[j];
   out_w[t] = row[k];
+}
+
+// headers of the fixed exchange: to every peer o {count of bucket o, this rank overflowed anywhere,
+// this rank's routed total}
+__global__ void fixed_header_kernel(int N, int32_t cap, const int32_t* __restrict__ counts, int32_t* __restrict__ hdr) {
+  int any = 0, tot = 0;
+  for (int p = 0; p < N; ++p) {
+    any |= counts[p] > cap ? 1 : 0;
+    tot += counts[p];
+  }
+  for (int o = threadIdx.x; o < N; o += blockDim.x) {
+    hdr[3 * o] = counts[o];
+    hdr[3 * o + 1] = any;
+    hdr[3 * o + 2] = tot;
+  }
+}
+
+// the summary the host reads later: counts sent [N], counts received [N] (own bucket: its own count),
+// the OR of every rank's overflow flag and the largest routed total of any rank -- the last two the
+// same on every rank
+__global__ void fixed_summary_kernel(int N, int me, const int32_t* __restrict__ counts, const int32_t* __restrict__ hs,
+                                     const int32_t* __restrict__ hr, int32_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  int any = hs[3 * me + 1], mx = hs[3 * me + 2];
+  for (int o = 0; o < N; ++o) {
+    out[o] = counts[o];
+    out[N + o] = o == me ? counts[me] : hr[3 * o];
+    if (o != me) {
+      any |= hr[3 * o + 1];
+      mx = max(mx, hr[3 * o + 2]);
+    }
+  }
+  out[2 * N] = any;
+  out[2 * N + 1] = mx;
+}
+
+// Owner gather of the fixed exchange, one launch: for a peer o, row j < min(its count, cap) of its
+// request recv_fix[o][j] into srow[o][j]; for the own bucket, send_ids[me][j] straight into this rank's
+// received rows (slot me * cap + j).  Lane map as owner_gather_kernel (k = 16 line rows: 8 lanes).
+__global__ __launch_bounds__(256) void fixed_gather_kernel(int N, int me, int32_t cap, int k, int rs,
+                                                          const int32_t* __restrict__ counts,
+                                                          const int32_t* __restrict__ hr,
+                                                          const int32_t* __restrict__ send_ids,
+                                                          const int32_t* __restrict__ recv_fix,
+                                                          const float* __restrict__ part, float* __restrict__ srow_emb,
+                                                          float* __restrict__ srow_w, float* __restrict__ recv_emb,
+                                                          float* __restrict__ recv_w) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool fast = k == 16 && rs == 32;
+  const int64_t i = fast ? t >> 3 : t;
+  if (i >= (int64_t)N * cap) return;
+  const int o = (int)(i / cap), j = (int)(i - (int64_t)o * cap);
+  const int cnt = min(o == me ? counts[me] : hr[3 * o], cap);
+  if (j >= cnt) return;
+  const int r = o == me ? send_ids[i] : recv_fix[i];
+  float* oe = o == me ? recv_emb : srow_emb;
+  float* ow = o == me ? recv_w : srow_w;
+  if (fast) {
+    const int c = (int)(t & 7);
+    if (c > 4) return;
+    const float4 v = reinterpret_cast<const float4*>(part)[(int64_t)r * 8 + c];
+    if (c < 4)
+      reinterpret_cast<float4*>(oe)[i * 4 + c] = v;
+    else
+      ow[i] = v.x;
+    return;
+  }
+  const float* row = part + (int64_t)r * rs;
+  for (int q = 0; q < k; ++q) oe[i * k + q] = row[q];
+  ow[i] = row[k];
 }
 
 // One rank, no dedupe: routing is the identity (every id is this rank's own, bucket order = batch
@@ -491,30 +613,67 @@ int realloc_dev(T** p, int64_t n) {
 // [nnz]-sized buffers of this rank's batch: the exchange's scratch, and pull slot `slot` only.
 // The other slot may hold a pull its forward has not consumed (or is still reading): it is never
 // touched here.  The slot being grown has no pending pull (rmx_shard_pull refuses one), and the
-// device sync retires any forward still reading its old buffers.
-int ensure_batch(rmx_shard& sh, int64_t nnz, int slot) {
-  if (nnz <= sh.cap_send && nnz <= sh.cap_slot[slot]) return RMX_OK;
+// device sync retires any forward still reading its old buffers.  nfix: N * cap of a fixed exchange
+// (0: dense buckets) -- send_ids then holds [N][cap] and the slot's rows nfix + nnz + 1 (the fixed
+// buckets, the overflow rows, the zero row).
+int ensure_batch(rmx_shard& sh, int64_t nnz, int slot, int64_t nfix = 0) {
+  const int64_t nrows = nfix + nnz + 1;
+  if (nnz <= sh.cap_send && nfix <= sh.cap_sfix && nnz <= sh.cap_slot[slot] && nrows <= sh.cap_rows[slot])
+    return RMX_OK;
   RMX_HIP(hipDeviceSynchronize());  // in-flight work on any stream may still use the old buffers
   int st;
-  if (nnz > sh.cap_send) {
+  if (nnz > sh.cap_send || nfix > sh.cap_sfix) {
+    const int64_t n = std::max(nnz, sh.cap_send);
     int64_t hc = 1024;
-    while (hc < 2 * nnz) hc <<= 1;
-    if ((st = realloc_dev(&sh.send_ids, nnz)) || (st = realloc_dev(&sh.hslot, nnz)) ||
-        (st = realloc_dev(&sh.hkeys, hc)) || (st = realloc_dev(&sh.hvals, hc))) {
-      sh.cap_send = sh.cap_hash = 0;
+    while (hc < 2 * n) hc <<= 1;
+    const int64_t sf = std::max(std::max(n, nfix), sh.cap_sfix);
+    if ((st = realloc_dev(&sh.send_ids, sf)) || (st = realloc_dev(&sh.send_ovf, n)) ||
+        (st = realloc_dev(&sh.hslot, n)) || (st = realloc_dev(&sh.hkeys, hc)) || (st = realloc_dev(&sh.hvals, hc))) {
+      sh.cap_send = sh.cap_hash = sh.cap_sfix = 0;
       return st;
     }
-    sh.cap_send = nnz;
+    sh.cap_send = n;
+    sh.cap_sfix = sf;
     sh.cap_hash = hc;
   }
-  if (nnz > sh.cap_slot[slot]) {
-    if ((st = realloc_dev(&sh.perm_s[slot], nnz)) || (st = realloc_dev(&sh.recv_emb_s[slot], nnz * sh.k)) ||
-        (st = realloc_dev(&sh.recv_w_s[slot], nnz))) {
-      sh.cap_slot[slot] = 0;
+  if (nnz > sh.cap_slot[slot] || nrows > sh.cap_rows[slot]) {
+    const int64_t n = std::max(nnz, sh.cap_slot[slot]), r = std::max(nrows, sh.cap_rows[slot]);
+    if ((st = realloc_dev(&sh.perm_s[slot], n)) || (st = realloc_dev(&sh.recv_emb_s[slot], r * sh.k)) ||
+        (st = realloc_dev(&sh.recv_w_s[slot], r))) {
+      sh.cap_slot[slot] = sh.cap_rows[slot] = 0;
       return st;
     }
-    sh.cap_slot[slot] = nnz;
+    sh.cap_slot[slot] = n;
+    sh.cap_rows[slot] = r;
   }
+  return RMX_OK;
+}
+
+// [N * cap]-sized owner-side buffers of the fixed exchange
+int ensure_fixed(rmx_shard& sh, int64_t nfix) {
+  if (nfix <= sh.cap_fix) return RMX_OK;
+  RMX_HIP(hipDeviceSynchronize());  // a peer's copy of the old rows may still be in flight
+  int st;
+  if ((st = realloc_dev(&sh.recv_fix, nfix)) || (st = realloc_dev(&sh.srow_emb, nfix * sh.k)) ||
+      (st = realloc_dev(&sh.srow_w, nfix))) {
+    sh.cap_fix = 0;
+    return st;
+  }
+  sh.cap_fix = nfix;
+  return RMX_OK;
+}
+
+// owner side of the overflow round
+int ensure_ovf(rmx_shard& sh, int64_t n) {
+  if (n <= sh.cap_ovf) return RMX_OK;
+  RMX_HIP(hipDeviceSynchronize());
+  int st;
+  if ((st = realloc_dev(&sh.recv_ovf, n)) || (st = realloc_dev(&sh.ovf_emb, n * sh.k)) ||
+      (st = realloc_dev(&sh.ovf_w, n))) {
+    sh.cap_ovf = 0;
+    return st;
+  }
+  sh.cap_ovf = n;
   return RMX_OK;
 }
 
@@ -580,22 +739,41 @@ __global__ __launch_bounds__(256) void unpermute_kernel(int64_t n, int k, const 
 // ---------------------------------------------------------------- transports --
 namespace {
 
+// Every call first checks the shard's communicator state: after rmx_shard_abort (or during destroy)
+// nothing more is posted on the torn-down communicator -- the exchange fails with RMX_E_COMM instead
+// (an abort while the exchange was in flight used to reach ncclSend on a freed comm)
 struct RcclTransport : Transport {
   ncclComm_t comm;
-  explicit RcclTransport(ncclComm_t c) : comm(c) {}
+  const std::atomic<int>* state;
+  RcclTransport(ncclComm_t c, const std::atomic<int>* st) : comm(c), state(st) {}
+  int live() const {
+    if (state->load() == 0) return RMX_OK;
+    set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
+    return RMX_E_COMM;
+  }
   int start() override {
+    if (int e = live()) return e;
     RMX_NCCL(ncclGroupStart());
     return RMX_OK;
   }
   int send(const void* p, size_t bytes, int peer, hipStream_t s) override {
+    if (int e = live()) return e;
     RMX_NCCL(ncclSend(p, bytes, ncclInt8, peer, comm, s));
     return RMX_OK;
   }
   int recv(void* p, size_t bytes, int peer, hipStream_t s) override {
+    if (int e = live()) return e;
     RMX_NCCL(ncclRecv(p, bytes, ncclInt8, peer, comm, s));
     return RMX_OK;
   }
   int end(hipStream_t) override {
+    // (a group already started is closed even after an abort: ncclGroupEnd only flushes this thread's
+    // group state; with the comm torn down the ops of the group were never posted)
+    if (state->load() != 0) {
+      (void)ncclGroupEnd();
+      set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
+      return RMX_E_COMM;
+    }
     RMX_NCCL(ncclGroupEnd());
     return RMX_OK;
   }
@@ -756,6 +934,11 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
   }
   RMX_HIP(hipMalloc(&sh->counts, sizeof(int32_t) * 4 * N));
   RMX_HIP(hipHostMalloc(&sh->h_counts, sizeof(int32_t) * 2 * N));
+  RMX_HIP(hipMalloc(&sh->hdr, sizeof(int32_t) * (8 * N + 2)));
+  for (int q = 0; q < 2; ++q) {
+    RMX_HIP(hipHostMalloc(&sh->h_hdr_s[q], sizeof(int32_t) * (2 * N + 2)));
+    RMX_HIP(hipEventCreateWithFlags(&sh->hdr_ev[q], hipEventDisableTiming));
+  }
   if (group) {
     std::lock_guard<std::mutex> lk(group->mu);
     if (!group->ev_send[rank]) {
@@ -770,7 +953,7 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     RMX_NCCL(ncclCommInitRank(&sh->comm, N, id, rank));
-    sh->tr.reset(new RcclTransport(sh->comm));
+    sh->tr.reset(new RcclTransport(sh->comm, &sh->comm_state));
   }
   *out = sh.release();
   return RMX_OK;
@@ -782,7 +965,8 @@ int shard_destroy(rmx_shard* sh) {
   (void)hipDeviceSynchronize();  // the exchange may have run on any stream
   sh->tr.reset();
   if (sh->ws_fence) (void)hipEventDestroy(sh->ws_fence);
-  if (sh->comm && !sh->aborted.load()) ncclCommDestroy(sh->comm);
+  int live = 0;  // claim the communicator: a concurrent rmx_shard_abort that got there first freed it
+  if (sh->comm && sh->comm_state.compare_exchange_strong(live, 2)) ncclCommDestroy(sh->comm);
   if (sh->group) {
     {
       std::lock_guard<std::mutex> lk(sh->group->mu);
@@ -792,13 +976,17 @@ int shard_destroy(rmx_shard* sh) {
   }
   for (float* q : sh->part) (void)hipFree(q);
   for (void* p : {(void*)sh->counts, (void*)sh->send_ids, (void*)sh->recv_ids, (void*)sh->send_emb, (void*)sh->send_w,
-                  (void*)sh->hkeys, (void*)sh->hvals, (void*)sh->hslot, (void*)sh->bcnt})
+                  (void*)sh->hkeys, (void*)sh->hvals, (void*)sh->hslot, (void*)sh->bcnt, (void*)sh->send_ovf,
+                  (void*)sh->recv_fix, (void*)sh->srow_emb, (void*)sh->srow_w, (void*)sh->hdr, (void*)sh->recv_ovf,
+                  (void*)sh->ovf_emb, (void*)sh->ovf_w})
     if (p) (void)hipFree(p);
   for (int q = 0; q < 2; ++q) {
     for (void* p : {(void*)sh->perm_s[q], (void*)sh->recv_emb_s[q], (void*)sh->recv_w_s[q]})
       if (p) (void)hipFree(p);
     if (sh->ready[q]) (void)hipEventDestroy(sh->ready[q]);
     if (sh->consumed[q]) (void)hipEventDestroy(sh->consumed[q]);
+    if (sh->hdr_ev[q]) (void)hipEventDestroy(sh->hdr_ev[q]);
+    if (sh->h_hdr_s[q]) (void)hipHostFree(sh->h_hdr_s[q]);
   }
   if (sh->h_counts) (void)hipHostFree(sh->h_counts);
   delete sh;
@@ -835,15 +1023,22 @@ void dedupe_auto(rmx_shard& sh, bool dd, int64_t nnz) {
 
 // Steps 1-5 of the exchange: fills pull slot `slot` (sh.perm / sh.recv_emb / sh.recv_w) for this
 // rank's batch.
-// Step 0-1 (dedupe + route) of this rank's batch into pull slot `slot`; *dd = dedupe ran.
-int shard_route(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot, bool* dd_out) {
+// Step 0-1 (dedupe + route) of this rank's batch into pull slot `slot`; *dd = dedupe ran.  cap >= 0: the
+// fixed-capacity bucket layout (route_scatter_kernel; cap 0 = every id in the overflow list), cap < 0 the
+// dense one; the row slot of an id with no owner is the zero row nfix + nnz (dense: nnz), cleared here.
+int shard_route(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot, bool* dd_out,
+                int64_t cap = -1) {
   const int N = sh.N;
   int st;
   *dd_out = false;
-  if ((st = ensure_batch(sh, nnz, slot))) return st;
+  const int64_t nfix = cap > 0 ? N * cap : 0;
+  if ((st = ensure_batch(sh, nnz, slot, nfix))) return st;
   sh.perm = sh.perm_s[slot];
   sh.recv_emb = sh.recv_emb_s[slot];
   sh.recv_w = sh.recv_w_s[slot];
+  const int64_t zslot = nfix + nnz;
+  RMX_HIP(hipMemsetAsync(sh.recv_emb + zslot * sh.k, 0, sizeof(float) * sh.k, s));
+  RMX_HIP(hipMemsetAsync(sh.recv_w + zslot, 0, sizeof(float), s));
   int32_t* cnt = sh.counts;  // [N] send counts
   RMX_HIP(hipMemsetAsync(sh.counts, 0, sizeof(int32_t) * 4 * N, s));
   // (auto at one rank: off -- no link traffic to save, the duplicates' rows are local reads)
@@ -872,7 +1067,7 @@ int shard_route(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids,
   hipLaunchKernelGGL(route_scan_kernel, dim3(N), dim3(1024), 0, s, nb, sh.bcnt, cnt);
   RMX_HIP(hipGetLastError());
   hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads), 0, s, rn, N, nb, rids, cnt, sh.bcnt,
-                     sh.send_ids, rslot, op);
+                     sh.send_ids, rslot, op, (int32_t)cap, (int32_t)zslot, sh.send_ovf);
   RMX_HIP(hipGetLastError());
   if (dd) {
     hipLaunchKernelGGL(dedupe_perm_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, sh.hslot,
@@ -882,12 +1077,177 @@ int shard_route(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids,
   return RMX_OK;
 }
 
+// bucket capacity of the fixed exchange for a routed total nnz: ~1.1 nnz / N (knob "shard_cap_pct", default
+// 110) + 64, a multiple of 64 -- uniform ids over N owners stay far inside it (a bucket's spread is
+// ~sqrt(nnz / N)); 0 for nnz = 0
+int64_t cap_of(const rmx_shard& sh, int64_t nnz) {
+  if (nnz <= 0) return 0;
+  const int64_t pct = std::max(1, tuning_get("shard_cap_pct", 110));
+  const int64_t c = (nnz * pct + 100 * sh.N - 1) / (100 * sh.N) + 64;
+  return (c + 63) / 64 * 64;
+}
+
+bool fixed_eligible(const rmx_shard& sh) { return sh.N > 1 && !sh.loopback && sh.tr && tuning_get("shard_fixed", 1) != 0; }
+
+// Steps 1-5 with fixed-capacity buckets (N > 1): no host sync.
+//   route into [N][cap] (+ overflow list) -> headers + ids to owners (one grouped send / recv, fixed sizes)
+//   -> summary to the host (async, read later by shard_resolve) -> owner gather (every peer + own bucket,
+//   one launch, bounded by the device counts) -> rows back (fixed sizes).
+// The ids of a bucket past cap get their rows in the overflow round, which shard_resolve runs on this
+// stream when any rank overflowed (the summary carries the OR of every rank's flag).
+int shard_exchange_fixed(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot) {
+  const int N = sh.N, k = sh.k, me = sh.rank;
+  const int64_t cap = sh.cap_next, nfix = N * cap;  // (from the previous exchange: the same on every rank)
+  if (nfix >= (int64_t(1) << 31) - nnz - 1) {
+    set_error("shard exchange: batch too large for int32 row slots");
+    return RMX_E_INVALID;
+  }
+  bool dd = false;
+  int err = shard_route(sh, s, nnz, d_ids, slot, &dd, cap);
+  auto keep = [&](int e) {
+    if (e && err == RMX_OK) err = e;
+    return err == RMX_OK;
+  };
+  if (err == RMX_OK) keep(ensure_fixed(sh, nfix));
+  int32_t* hs = sh.hdr;          // [N][3] sent
+  int32_t* hr = sh.hdr + 3 * N;  // [N][3] received
+  int32_t* sm = sh.hdr + 6 * N;  // summary [2N + 2]
+  if (err == RMX_OK) {
+    hipLaunchKernelGGL(fixed_header_kernel, dim3(1), dim3(64), 0, s, N, (int32_t)cap, sh.counts, hs);
+    keep(hipGetLastError() == hipSuccess ? RMX_OK : RMX_E_HIP);
+  }
+  Transport& tr = *sh.tr;
+  // (as in the counted exchange: every rank passes every start() / end(), a failed rank posts nothing)
+  keep(tr.start());
+  for (int o = 0; o < N && err == RMX_OK; ++o) {
+    if (o == me) continue;
+    if (keep(tr.send(hs + 3 * o, 3 * sizeof(int32_t), o, s)) && (cap == 0 || keep(tr.send(sh.send_ids + o * cap, sizeof(int32_t) * cap, o, s))) &&
+        keep(tr.recv(hr + 3 * o, 3 * sizeof(int32_t), o, s)) && cap > 0)
+      keep(tr.recv(sh.recv_fix + o * cap, sizeof(int32_t) * cap, o, s));
+  }
+  keep(tr.end(s));
+  if (err == RMX_OK) {
+    hipLaunchKernelGGL(fixed_summary_kernel, dim3(1), dim3(64), 0, s, N, me, sh.counts, hs, hr, sm);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(sh.h_hdr_s[slot], sm, sizeof(int32_t) * (2 * N + 2), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(sh.hdr_ev[slot], s) != hipSuccess) {
+      set_error("shard exchange: the summary's device-to-host copy failed");
+      keep(RMX_E_HIP);
+    }
+  }
+  if (err == RMX_OK && nfix > 0) {
+    const int64_t threads = (k == 16 && sh.rs == 32) ? nfix * 8 : nfix;
+    hipLaunchKernelGGL(fixed_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, N, me,
+                       (int32_t)cap, k, sh.rs, sh.counts, hr, sh.send_ids, sh.recv_fix, sh.part[0], sh.srow_emb,
+                       sh.srow_w, sh.recv_emb, sh.recv_w);
+    keep(hipGetLastError() == hipSuccess ? RMX_OK : RMX_E_HIP);
+  }
+  keep(tr.start());
+  for (int o = 0; o < N && err == RMX_OK && cap > 0; ++o) {
+    if (o == me) continue;
+    if (keep(tr.send(sh.srow_emb + o * cap * k, sizeof(float) * cap * k, o, s)) &&
+        keep(tr.send(sh.srow_w + o * cap, sizeof(float) * cap, o, s)) &&
+        keep(tr.recv(sh.recv_emb + o * cap * k, sizeof(float) * cap * k, o, s)))
+      keep(tr.recv(sh.recv_w + o * cap, sizeof(float) * cap, o, s));
+  }
+  keep(tr.end(s));
+  sh.unresolved[slot] = err == RMX_OK;
+  sh.last_fixed = err == RMX_OK ? slot : -1;
+  sh.last_sent_dev = false;
+  sh.slot_stream[slot] = s;
+  sh.slot_cap[slot] = cap;
+  sh.slot_n[slot] = nnz;
+  sh.slot_dd[slot] = dd;
+  return err;
+}
+
+// The overflow check of a fixed exchange in slot `slot` (a no-op once done): waits for its summary --
+// normally long on the host already -- and, when any rank overflowed, runs the counted overflow round on
+// the exchange's stream: overflow ids to owners, owner gather, rows back into [N * cap, ...).  Every rank
+// calls this for the same exchanges in the same order (the next exchange and the slot's forward both
+// resolve first), so the rounds pair up.  *ran = the overflow round ran (the slot's rows changed).
+int shard_resolve(rmx_shard& sh, int slot, bool* ran = nullptr) {
+  if (ran) *ran = false;
+  if (!sh.unresolved[slot]) return RMX_OK;
+  sh.unresolved[slot] = false;
+  RMX_HIP(hipEventSynchronize(sh.hdr_ev[slot]));
+  const int N = sh.N, k = sh.k, me = sh.rank;
+  const int32_t* h = sh.h_hdr_s[slot];
+  const int64_t cap = sh.slot_cap[slot], nfix = N * cap;
+  {  // (dedupe auto needs this exchange's sent total)
+    const int64_t keep_sent = sh.last_sent;
+    sh.last_sent = 0;
+    for (int o = 0; o < N; ++o) sh.last_sent += h[o];
+    dedupe_auto(sh, sh.slot_dd[slot], sh.slot_n[slot]);
+    if (sh.last_fixed != slot) sh.last_sent = keep_sent;
+  }
+  sh.cap_next = cap_of(sh, h[2 * N + 1]);  // the next exchange's capacity (identical on every rank)
+  if (!h[2 * N]) return RMX_OK;
+  ++sh.rounds2;
+  if (ran) *ran = true;
+  hipStream_t s = sh.slot_stream[slot];
+  std::vector<int64_t> ho(N), hro(N), os(N + 1, 0), ros(N + 1, 0);
+  for (int o = 0; o < N; ++o) {
+    ho[o] = std::max<int64_t>(0, h[o] - cap);
+    hro[o] = o == me ? 0 : std::max<int64_t>(0, h[N + o] - cap);
+    os[o + 1] = os[o] + ho[o];     // the scatter's overflow order: buckets in owner order
+    ros[o + 1] = ros[o] + hro[o];  // the peers' overflow requests, in peer order
+  }
+  int err = ensure_ovf(sh, ros[N]);
+  auto keep = [&](int e) {
+    if (e && err == RMX_OK) err = e;
+    return err == RMX_OK;
+  };
+  float* remb = sh.recv_emb_s[slot];
+  float* rw = sh.recv_w_s[slot];
+  Transport& tr = *sh.tr;
+  keep(tr.start());
+  for (int o = 0; o < N && err == RMX_OK; ++o) {
+    if (o == me) continue;
+    if (ho[o]) keep(tr.send(sh.send_ovf + os[o], sizeof(int32_t) * ho[o], o, s));
+    if (hro[o] && err == RMX_OK) keep(tr.recv(sh.recv_ovf + ros[o], sizeof(int32_t) * hro[o], o, s));
+  }
+  keep(tr.end(s));
+  if (err == RMX_OK) keep(launch_owner_gather(s, ros[N], k, sh.rs, sh.recv_ovf, sh.part[0], sh.ovf_emb, sh.ovf_w));
+  if (err == RMX_OK)
+    keep(launch_owner_gather(s, ho[me], k, sh.rs, sh.send_ovf + os[me], sh.part[0], remb + (nfix + os[me]) * k,
+                             rw + nfix + os[me]));
+  keep(tr.start());
+  for (int o = 0; o < N && err == RMX_OK; ++o) {
+    if (o == me) continue;
+    if (hro[o] && keep(tr.send(sh.ovf_emb + ros[o] * k, sizeof(float) * hro[o] * k, o, s)))
+      keep(tr.send(sh.ovf_w + ros[o], sizeof(float) * hro[o], o, s));
+    if (ho[o] && err == RMX_OK && keep(tr.recv(remb + (nfix + os[o]) * k, sizeof(float) * ho[o] * k, o, s)))
+      keep(tr.recv(rw + nfix + os[o], sizeof(float) * ho[o], o, s));
+  }
+  keep(tr.end(s));
+  if (err == RMX_OK && sh.ready[slot]) keep(hipEventRecord(sh.ready[slot], s) == hipSuccess ? RMX_OK : RMX_E_HIP);
+  return err;
+}
+
+// every pending overflow check, oldest pull first (before an exchange reuses the scratch buffers)
+int shard_resolve_all(rmx_shard& sh) {
+  int st = RMX_OK;
+  for (int q = 0; q < 2; ++q)
+    if (sh.unresolved[q] && !st) st = shard_resolve(sh, q);
+  return st;
+}
+
 // Steps 1-5 of the exchange: fills pull slot `slot` (sh.perm / sh.recv_emb / sh.recv_w) for this
 // rank's batch.
 int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot = 0) {
   const int N = sh.N, k = sh.k;
   int st;
   bool dd = false;
+  if ((st = shard_resolve_all(sh))) return st;  // a pending overflow round uses the scratch below
+  if (fixed_eligible(sh)) {
+    if (sh.comm_state.load() != 0) {
+      set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
+      return RMX_E_COMM;
+    }
+    return shard_exchange_fixed(sh, s, nnz, d_ids, slot);
+  }
+  sh.last_fixed = -1;
   if (N == 1 && !sh.loopback && sh.dedupe != 1) {
     // one rank, no dedupe (auto is off at one rank): identity routing, one gather pass, no host sync
     if ((st = ensure_batch(sh, nnz, slot))) return st;
@@ -935,7 +1295,7 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
     // (the device count also bounds a batch holding ids outside [0, V), which route no row)
     return launch_owner_gather(s, nnz, k, sh.rs, sh.send_ids, sh.part[0], sh.recv_emb, sh.recv_w, cnt);
   }
-  if (sh.aborted.load()) {
+  if (sh.comm_state.load() != 0) {
     set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
     return RMX_E_COMM;
   }
@@ -967,6 +1327,11 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
       set_error("shard exchange: the counts' device-to-host copy failed");
       keep(RMX_E_HIP);
     }
+  }
+  // an abort while this thread waited for the counts: post nothing more (the comm is torn down)
+  if (err == RMX_OK && sh.comm_state.load() != 0) {
+    set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
+    keep(RMX_E_COMM);
   }
   if (err != RMX_OK) std::fill(sh.h_counts, sh.h_counts + 2 * N, 0);  // post nothing from here
   hr[me] = hc[me];
@@ -1017,6 +1382,7 @@ bool direct_eligible(const rmx_shard& sh) {
 
 int shard_map_rows(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids, int slot) {
   int st;
+  sh.last_fixed = -1;
   if ((st = ensure_batch(sh, nnz, slot))) return st;
   sh.last_sent = nnz;
   sh.last_sent_dev = false;
@@ -1125,7 +1491,8 @@ extern "C" int rmx_shard_abort(rmx_shard* sh) {
     rmx::set_error("rmx_shard_abort: null shard");
     return RMX_E_INVALID;
   }
-  if (!sh->comm || sh->aborted.exchange(true)) return RMX_OK;
+  int live = 0;  // claim the communicator (a destroy or an earlier abort got it first: nothing to do)
+  if (!sh->comm || !sh->comm_state.compare_exchange_strong(live, 1)) return RMX_OK;
   const ncclResult_t r = ncclCommAbort(sh->comm);
   if (r != ncclSuccess) {
     rmx::set_error(std::string("rmx_shard_abort: ") + ncclGetErrorString(r));
@@ -1170,6 +1537,8 @@ extern "C" int64_t rmx_owner_hash(uint64_t key, int64_t num_rows, int nranks, in
   return p % nranks;
 }
 
+extern "C" int64_t rmx_shard_overflow_rounds(const rmx_shard* sh) { return sh ? sh->rounds2 : -1; }
+
 extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
   if (!sh) {
     set_error("rmx_shard_set_dedupe: NULL shard");
@@ -1187,6 +1556,15 @@ extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
 
 extern "C" int64_t rmx_shard_last_sent(const rmx_shard* sh) {
   if (!sh) return -1;
+  if (sh->last_fixed >= 0) {  // the last exchange was a fixed one: its summary (a local wait, no collective)
+    const int q = sh->last_fixed;
+    if (hipSetDevice(sh->ctx->device) != hipSuccess || hipEventSynchronize(sh->hdr_ev[q]) != hipSuccess) return -1;
+    int64_t t = 0;
+    for (int o = 0; o < sh->N; ++o) t += sh->h_hdr_s[q][o];
+    sh->last_sent = t;
+    sh->last_fixed = -1;
+    return t;
+  }
   if (sh->last_sent_dev) {  // one rank, deduplicated: the distinct count is counts[0] on the device
     int32_t c = 0;
     if (hipSetDevice(sh->ctx->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
@@ -1215,12 +1593,18 @@ extern "C" int rmx_shard_gather(rmx_shard* sh, int64_t n, const int32_t* d_ids, 
   if (sh->consumed_rec[0]) RMX_HIP(hipStreamWaitEvent(s, sh->consumed[0], 0));
   int st = shard_exchange(*sh, s, n, d_ids, 0);
   if (st) return st;
-  // un-permute into id order: d_emb[i] = recv_emb[perm[i]]
-  if (n <= 0) return RMX_OK;
-  const int64_t threads = sh->k == 16 ? n * 4 : n;
-  hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, sh->k, sh->perm,
-                     sh->recv_emb, sh->recv_w, d_emb, d_w);
-  RMX_HIP(hipGetLastError());
+  // un-permute into id order: d_emb[i] = recv_emb[perm[i]]; then the overflow check (a fixed exchange):
+  // when the overflow round ran, the un-permute runs again over the completed rows
+  for (int pass = 0; pass < 2; ++pass) {
+    if (n > 0) {
+      const int64_t threads = sh->k == 16 ? n * 4 : n;
+      hipLaunchKernelGGL(unpermute_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, n, sh->k,
+                         sh->perm, sh->recv_emb, sh->recv_w, d_emb, d_w);
+      RMX_HIP(hipGetLastError());
+    }
+    bool ran = false;
+    if (pass == 0 && ((st = shard_resolve(*sh, 0, &ran)) || !ran)) return st;
+  }
   return RMX_OK;
 }
 
@@ -1289,6 +1673,10 @@ extern "C" int rmx_forward_pulled(rmx_model* m, rmx_shard* sh, int32_t B, int sl
                                              " ids, not batch * nFields");
       return sh->slot_nnz[slot] < 0 ? RMX_E_INVALID : RMX_E_SHAPE;
     }
+    // the slot's overflow check (normally its summary is long on the host; the overflow round, when
+    // any rank needs it, runs on the pull's stream and re-records ready)
+    const int rst = shard_resolve(*sh, slot);
+    if (rst) return rst;
     RMX_HIP(hipStreamWaitEvent(s, sh->ready[slot], 0));
     perm = sh->perm_s[slot];
     emb = sh->recv_emb_s[slot];
@@ -1376,6 +1764,14 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
   in.dtype = kF32;
   in.beta = m->beta;
   in.out = d_out;
+  st = model_forward(*m, s, in);
+  if (m->timing) --m->timed_calls;
+  if (st) return st;
+  // a fixed exchange's overflow check comes after the forward is queued (the host waits on a summary the
+  // GPU produced before the rows even moved); when the overflow round runs, the forward runs again
+  bool ran = false;
+  if ((st = shard_resolve(*sh, 0, &ran)) || !ran) return st;
+  if (m->timing) ++m->timed_calls;
   st = model_forward(*m, s, in);
   if (m->timing) --m->timed_calls;
   return st;

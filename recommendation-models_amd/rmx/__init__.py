@@ -19,6 +19,7 @@ from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT
                    LAYOUT_ROW_MAJOR, DTYPE_F32, DTYPE_BF16, FORMAT_LIBSVM, FORMAT_LIBFFM, check, ptr)
 
 import ctypes
+import threading
 
 __all__ = ["RecModelType", "CooLongFloatMatrix", "RecModel", "LR", "DeepFM", "XDeepFM", "DCN", "PNN", "DNN",
            "Context", "DeviceArray", "EmbeddingTable", "ShardedTable", "ExchangeGroup", "comm_unique_id", "SampleParser", "RmxError", "IllegalArgumentError",
@@ -182,6 +183,7 @@ class EmbeddingTable:
         check(_lib.lib.rmx_table_create_ex(ctx.handle, int(num_rows), int(embedding_dim), int(dtype),
                                            ctypes.byref(h)))
         self.handle = h
+        self._lock = threading.Lock()
         self.ctx = ctx
         self.rows = int(num_rows)
         self.k = int(embedding_dim)
@@ -274,6 +276,7 @@ class ShardedTable:
             check(_lib.lib.rmx_shard_create(ctx.handle, int(num_rows), int(embedding_dim), int(nranks), int(rank),
                                             uid, ctypes.byref(h)))
         self.handle = h
+        self._lock = threading.Lock()
         self.ctx = ctx
         self.rows = int(num_rows)
         self.k = int(embedding_dim)
@@ -310,6 +313,10 @@ class ShardedTable:
         """Ids this rank sent to owners in its last exchange."""
         return int(_lib.lib.rmx_shard_last_sent(self.handle))
 
+    def overflow_rounds(self):
+        """Overflow rounds of the fixed-capacity exchange run so far (nranks > 1)."""
+        return int(_lib.lib.rmx_shard_overflow_rounds(self.handle))
+
     def pull(self, ids_dev, n, slot, stream=None):
         """Collective: exchange n ids into pull slot 0 / 1 (ParRecModel.pull*); a model's
         forward_pulled consumes the slot, possibly on another stream."""
@@ -321,14 +328,18 @@ class ShardedTable:
 
     def abort(self):
         """Tear down the RCCL communicator from any thread (a watchdog over a stuck exchange):
-        later exchanges raise; only close() may follow (rmx_shard_abort)."""
-        if self.handle:
-            check(_lib.lib.rmx_shard_abort(self.handle))
+        later exchanges raise; only close() may follow (rmx_shard_abort).  Serialised with close() by
+        a lock: once close() has taken the handle, abort() is a no-op (the C side also orders the
+        two by a compare-exchange on the communicator's state)."""
+        with self._lock:
+            if self.handle:
+                check(_lib.lib.rmx_shard_abort(self.handle))
 
     def close(self):
-        if self.handle:
-            _lib.lib.rmx_shard_destroy(self.handle)
-            self.handle = None
+        with self._lock:  # the handle is cleared before the destroy: a later abort() sees None
+            h, self.handle = self.handle, None
+        if h:
+            _lib.lib.rmx_shard_destroy(h)
 
     def __del__(self):
         try:

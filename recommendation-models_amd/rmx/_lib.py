@@ -103,6 +103,7 @@ SIGNATURES = [
     ("rmx_owner_hash", c_i64, [c_u64, c_i64, c_int, c_i64, c_vp]),
     ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),
     ("rmx_shard_last_sent", c_i64, [c_vp]),
+    ("rmx_shard_overflow_rounds", c_i64, [c_vp]),
     ("rmx_predict_ids", c_int, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),
     ("rmx_auc", c_int, [c_vp, c_i64, c_vp, c_vp, ctypes.POINTER(ctypes.c_double), c_vp]),
     ("rmx_samples_parse", c_int, [c_vp, c_sz, c_int, c_int, c_vp]),

@@ -1,6 +1,7 @@
 """bench.py's sharded sub-record guard (CPU, no GPU): an exception inside the companion is recorded
 in the sub-record, and a companion that never returns is ended by the watchdog, which still prints
-the main line (with the sub-record marked as timed out) and exits 0."""
+the main line (with the sub-record marked as timed out) and exits 124, so launch_ranks and the driver
+see the hang."""
 import json
 import os
 import subprocess
@@ -26,7 +27,7 @@ def test_companion_exception_is_recorded(monkeypatch):
     assert bench.LIVE_SHARDS == []
 
 
-def test_companion_watchdog_prints_line_and_exits_zero(tmp_path):
+def test_companion_watchdog_prints_line_and_exits_124(tmp_path):
     script = tmp_path / "hang.py"
     script.write_text(
         "import sys, time, types\n"
@@ -43,7 +44,7 @@ def test_companion_watchdog_prints_line_and_exits_zero(tmp_path):
         "bench.sharded_companion(args, None, None, 0, 2, None, {'metric': 'm', 'value': 3.0})\n"
         "print('not reached')\n" % ROOT)
     p = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=60)
-    assert p.returncode == 0, p.stderr
+    assert p.returncode == 124, p.stderr
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1
     d = json.loads(lines[0])

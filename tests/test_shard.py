@@ -733,3 +733,137 @@ def test_rccl_single_rank_reads_partition_in_place(kind):
     m.forward_pulled(sh, B, 1, got2, ctx.stream)
     ctx.sync()
     assert np.array_equal(got.numpy(), ref.numpy()) and np.array_equal(got2.numpy(), ref.numpy())
+
+
+# ------------------------------------ fixed-capacity exchange: overflow round, zero rows (round 4) ----
+def _group_forward_stats(kind, N, V, B, zipf, dedupe, h_ids_of=None, pipelined=False):
+    """_group_forward, also returning every rank's overflow-round count; h_ids_of(r) overrides the ids."""
+    import rmx
+    g = rmx.ExchangeGroup(N)
+
+    def rank(r):
+        ctx, ctx_x = rmx.Context(0), rmx.Context(0)
+        sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+        sh.set_dedupe(dedupe)
+        sh.fill_synthetic(SEED_TAB)
+        nb = 3 if pipelined else 1
+        ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
+        if h_ids_of is not None:
+            ids.upload(h_ids_of(r))
+        else:
+            rmx.gen_ids(ctx, SEED_IDS, 11 + r * nb * B, nb * B, F, V, ids, zipf=zipf)
+        m = _models_v(V)[kind]()
+        m.setMats(m.initMats(SEED_MATS))
+        m.setBias(0.01)
+        ctx.sync()
+        if pipelined:
+            got = _pipelined(m, sh, ids, B, nb, ctx, ctx_x)
+        else:
+            o = rmx.DeviceArray(ctx, B, np.float32)
+            for _ in range(2):  # buffers reused across batches
+                m.forward_ids_sharded(sh, B, ids, o, ctx.stream)
+            ctx.sync()
+            got = [o.numpy()]
+        out = (got, ids.numpy(), sh.overflow_rounds())
+        sh.close()
+        return out
+
+    return _run_ranks(N, rank)
+
+
+def _replicated(kind, V, h_ids, B, nb):
+    import rmx
+    ctx = rmx.default_context()
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    m = _models_v(V)[kind]()
+    m.setMats(m.initMats(SEED_MATS))
+    m.setBias(0.01)
+    ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
+    ids.upload(h_ids)
+    res = []
+    for i in range(nb):
+        ref = rmx.DeviceArray(ctx, B, np.float32)
+        m.forward_ids(table, B, ids.view(i * B * F, B * F), ref)
+        ctx.sync()
+        res.append(ref.numpy())
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipelined", [False, True])
+@pytest.mark.parametrize("N,zipf,cap_pct", [(2, 0.0, 110), (8, 0.0, 110), (4, 1.1, 110), (8, 1.1, 110),
+                                            (4, 0.0, 30), (8, 0.0, 60)])
+def test_fixed_exchange_overflow_round_bitwise(N, zipf, cap_pct, pipelined):
+    """The N > 1 exchange with fixed-capacity buckets (~1.1 nnz / N per peer, no host sync): uniform ids
+    never overflow; Zipf(1.1) ids without dedupe pile onto the hot ids' owners, and a small capacity
+    (shard_cap_pct 30 / 60) overflows every bucket -- every rank then runs the counted overflow round
+    (the same number of collectives on every rank), and every forward stays bitwise the replicated
+    table's, through forward_ids_sharded and through the pull / forward_pulled pipeline."""
+    import rmx
+    V, B = 100_003, 1000
+    rmx.set_tuning("shard_cap_pct", cap_pct)
+    try:
+        outs = _group_forward_stats("deepfm", N, V, B, zipf, False, pipelined=pipelined)
+    finally:
+        rmx.set_tuning("shard_cap_pct", None)
+    rounds = {o[2] for o in outs}
+    assert len(rounds) == 1, rounds  # every rank ran the same rounds
+    n_ex = 3 if pipelined else 2  # exchanges per rank
+    # the first exchange has no agreed capacity yet (cap 0): it always runs the overflow round
+    if zipf == 0.0 and cap_pct >= 110:
+        assert rounds == {1}
+    if cap_pct < 100:
+        assert rounds == {n_ex}
+    nb = 3 if pipelined else 1
+    for r, (got, h_ids, _) in enumerate(outs):
+        ref = _replicated("deepfm", V, h_ids, B, nb)
+        for i in range(nb):
+            assert np.array_equal(got[i], ref[i]), (r, i)
+
+
+@pytest.mark.gpu
+def test_fixed_exchange_zipf_without_dedupe_overflows():
+    """Zipf(1.1) ids at N = 8 without dedupe: the hot ids' owners get far more than 1.1 nnz / N, so the
+    overflow round runs in the second exchange too (the first always runs it; results bitwise, above)."""
+    outs = _group_forward_stats("deepfm", 8, 100_003, 2000, 1.1, False)
+    assert all(o[2] == 2 for o in outs), [o[2] for o in outs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,dedupe", [(1, True), (3, False), (3, True)])
+def test_out_of_range_ids_read_zero_rows(N, dedupe):
+    """an id outside [0, V) reads a zero row (zero embedding, zero first-order weight) on
+    every routed path -- the fixed exchange, a dedupe route, one rank -- instead of another id's row:
+    the affected samples match the fp64 oracle fed zero rows, the others are bitwise the replicated
+    forward."""
+    import rmx
+    V, B = 100_003, 400
+    bad = {(0, 3): V + 5, (7, 0): -2, (B - 1, F - 1): 1 << 30, (9, 5): -1}
+
+    def ids_of(r):
+        h = oc.gen_ids(SEED_IDS, 77 + r * B, B, F, V).reshape(B, F).copy()
+        for (i, f), v in bad.items():
+            h[i, f] = v
+        return h.ravel().astype(np.int32)
+
+    outs = _group_forward_stats("deepfm", N, V, B, 0.0, dedupe, h_ids_of=ids_of)
+    om = oc.make_model(oc.DEEPFM, F, K, fc=(400, 400, 400))
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    bad_rows = sorted({i for i, _ in bad})
+    for r, (got, h_ids, _) in enumerate(outs):
+        h = h_ids.reshape(B, F)
+        good = np.setdiff1d(np.arange(B), bad_rows)
+        fixed = h.copy()
+        fixed[bad_rows] = 0
+        ref = _replicated("deepfm", V, fixed.ravel(), B, 1)[0]
+        assert np.array_equal(got[0][good], ref[good]), r
+        sl = h[bad_rows].astype(np.int64)
+        ok = (sl >= 0) & (sl < V)
+        w, e = oc.gather(wt, et, 1, np.where(ok, sl, 0).ravel())
+        w = np.where(ok.ravel(), w, 0).astype(np.float32)
+        e = np.where(np.repeat(ok.ravel(), K), e, 0).astype(np.float32)
+        n = len(bad_rows)
+        p = oc.forward(om, n, np.repeat(np.arange(n, dtype=np.int64), F), np.array([0.01], np.float32), w, e,
+                       oc.init_mats(om, SEED_MATS), 1)
+        assert np.abs(got[0][bad_rows] - p).max() <= 1e-5, r
