@@ -47,7 +47,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 PEAK_S3_TFLOPS = PEAK_BF16_TFLOPS / 6
 # stages whose GEMMs run on the split (f32_split on): priced against its peak.  The backward stages
 # (dW and dX on the split; the CIN backward's rocBLAS part is fp32) take the higher peak too.
-S3_STAGES = ("tower_layer", "tower_tail", "cin_layer", "tower_back", "cin_back")
+S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "cin_layer", "tower_back", "cin_back")
 
 
 def parse():
@@ -82,6 +82,8 @@ def parse():
                          "leaves its idle clock state first (0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-only", action="store_true",
+                    help="no CPU timing, but the parity check of the predicted rows against the fp64 oracle (grids)")
     ap.add_argument("--set", default="", help="kernel knobs before building the model, k=v,k=v (rmx_set_tuning)")
     return ap.parse_args()
 
@@ -130,6 +132,8 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * FC[0] * FC[1]
     if stage == "tower_layer3":
         return "flop", 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
+    if stage == "tower_small":  # the whole tower (+ the output dot) in one launch (csrc/k_small_s3.hip)
+        return "flop", 2.0 * B * (k1 * FC[0] + FC[0] * FC[1] + FC[1] * FC[2] + FC[2])
     if stage == "tower_tail":  # layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip, k_tail_s3.hip)
         return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
     if stage.startswith("cin_layer"):
@@ -216,7 +220,7 @@ def cpu_baseline_plumbing(oc, budget_s, threads):
                       "(oracle/rmx_oracle.c) + Mann-Whitney AUC, %.1f s" % (done // PLUMB_ROWS, t_tot)}
 
 
-def parity_check(workload, got, row0, n=512, vocab=V):
+def parity_check(workload, got, row0, n=512, vocab=V, ids_host=None):
     """The checker beside the CPU baseline: GPU probabilities of rows [row0, row0 + n) of the bench
     set against the oracle on the same rows (fp64 oracle; bf16 workloads: the oracle's bf16-storage
     emulation, precision 2).  A V = 100M table is not materialised on the host: the
@@ -226,7 +230,8 @@ def parity_check(workload, got, row0, n=512, vocab=V):
     if workload == "xdeepfm":
         n = min(n, 64)
     mats = oc.init_mats(om, SEED_MATS)
-    ids = oc.gen_ids(SEED_IDS, row0, n, F, vocab).astype(np.int64)
+    # (ids_host: the bench's own ids read back, e.g. the Zipf(1.1) set, which the oracle has no generator for)
+    ids = (ids_host[:n * F] if ids_host is not None else oc.gen_ids(SEED_IDS, row0, n, F, vocab)).astype(np.int64)
     if vocab == V:
         wt, et = oc.gen_table(SEED_TAB, V, K)
         w, e = oc.gather(wt, et, 1, ids)
@@ -607,7 +612,8 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     res = {"value": value, "ms_per_step": t_rank * 1e3 / steps, "B": B, "Vw": Vw, "nrows": nrows,
            "roofline": roof, "stages": per_stage, "stage_sum_ms": round(stage_sum, 4), "predict_auc": pa,
            "settle_steps": settle,
-           "out": out.numpy()[:512], "bf16": bf16, "split": split}
+           "out": out.numpy()[:512], "bf16": bf16, "split": split,
+           "ids_head": ids.numpy()[:512 * F] if args.zipf else None}
     if sharded:
         res["exchange"] = {"dedupe": "off" if args.no_dedupe else ("on" if args.dedupe_on else "auto"),
                            "mode": ("one rank: the batch's ids map to partition rows p(id) and the forward reads "
@@ -770,7 +776,11 @@ def main():
         companion = run(args, "xdeepfm", rmx, ctx, rank, world, dist, args.steps, args.warmup, B=16384)
 
     cpu = cpu2 = None
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not train
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not train and not args.parity_only
+    if rank == 0 and world == 1 and args.parity_only and not train and args.workload != "lr_plumbing":
+        cpu = {"parity_check": parity_check(args.workload, r["out"], 0, vocab=r["Vw"], ids_host=r.get("ids_head"))}
+        if companion:
+            cpu2 = {"parity_check": parity_check("xdeepfm", companion["out"], 0)}
     if want_cpu:
         cpu = cpu_baseline_sweep(args.workload, args.cpu_seconds)
         if args.workload == "lr_plumbing":

@@ -1,0 +1,128 @@
+// k_rowown.hpp -- the row-owner split-GEMM machinery shared by the fp32 tower kernels of k_head_s3.hip
+// (tower layer 1, gathered) and k_tail_s3.hip (layers 2 + 3 + head), gfx950.
+//
+// A block of 8 waves (two per SIMD) owns 128 rows; a wave owns 16 rows and ALL 416 columns of a layer.
+// The MFMA runs with the operands swapped (D = W x^T, v_mfma_f32_16x16x32_bf16 with the weight plane as
+// A), so lane (r16, g) holds outputs n = 16 t + 4 g .. + 3 of its sample r16 -- the K values that lane
+// group g feeds the next layer at the split engine's positions (k_gemm.hpp kPrecS3: step c, half h,
+// K = 32 c + 16 h + 4 g + q).  The weights (fp32 pre-split into three bf16 planes, W3 [steps][3][416][32])
+// stream through LDS in "units" of one K step x one column half (13 tiles x 3 planes x 1 KiB = 39 KiB), a
+// 3-slot ring: unit U + 2's DMAs are issued during unit U, one per column tile, one barrier per unit.
+#pragma once
+
+#include "k_gemm.hpp"
+
+namespace rmx {
+namespace rowown {
+
+constexpr int kQBM = 128;                    // rows per row block
+constexpr int kQW = 8;                       // waves
+constexpr int kQThreads = kQW * 64;
+constexpr int kQNT = 25;                     // computed column tiles (N = 400)
+constexpr int kQN = 416;                     // Npad: packed rows of W per plane and K step
+constexpr int kQUT = 13;                     // column tiles per unit (one half of Npad)
+constexpr int kQUnit = 3 * kQUT * 16 * 64;   // bytes per unit: 3 planes x 208 rows x 64 B = 39,936
+constexpr int kQIns = kQUnit / 1024;         // 1-KiB DMA instructions per unit (39)
+constexpr int kQQ = (kQIns + kQW - 1) / kQW; // per wave (5; wave 7's fifth repeats instruction 38)
+constexpr int kQSlots = 3;
+static_assert(kQQ == 5 && kQIns == 39, "the static vmcnt counts assume 5 weight DMAs per wave per unit");
+
+// Diagnostic builds only (timing probes, wrong results; never set in librmx.so): 1 = no DMAs after the
+// prologue, 2 = no MFMAs
+#ifndef RMX_QTAIL_DIAG
+#define RMX_QTAIL_DIAG 0
+#endif
+// the tiles of a unit that carry its five weight DMAs (timing A/B)
+#ifndef RMX_QTAIL_DOFF
+#define RMX_QTAIL_DOFF 0
+#endif
+#ifndef RMX_QTAIL_DSTRIDE
+#define RMX_QTAIL_DSTRIDE 1
+#endif
+
+// this wave's DMA q of a unit whose planes start at `src` into the slot at `dst` (LDS byte offset).
+// Instruction ins = w + 8 q fills unit rows [16 ins, 16 ins + 16): plane ins / 13, tile ins % 13; lane L
+// writes physical 16-B slot L & 3 of row L >> 2, so it loads logical slot swz_slot(row, L & 3) (the
+// swizzle is an involution; the key of row 16 t + (L >> 2) depends on L only): lo = its element offset.
+__device__ __forceinline__ void q_dma(const bf16_t* src, char* lds, int slot, int w, int q, int lo) {
+  int ins = w + q * kQW;
+  ins = ins < kQIns ? ins : kQIns - 1;
+  const int pl = ins / kQUT, t = ins - pl * kQUT;
+  int l = lo;
+  asm volatile("" : "+v"(l));  // formed here: hoisted, the 130 per-unit sources of layer 3 spilled
+  const bf16_t* s = src + (pl * kQN + t * 16) * 32 + l;
+  __builtin_amdgcn_global_load_lds(s, (__attribute__((address_space(3))) void*)(lds + slot * kQUnit + ins * 1024), 16,
+                                   0, 0);
+}
+
+__device__ __forceinline__ int q_next(int s) { return s == kQSlots - 1 ? 0 : s + 1; }
+
+// per-lane byte offset of the weight fragments (row r16 of a tile, logical slot g), opaque so the
+// fragment addresses are formed per use
+__device__ __forceinline__ int q_fbase(int lane) {
+  int fb = (lane & 15) * 64 + swz_slot(lane & 15, lane >> 4) * 16;
+  asm volatile("" : "+v"(fb));
+  return fb;
+}
+
+// One unit: NT column tiles (local tiles 0 .. NT - 1 of the unit's half) of one K step.  acc[T0 + t] +=
+// W_t h^T on the split planes (ah, am, al) of this wave's 16 rows; dma(q) issues the wave's q-th DMA of
+// unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.
+template <int NT, int T0, int NA, int PF = 2>
+__device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
+                                       f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo) {
+  f32x4 bq[PF + 1][3];
+  int fbu = fb;
+  asm volatile("" : "+v"(fbu));
+  auto ldb = [&](int t, f32x4* b) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) b[pl] = *reinterpret_cast<const f32x4*>(ub + fbu + pl * (kQUT * 1024) + t * 1024);
+  };
+#pragma unroll
+  for (int t = 0; t < PF; ++t) ldb(t, bq[t]);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t + PF < NT) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
+    // DMA q rides tile RMX_QTAIL_DOFF + q * RMX_QTAIL_DSTRIDE
+    constexpr int kD0 = RMX_QTAIL_DOFF, kDS = RMX_QTAIL_DSTRIDE;
+    static_assert(kD0 + (kQQ - 1) * kDS < kQUT - 1, "every unit (12 or 13 tiles) carries all its DMAs");
+    if (t >= kD0 && (t - kD0) % kDS == 0 && (t - kD0) / kDS < kQQ && !(RMX_QTAIL_DIAG & 1))
+      q_dma(dsrc, lds, dslot, w, (t - kD0) / kDS, lo);
+    __builtin_amdgcn_sched_barrier(0);
+    const f32x4* b = bq[t % (PF + 1)];
+    const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
+    const bf16x8 bm = __builtin_bit_cast(bf16x8, b[1]);
+    const bf16x8 bl = __builtin_bit_cast(bf16x8, b[2]);
+    if constexpr (RMX_QTAIL_DIAG & 2) {
+      acc[T0 + t] += b[0] + b[1] + b[2] + __builtin_bit_cast(f32x4, ah);
+      continue;
+    }
+    f32x4 d = acc[T0 + t];
+    // the engine's product order (k_gemm.hpp compute_step_s3), operands swapped: smallest terms first
+    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, d, 0, 0, 0);
+    acc[T0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, d, 0, 0, 0);
+  }
+}
+
+// unit start: this unit's DMAs (issued two units ago) have landed for this wave (N = vector-memory
+// instructions the wave issued during the previous unit), then for every wave; the slot the next DMAs
+// overwrite was read by every wave before this barrier
+template <int N>
+__device__ __forceinline__ void q_enter() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ f32x4 relu4(f32x4 v) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+  return v;
+}
+
+}  // namespace rowown
+}  // namespace rmx

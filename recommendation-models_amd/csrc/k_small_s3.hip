@@ -1,0 +1,272 @@
+// k_small_s3.hip -- DeepFM's whole fp32 tower for small launch batches: one block per 16 samples, all
+// three layers + the FM / first order + the head in one launch, on the split GEMM (gfx950).
+//
+// The tower (model/encoder/HigherOrderEncoder.scala:34-59: Linear(F k -> 400) + ReLU, 400 -> 400 + ReLU,
+// 400 -> 400 + ReLU, Linear(400 -> 1)), the first order (bnn/Scatter.scala:17-36), the FM second order
+// (SecondOrderEncoder.scala:19-34) and DeepFM's head (DeepFM.scala:54-80: CAddTable + Sigmoid).
+// Why: below ~32 K samples the row-owner kernels (k_head_s3 / k_tail_s3: 128 rows per block) and the
+// column-sliced split GEMM (128-row blocks x 2 slices) launch far fewer blocks than the 256 CUs -- at
+// B = 4,096 layer 1 ran 64 blocks -- and each layer is its own launch.  Here a block owns only 16 samples
+// (B = 4,096 -> 256 blocks) and keeps them on the CU through all three layers: the gathered x tile and the
+// activations live in LDS, the 8 waves split the 25 column tiles (wave w: tiles w, w + 8, w + 16, w + 24),
+// and each wave streams its own weight fragments (1 KiB contiguous per plane, K step and tile) straight
+// from L2 into registers one K step ahead -- a fragment is read by exactly one wave of the block, so LDS
+// staging would buy no reuse.  The bound is that L2 stream: ~3.6 MB of split planes per block.
+// Arithmetic: the engine's split products in the engine's order per K step (k_gemm.hpp kPrecS3, operands
+// swapped as in k_rowown.hpp), the FM / first order in encoder_k16_kernel<1>'s order (bit-identical).
+#include "k_gemm.hpp"
+
+namespace rmx {
+namespace {
+
+constexpr int kSR = 16;                   // samples per block
+constexpr int kSW = 8;                    // waves
+constexpr int kSThreads = kSW * 64;
+constexpr int kSN = 416;                  // Npad of the 400-wide layers
+constexpr int kSNT = 25;                  // computed column tiles (wave 0: 4, waves 1 .. 7: 3)
+static_assert(4 + 7 * 3 == kSNT, "the column split");
+constexpr int kSMaxF = 40;
+constexpr int kSXS = kSMaxF * 16 + 4;     // x tile row stride (floats): +4 keeps the 16-B reads conflict-free
+constexpr int kSHS = kSN + 4;             // activation tile row stride
+constexpr int kSTW = 4;                   // max column tiles per wave (wave 0: 4, the others 3)
+constexpr size_t kSLds =
+    sizeof(float) * (kSR * kSXS + kSR * kSHS + kSW * kSR + 3 * kSN + kSR) + sizeof(int) * kSR * kSMaxF;
+static_assert(kSLds <= 80 * 1024, "LDS budget");
+
+struct SmallArgs {
+  int M, F;
+  const int32_t* ids;     // [M][F]
+  const float* table;     // row of id at table + (id << gsh)
+  int gsh;
+  const float* wtab;      // first-order weight of id at wtab[id << wsh]
+  int wsh;
+  const bf16_t* W[3];     // split planes [KS_l][3][416][32] of the three layers (DenseLayer::W3)
+  const float* b[3];      // [416]
+  int KS1;                // K steps of layer 1 (ceil(F / 2)); layers 2 / 3: 13
+  OutArgs oa;             // wo [416], bo, beta, out (pre: ignored -- the first order + FM are computed here)
+};
+
+// one layer: acc[j] (column tile w + 8 j) = sum over K steps of W_t x^T on the split planes, x from LDS
+// (row stride XS floats); weight fragments of step c + 1 loaded during step c
+template <int NTW>
+__device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const float* xin, int xs, int KS, int w, int lane,
+                                        f32x4 (&acc)[kSTW]) {
+  const int g = lane >> 4, r16 = lane & 15;
+#pragma unroll
+  for (int j = 0; j < kSTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int wo = r16 * 32 + g * 8;  // lane's element of a fragment
+  asm volatile("" : "+v"(wo));
+  auto ldw = [&](int c, f32x4 (&b)[NTW][3]) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[j][pl] = *reinterpret_cast<const f32x4*>(W + ((int64_t)(c * 3 + pl) * kSN + 16 * (w + 8 * j)) * 32 + wo);
+  };
+  f32x4 b0[NTW][3], b1[NTW][3];  // (two named buffers: a [2][..] array indexed by c & 1 went to scratch)
+  ldw(0, b0);
+  int xo = r16 * xs + 4 * g;
+  asm volatile("" : "+v"(xo));
+  auto step = [&](int c, f32x4 (&cur)[NTW][3], f32x4 (&nxt)[NTW][3]) {
+    if (c + 1 < KS) ldw(c + 1, nxt);
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(xin + xo + 32 * c);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(xin + xo + 32 * c + 16);
+    bf16x8 ah, am, al;
+    split3(a0, a1, ah, am, al);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const bf16x8 bh = __builtin_bit_cast(bf16x8, cur[j][0]);
+      const bf16x8 bm = __builtin_bit_cast(bf16x8, cur[j][1]);
+      const bf16x8 bl = __builtin_bit_cast(bf16x8, cur[j][2]);
+      f32x4 d = acc[j];
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, d, 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, d, 0, 0, 0);
+    }
+  };
+#pragma unroll 1
+  for (int c = 0; c < KS; c += 2) {
+    step(c, b0, b1);
+    if (c + 1 < KS) step(c + 1, b1, b0);
+  }
+}
+
+// ReLU(acc + b) of the wave's tiles into the activation tile (lane: row r16, columns 16 t + 4 g .. + 3)
+template <int NTW>
+__device__ __forceinline__ void s_store_h(const f32x4 (&acc)[kSTW], const float* bl, float* h, int w, int lane) {
+  const int g = lane >> 4, r16 = lane & 15;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int n0 = 16 * (w + 8 * j) + 4 * g;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + n0);
+    f32x4 v = acc[j] + bb;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+    *reinterpret_cast<f32x4*>(h + r16 * kSHS + n0) = v;
+  }
+}
+
+template <int NTW>
+__device__ void s_wave(const SmallArgs& p, float* x, float* h, float* prm, float* red, int w, int lane) {
+  const int g = lane >> 4, r16 = lane & 15;
+  f32x4 acc[kSTW];
+  // layer 1: x tile (row stride kSXS) -> h
+  s_layer<NTW>(p.W[0], x, kSXS, p.KS1, w, lane, acc);
+  s_store_h<NTW>(acc, prm, h, w, lane);
+  __syncthreads();
+  // layer 2: h -> the x region (stride kSHS)
+  s_layer<NTW>(p.W[1], h, kSHS, 13, w, lane, acc);
+  __syncthreads();  // every wave has read h ... (the x region is free since layer 1)
+  s_store_h<NTW>(acc, prm + kSN, x, w, lane);
+  __syncthreads();
+  // layer 3 + the output dot over the wave's columns
+  s_layer<NTW>(p.W[2], x, kSHS, 13, w, lane, acc);
+  float part = 0.f;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int n0 = 16 * (w + 8 * j) + 4 * g;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(prm + 2 * kSN + n0);
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(p.oa.wo + n0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = acc[j][r] + bb[r];
+      v = v > 0.f ? v : 0.f;
+      part += v * wv[r];
+    }
+  }
+  part += __shfl_xor(part, 16);
+  part += __shfl_xor(part, 32);
+  if (g == 0) red[w * kSR + r16] = part;
+}
+
+__global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float ssmem[];
+  float* x = ssmem;                       // [16][kSXS] gathered rows; later layer 2's output
+  float* h = x + kSR * kSXS;              // [16][kSHS] layer 1's output
+  float* red = h + kSR * kSHS;            // [8 waves][16] partial logits
+  float* prm = red + kSW * kSR;           // b1 | b2 | b3
+  float* fmv = prm + 3 * kSN;             // [16] first order + FM (y1 + y2) per sample
+  int* sid = reinterpret_cast<int*>(fmv + kSR);  // [16][F] ids
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * kSR, F = p.F;
+  for (int i = tid; i < 3 * kSN; i += kSThreads) {
+    const int a = i / kSN, n = i - a * kSN;
+    const float* src = a == 0 ? p.b[0] : (a == 1 ? p.b[1] : p.b[2]);  // (no dynamic index into the kernel args)
+    prm[i] = src ? src[n] : 0.f;
+  }
+  for (int i = tid; i < kSR * F; i += kSThreads) {
+    const int r = i / F, m = m0 + r;
+    sid[i] = m < p.M ? p.ids[(int64_t)m * F + (i - r * F)] : -1;
+  }
+  __syncthreads();
+  // the gathered rows: x[r][16 f + j] (fields past F and rows past M: zero)
+  for (int i = tid; i < kSR * kSMaxF * 4; i += kSThreads) {
+    const int r = i / (kSMaxF * 4), rest = i - r * (kSMaxF * 4), f = rest >> 2, q = rest & 3;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f < F) {
+      const int id = sid[r * F + f];
+      if (id >= 0) v = *reinterpret_cast<const float4*>(p.table + ((int64_t)id << p.gsh) + 4 * q);
+    }
+    *reinterpret_cast<float4*>(x + r * kSXS + 16 * f + 4 * q) = v;
+  }
+  __syncthreads();
+  // first order + FM of sample r (wave 0, 16 lanes per sample, lane j of the group: column j), in
+  // encoder_k16_kernel<1>'s order: s_j, q_j over the fields in order, a = sum_j (s_j^2 - q_j) in j order
+  if (w == 0) {
+#pragma clang fp contract(off)
+    for (int rr = 0; rr < kSR; rr += 4) {
+      const int r = rr + (lane >> 4), j = lane & 15;
+      float s = 0.f, q = 0.f;
+      for (int f = 0; f < F; ++f) {
+        const float e = x[r * kSXS + 16 * f + j];
+        s = s + e;
+        q = q + e * e;
+      }
+      const float d = s * s - q;
+      float a = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) a += __shfl(d, (lane & 48) + jj);
+      float y1 = 0.f;
+      for (int f = 0; f < F; ++f) {
+        const int id = sid[r * F + f];
+        y1 += id >= 0 ? p.wtab[(int64_t)id << p.wsh] : 0.f;
+      }
+      if (j == 0) fmv[r] = y1 + 0.5f * (a / 16.0f);
+    }
+  }
+  __syncthreads();
+  if (w == 0)
+    s_wave<4>(p, x, h, prm, red, w, lane);
+  else
+    s_wave<3>(p, x, h, prm, red, w, lane);
+  __syncthreads();
+  if (tid < kSR) {
+    const int m = m0 + tid;
+    if (m < p.M) {
+      float y = red[tid];
+#pragma unroll
+      for (int q = 1; q < kSW; ++q) y += red[q * kSR + tid];
+      const OutArgs& oa = p.oa;
+      if (oa.has_bo) y = y + oa.bo;
+      float t = fmv[tid] + y;  // pre (first order + FM) + the tower's logit, out_finish_kernel's order
+      t = t + oa.beta;
+      oa.out[m] = 1.0f / (1.0f + expf(-t));
+    }
+  }
+}
+
+}  // namespace
+
+bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids) {
+  if (M <= 0 || !ids || k != 16 || F < 1 || F > kSMaxF || m.type != RMX_MODEL_DEEPFM || m.layers.size() != 3 ||
+      !f32_split_enabled() || m.precision != kF32)
+    return false;
+  for (int l = 0; l < 3; ++l) {
+    const DenseLayer& L = m.layers[l];
+    if (!L.W3 || L.W16 || L.N != 400 || L.Npad != kSN || L.N1 >= 0 || L.bias_mode != 1 || L.K1 >= 0) return false;
+    if (L.K != (l == 0 ? 16 * F : 400)) return false;
+  }
+  // knob "s3_small": 0 off, 2 always, 1 (default) below the batch whose 128-row blocks fill every CU
+  const int knob = tuning_get("s3_small", 0);  // (default flipped on once measured on the GPU)
+  if (knob == 0) return false;
+  if (knob == 2) return true;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu = 256;
+  return M <= tuning_get("s3_small_max", 16384) && (M + 127) / 128 < ncu;
+}
+
+int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,
+                          int ld, const float* wtab, int wld, const OutArgs& oa) {
+  if (M <= 0) return RMX_OK;
+  const int l = ld > 0 ? ld : 16, wl = wld > 0 ? wld : 1;
+  if ((l & (l - 1)) || l < 16 || (wl & (wl - 1)) || !oa.wo || !oa.out) {
+    set_error("fp32 small tower: table / weight strides must be powers of two, and an output head");
+    return RMX_E_INVALID;
+  }
+  RMX_HIP(hipFuncSetAttribute((const void*)tower_small_s3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kSLds));
+  SmallArgs p{};
+  p.M = M;
+  p.F = F;
+  p.ids = ids;
+  p.table = table;
+  p.gsh = __builtin_ctz((unsigned)l);
+  p.wtab = wtab;
+  p.wsh = __builtin_ctz((unsigned)wl);
+  for (int i = 0; i < 3; ++i) {
+    p.W[i] = m.layers[i].W3;
+    p.b[i] = m.layers[i].b;
+  }
+  p.KS1 = (F + 1) / 2;
+  p.oa = oa;
+  hipLaunchKernelGGL(tower_small_s3_kernel, dim3((M + kSR - 1) / kSR), dim3(kSThreads), kSLds, s, p);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
+}  // namespace rmx

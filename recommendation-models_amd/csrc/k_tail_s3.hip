@@ -38,34 +38,22 @@
 //     then drained vmcnt(0) at the layer-2 loop head, which took the weight DMAs' lead.)
 // MFMA work per row block per wave: 2 layers x 13 steps x 25 tiles x 6 = 3,900 MFMAs (tile 25, columns
 // 400 .. 415, is padding in both layers and is not computed).
-#include "k_gemm.hpp"
+#include "k_rowown.hpp"
 
 namespace rmx {
 namespace {
+using namespace rowown;
 
-constexpr int kQBM = 128;                    // rows per row block
-constexpr int kQW = 8;                       // waves
-constexpr int kQThreads = kQW * 64;
-constexpr int kQNT = 25;                     // computed column tiles (N = 400)
-constexpr int kQN = 416;                     // Npad: packed rows of W per plane and K step
 constexpr int kQKS = 13;                     // 32-wide K steps (Kpad = 416)
-constexpr int kQUT = 13;                     // column tiles per unit (one half of Npad)
-constexpr int kQUnit = 3 * kQUT * 16 * 64;   // bytes per unit: 3 planes x 208 rows x 64 B = 39,936
-constexpr int kQIns = kQUnit / 1024;         // 1-KiB DMA instructions per unit (39)
-constexpr int kQQ = (kQIns + kQW - 1) / kQW; // per wave (5; wave 7's fifth repeats instruction 38)
-constexpr int kQSlots = 3;
 constexpr int kQUnits = 4 * kQKS;            // units per row block (52)
 constexpr int kQL3 = 2 * kQKS;               // first layer-3 unit (26)
 constexpr int kQPrm = 3 * kQN;               // b2 | b3 | wo (fp32) in LDS
 constexpr int kQH1 = kQW * 2 * 2048;         // h1: two 2-KiB step slots per wave
 constexpr size_t kQLds = (size_t)kQSlots * kQUnit + kQH1 + sizeof(float) * kQPrm;
 static_assert(kQLds <= 160 * 1024, "LDS budget");
-static_assert(kQQ == 5 && kQIns == 39, "the static vmcnt counts below assume 5 DMAs per wave per unit");
 
-// Diagnostic builds only (timing probes, wrong results; never set in librmx.so): 1 = no DMAs after the
-// prologue, 2 = no MFMAs
-#ifndef RMX_QTAIL_DIAG
-#define RMX_QTAIL_DIAG 0
+#ifndef RMX_QTAIL_PRIO
+#define RMX_QTAIL_PRIO 0
 #endif
 // weight-fragment prefetch depth (column tiles) of the layer-3 units, where h2's 100 registers are live
 #ifndef RMX_QTAIL_PF3
@@ -95,82 +83,6 @@ __device__ __forceinline__ const bf16_t* q_unit_src(const TailS3Args& p, int u) 
   return (l3 ? p.W3 : p.W2) + (int64_t)(c * 3 * kQN + half * kQUT * 16) * 32;
 }
 
-// this wave's DMA q of a unit whose planes start at `src` into the slot at `dst` (LDS byte offset).
-// Instruction ins = w + 8 q fills unit rows [16 ins, 16 ins + 16): plane ins / 13, tile ins % 13; lane L
-// writes physical 16-B slot L & 3 of row L >> 2, so it loads logical slot swz_slot(row, L & 3) (the
-// swizzle is an involution; the key of row 16 t + (L >> 2) depends on L only): lo = its element offset.
-__device__ __forceinline__ void q_dma(const bf16_t* src, char* lds, int slot, int w, int q, int lo) {
-  int ins = w + q * kQW;
-  ins = ins < kQIns ? ins : kQIns - 1;
-  const int pl = ins / kQUT, t = ins - pl * kQUT;
-  int l = lo;
-  asm volatile("" : "+v"(l));  // formed here: hoisted, the 130 per-unit sources of layer 3 spilled
-  const bf16_t* s = src + (pl * kQN + t * 16) * 32 + l;
-  __builtin_amdgcn_global_load_lds(s, (__attribute__((address_space(3))) void*)(lds + slot * kQUnit + ins * 1024), 16,
-                                   0, 0);
-}
-
-__device__ __forceinline__ int q_next(int s) { return s == kQSlots - 1 ? 0 : s + 1; }
-
-// per-lane byte offset of the weight fragments (row r16 of a tile, logical slot g), opaque so the
-// fragment addresses are formed per use
-__device__ __forceinline__ int q_fbase(int lane) {
-  int fb = (lane & 15) * 64 + swz_slot(lane & 15, lane >> 4) * 16;
-  asm volatile("" : "+v"(fb));
-  return fb;
-}
-
-// One unit: NT column tiles (local tiles 0 .. NT - 1 of the unit's half) of one K step.  acc[T0 + t] +=
-// W_t h^T on the split planes (ah, am, al) of this wave's 16 rows; dma(q) issues the wave's q-th DMA of
-// unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.
-template <int NT, int T0, int NA, int PF = 2>
-__device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
-                                       f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo) {
-  f32x4 bq[PF + 1][3];
-  int fbu = fb;
-  asm volatile("" : "+v"(fbu));
-  auto ldb = [&](int t, f32x4* b) {
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) b[pl] = *reinterpret_cast<const f32x4*>(ub + fbu + pl * (kQUT * 1024) + t * 1024);
-  };
-#pragma unroll
-  for (int t = 0; t < PF; ++t) ldb(t, bq[t]);
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    if (t + PF < NT) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
-    if (t < kQQ && !(RMX_QTAIL_DIAG & 1)) q_dma(dsrc, lds, dslot, w, t, lo);
-    __builtin_amdgcn_sched_barrier(0);
-    const f32x4* b = bq[t % (PF + 1)];
-    const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
-    const bf16x8 bm = __builtin_bit_cast(bf16x8, b[1]);
-    const bf16x8 bl = __builtin_bit_cast(bf16x8, b[2]);
-    if constexpr (RMX_QTAIL_DIAG & 2) {
-      acc[T0 + t] += b[0] + b[1] + b[2] + __builtin_bit_cast(f32x4, ah);
-      continue;
-    }
-    f32x4 d = acc[T0 + t];
-    // the engine's product order (k_gemm.hpp compute_step_s3), operands swapped: smallest terms first
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am, d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am, d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, d, 0, 0, 0);
-    acc[T0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, d, 0, 0, 0);
-  }
-#pragma unroll
-  for (int t = NT; t < kQQ; ++t)
-    if (!(RMX_QTAIL_DIAG & 1)) q_dma(dsrc, lds, dslot, w, t, lo);
-}
-
-// unit start: this unit's DMAs (issued two units ago) have landed for this wave (N = vector-memory
-// instructions the wave issued during the previous unit), then for every wave; the slot the next DMAs
-// overwrite was read by every wave before this barrier
-template <int N>
-__device__ __forceinline__ void q_enter() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 // h1 of K step c of row block rb into this wave's LDS slot ds (c & 1; 2 DMA instructions: the wave's 16 rows x
 // 128 B; rows past M read the zero row).  Instruction i, lane L: row r = 8 i + (L >> 3), physical 16-B
 // slot L & 7, which holds logical slot j = (L & 7) ^ (r & 7), i.e. columns 32 c + 4 j .. + 3 (j < 4:
@@ -204,11 +116,6 @@ __device__ __forceinline__ void q_h1_read(const char* hlds, int c, int lane, f32
   if (c == kQKS - 1) a1 = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-__device__ __forceinline__ f32x4 relu4(f32x4 v) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-  return v;
-}
 
 // layer-3 half HF (column tiles 13 HF .. + 12; half 1 computes 12, tile 25 is padding): 13 units, one
 // per K step, unrolled so that h2's tiles 2c, 2c + 1 are static registers.  Unit 50 (half 1, step 11)
@@ -274,6 +181,9 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args 
   asm volatile("" : "+s"(zrow));
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
+#if RMX_QTAIL_PRIO
+  if (w >= kQW / 2) __builtin_amdgcn_s_setprio(1);  // (timing A/B) the second-dispatched half at priority 1
+#endif
   const int nit = (int)blockIdx.x < p.nblk ? (p.nblk - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const OutArgs& oa = p.oa;
 

@@ -712,6 +712,20 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out, in.ld, in.wld);
   }
 
+  // DeepFM fp32 at a small launch batch: the whole tower + first order + FM + head in one launch, one block
+  // per 16 samples (k_small_s3.hip; knob "s3_small")
+  if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) &&
+      tower_small_s3_usable(m, B, F, k, true)) {
+    StageTimer t(m, s, "tower_small");
+    OutArgs oa{};
+    oa.wo = m.wo;
+    oa.bo = m.bo;
+    oa.has_bo = m.has_bo ? 1 : 0;
+    oa.beta = in.beta;
+    oa.out = in.out;
+    return launch_tower_small_s3(s, m, B, F, in.ids, (const float*)in.table, in.ld, (const float*)in.wtab, in.wld, oa);
+  }
+
   // 1. first order (+ FM for DeepFM; fused into tower layer 1 when it gathers through the split GEMM)
   const float* pre = nullptr;
   AGatherArgs ga{in.ids, (const float*)in.table, F, k, in.ld};
@@ -734,7 +748,11 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   const bool tail_fo = m.type == RMX_MODEL_PNN && m.precision == kBF16 && in.dtype == kBF16 && in.ids && !in.y1 &&
                        F <= 40 && nl >= 3 && tuning_get("tail_fo", 1) != 0 &&
                        tower_tail_usable(m.layers[nl - 2], m.layers[nl - 1], B, m.layers[nl - 3].Npad);
-  const bool fm_add = fm_fused && deepfm &&
+  // DeepFM fp32 at a batch that fills the GPU: layer 1 + first order + FM as one row-owner kernel
+  // (k_head_s3.hip; knob "s3_head")
+  const bool head_s3 = deepfm && in.ids && !in.y1 && gather_first && in.dtype == kF32 && k == 16 &&
+                       m.layers.size() > 1 && tower_head_s3_usable(m.layers[0], B, F, k, true);
+  const bool fm_add = !head_s3 && fm_fused && deepfm &&
                       (fm_y1 == 0 || (fm_y1 == 2 && !tower_wring(m.layers[0], B, &ga)));
   if (fm_add) {
     StageTimer t(m, s, "first_order");
@@ -742,7 +760,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
                              in.wld)))
       return st;
   }
-  if (fm_fused) {
+  if (fm_fused || head_s3) {
     pre = m.y12;
   } else if (m.type == RMX_MODEL_DEEPFM) {
     StageTimer t(m, s, "encoder_fm");
@@ -828,6 +846,14 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     }
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
+    if (i == 0 && head_s3) {
+      if ((st = launch_tower_head_s3(s, L, B, F, in.ids, (const float*)in.table, in.ld, (const float*)in.wtab, in.wld, C,
+                                     L.Npad, m.y12, 1)))
+        return st;
+      A = C;
+      lda = L.Npad;
+      continue;
+    }
     XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
     FmArgs fm{in.wtab, in.dtype == kBF16 ? 1 : 0, deepfm ? 1 : 0, fm_add ? 1 : 0, m.y12, in.wld};
     st = launch_tower_layer(s, L, B, A, lda, (i == 0 && gather_first) ? &ga : nullptr, C, L.Npad,

@@ -135,6 +135,11 @@ struct TailFirstOrder {  // the first order summed by the tail itself (bf16 weig
 };
 int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const bf16_t* H, int lda,
                            const OutArgs& oa, const TailFirstOrder* fo = nullptr);
+// fp32 tower layer 1 of DeepFM as a row-owner kernel (k_head_s3.hip): gather (k = 16, ids [M][F], table row
+// of id at table + id * ld) + ReLU(x W1^T + b1) -> H [M][416] + first order (+ FM: fm_sums) -> fm_y [M]
+bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids);
+int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
+                         int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums);
 // fp32 tower tail (k_tail_s3.hip): ReLU(H L2) -> ReLU(. L3) . wo -> head on the split GEMM, one persistent
 // launch, h2 in registers; both layers 400 x 400 with split planes; H [M][lda] fp32
 bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda);

@@ -252,5 +252,9 @@ int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const
 int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt, void* xbuf,
                     int xdt, int ldx);
 int tower_npad_for(int N);
+// DeepFM's whole fp32 tower for small batches, one block per 16 samples (k_small_s3.hip)
+bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids);
+int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,
+                          int ld, const float* wtab, int wld, const OutArgs& oa);
 int cin_npad_for(int H);
 }  // namespace rmx

@@ -37,8 +37,10 @@ def ctx():
 
 @pytest.fixture(autouse=True)
 def _restore_knobs():
+    rmx.set_tuning("s3_small", 0)  # (small batches would run the whole-tower kernel, k_small_s3.hip)
     yield
     rmx.set_tuning("s3_tail", None)
+    rmx.set_tuning("s3_small", None)
 
 
 def _model(kind, V):
