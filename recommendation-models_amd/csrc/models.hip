@@ -752,6 +752,11 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // (k_head_s3.hip; knob "s3_head")
   const bool head_s3 = deepfm && in.ids && !in.y1 && gather_first && in.dtype == kF32 && k == 16 &&
                        m.layers.size() > 1 && tower_head_s3_usable(m.layers[0], B, F, k, true);
+  // bf16 towers with a gathered k = 16 layer 1 (DCN: the cross dots ride as raw columns): the row-owner
+  // layer 1 (k_head_bf16.hip; knob "bf16_head")
+  const bool head_bf16 = !deepfm && m.type != RMX_MODEL_PNN && m.type != RMX_MODEL_XDEEPFM && in.ids && !in.y1 &&
+                         gather_first && in.dtype == kBF16 && m.precision == kBF16 && k == 16 && m.layers.size() > 1 &&
+                         tower_head_bf16_usable(m.layers[0], B, F, k, true);
   const bool fm_add = !head_s3 && fm_fused && deepfm &&
                       (fm_y1 == 0 || (fm_y1 == 2 && !tower_wring(m.layers[0], B, &ga)));
   if (fm_add) {
@@ -846,6 +851,17 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     }
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
+    if (i == 0 && head_bf16) {
+      XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
+      if ((st = launch_tower_head_bf16(s, L, B, F, in.ids, (const bf16_t*)in.table, in.ld, (const bf16_t*)in.wtab,
+                                       in.wld, reinterpret_cast<bf16_t*>(C), L.Npad, m.dcn_fused ? &xc : nullptr,
+                                       fm_fused ? m.y12 : nullptr)))
+        return st;
+      if (m.dcn_fused && (st = launch_cross_finish(s, B, m.cross_depth, m.xcol, m.cross_scalars, m.pre2))) return st;
+      A = C;
+      lda = L.Npad;
+      continue;
+    }
     if (i == 0 && head_s3) {
       if ((st = launch_tower_head_s3(s, L, B, F, in.ids, (const float*)in.table, in.ld, (const float*)in.wtab, in.wld, C,
                                      L.Npad, m.y12, 1)))
