@@ -456,6 +456,7 @@ void model_release(rmx_model& m) {
   dev_free(m.cross_b);
   dev_free(m.wo_x);
   dev_free(m.pairs);
+  pnn_head_release(m.pnn);
   dev_free(m.h[0]);
   dev_free(m.h[1]);
   dev_free(m.y12);
@@ -495,6 +496,7 @@ static int copy_slice(hipStream_t s, const float* src, int n, int npad, float* d
 int model_set_precision(rmx_model& m, int dtype) {
   RMX_HIP(hipSetDevice(m.ctx->device));
   RMX_HIP(hipStreamSynchronize(m.ctx->stream));
+  pnn_head_release(m.pnn);
   for (auto& L : m.layers) {
     dev_free(L.W);
     dev_free(L.W16);
@@ -536,6 +538,10 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
     if (L.W3 && (st = launch_pack_split3(s, L.W, L.Kpad / kChunk, L.Npad, L.W3))) return st;
     if (L.WT && (st = launch_pack_linear_t(s, m.mats_dev, L))) return st;
   }
+  // PNN bf16 at k = 16: layer 1's weights in the on-chip-product kernel's K order (k_pnn_head.hip)
+  if (m.type == RMX_MODEL_PNN && m.precision == kBF16 && m.k == 16 && m.layers.size() > 1 &&
+      (st = pnn_head_prepare(s, m.mats_dev, m.layers[0], m.F, m.pnn)))
+    return st;
   if (!m.layers.empty()) {
     const auto& last = m.layers.back();
     if ((st = copy_slice(s, m.mats_dev + m.wo_off, last.N, last.Npad, m.wo))) return st;
@@ -792,6 +798,9 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   oa.part = m.opart;
   const float* A = nullptr;
   int lda = 0;
+  size_t i0 = 0;  // first tower layer the loop below runs
+  const bool pnn_head = m.type == RMX_MODEL_PNN && in.ids && !in.y1 && in.dtype == kBF16 && m.precision == kBF16 &&
+                        m.layers.size() > 1 && pnn_head_usable(m.pnn, m.layers[0], B, F, k, true);
 
   if (m.type == RMX_MODEL_XDEEPFM) {
     const float* uprev = nullptr;
@@ -814,6 +823,16 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
         return st;
     }
     oa.pre2 = m.pre2;
+  } else if (m.type == RMX_MODEL_PNN && pnn_head) {
+    // layer 1 with the products generated on chip: [x | ip] never reaches HBM (k_pnn_head.hip)
+    StageTimer t(m, s, "tower_layer1");
+    if ((st = launch_pnn_head(s, m.pnn, m.layers[0], B, F, in.ids, (const bf16_t*)in.table,
+                              reinterpret_cast<bf16_t*>(m.h[0]), m.layers[0].Npad)))
+      return st;
+    A = m.h[0];
+    lda = m.layers[0].Npad;
+    gather_first = false;
+    i0 = 1;
   } else if (m.type == RMX_MODEL_PNN) {
     StageTimer t(m, s, "product");
     if ((st = launch_product(s, B, F, k, in.ids, in.table, in.dtype, m.pairs, F * (F - 1) / 2, m.xbuf, m.precision,
@@ -833,7 +852,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
 
   // 3. tower (the last layer runs the output head: dot + bias + CAddTable + Sigmoid)
   static const char* names[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
-  for (size_t i = 0; i < m.layers.size(); ++i) {
+  for (size_t i = i0; i < m.layers.size(); ++i) {
     const bool last = i + 1 == m.layers.size();
     const DenseLayer& L = m.layers[i];
     // bf16: the last hidden layer and the output layer in one persistent kernel (k_tail.hip)

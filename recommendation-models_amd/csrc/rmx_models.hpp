@@ -108,6 +108,7 @@ struct rmx_model {
   rmx::CrossScalars cross_scalars{};
   float* xcol = nullptr;                    // [B][L + 1] raw fused cross dots
   int32_t* pairs = nullptr;                 // PNN (row, col) pairs [P][2]
+  rmx::PnnHead pnn;                         // PNN bf16: layer 1 with on-chip products (k_pnn_head.hip)
   int precision = 0;                        // kF32 / kBF16 (rmx_model_set_precision)
   bool params_ready = false;
   float beta = 0.f;
