@@ -64,8 +64,7 @@ __device__ __forceinline__ void p_wdma(const bf16_t* src, char* lds, int slot, i
   int lo = (threadIdx.x & 63) >> 2;  // row of the tile; physical slot lane & 3 holds logical swz_slot(row, .)
   lo = lo * 32 + swz_slot(lo, threadIdx.x & 3) * 8;
   asm volatile("" : "+v"(lo));
-  __builtin_amdgcn_global_load_lds(src + ins * 16 * 32 + lo,
-                                   (__attribute__((address_space(3))) void*)(lds + slot * kPUnit + ins * 1024), 16, 0, 0);
+  lds_dma<16>(src + ins * 16 * 32 + lo, lds + slot * kPUnit + ins * 1024);
 }
 
 // ids of pair c (fields 2c, 2c + 1) of row block rb into id slot c & 3 (lanes 0 .. 31: field 2c + (L >> 4),
@@ -76,9 +75,7 @@ __device__ __forceinline__ void p_id_dma(const PnnArgs& p, char* wl, int rb, int
   const int m = rb * kPBM + w * 16 + s, fld = 2 * c + f;
   const bool ok = rb < p.nblk && m < p.M && fld < p.F;
   const int32_t* src = ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1;
-  if (lane < 32)
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wl + kPRows + (c & 3) * 128), 4, 0,
-                                     0);
+  if (lane < 32) lds_dma<4>(src, wl + kPRows + (c & 3) * 128);
 }
 
 // rows of pair c from the ids in slot c & 3: lane L = field 2c + (L >> 5), half (L >> 4) & 1, sample L & 15
@@ -89,7 +86,7 @@ __device__ __forceinline__ void p_row_dma(const PnnArgs& p, char* wl, int c, int
   asm volatile("" : "+v"(f), "+v"(h), "+v"(s));
   const int id = ids[f * 16 + s];
   const void* src = id >= 0 ? (const void*)(p.table + ((int64_t)id << 4) + 8 * h) : (const void*)g_rmx_zero16;
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wl + c * 1024), 16, 0, 0);
+  lds_dma<16>(src, wl + c * 1024);
 }
 
 // the prologue's rows of pair c of row block rb, ids read straight from HBM
@@ -98,7 +95,7 @@ __device__ __forceinline__ void p_row_direct(const PnnArgs& p, char* wl, int rb,
   const int m = rb * kPBM + w * 16 + s, fld = 2 * c + f;
   const int id = (rb < p.nblk && m < p.M && fld < p.F) ? p.ids[(int64_t)m * p.F + fld] : -1;
   const void* src = id >= 0 ? (const void*)(p.table + ((int64_t)id << 4) + 8 * h) : (const void*)g_rmx_zero16;
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wl + c * 1024), 16, 0, 0);
+  lds_dma<16>(src, wl + c * 1024);
 }
 
 template <int N>
@@ -135,8 +132,9 @@ __device__ __forceinline__ int p_sld(const int32_t* base, int i) {
 
 // One unit t of a row block.  The B fragment is x (pair t of the image) for t < KSX, else the ip fragment
 // computed by the previous unit; when unit t + 1 is an ip unit its fragment is computed here on the side
-// (quads from p.quads).  One loop runs every unit (runtime flags, uniform branches): two loops over the
-// two kinds made the compiler copy the 104 accumulators at every back edge.
+// (quads from p.quads).  One loop runs every unit, the ip work under uniform per-tile branches: two loops
+// over the two kinds, or the two kinds as two bodies under one branch, made the compiler copy the 104
+// accumulators between VGPRs and AGPRs every unit.
 __device__ __forceinline__ void p_unit(const PnnArgs& p, char* smem, char* wl, const char* rl, int t, int rb, int rbn,
                                        int& slot, int fb, int lane, int w, f32x4 (&acc)[kPNT], bf16x8& ipf) {
   p_enter<kPQ>();  // all but this wave's last 7 DMAs (the previous unit's weights) have landed
@@ -149,10 +147,14 @@ __device__ __forceinline__ void p_unit(const PnnArgs& p, char* smem, char* wl, c
   const int rp = sc & 127, ipr = (sc >> 8) & 127;
   if (rp != kNone) p_row_dma(p, wl, rp, lane);
   if (ipr != kNone) p_id_dma(p, wl, (sc >> 15) & 1 ? rbn : rb, ipr, w, lane);
-  __builtin_amdgcn_sched_barrier(0);
+  // this unit's weight DMAs (unit t + 2) all here, ahead of the fragment reads: interleaved with them, each
+  // LDS DMA made the compiler drain lgkmcnt -- the prefetched fragments -- before the next MFMA
   const int ds = slot == 0 ? 2 : slot - 1;  // (slot + 2) mod 3
   const int tn = t + 2 < p.KS ? t + 2 : t + 2 - p.KS;
   const bf16_t* src = p.W + (int64_t)tn * kQN * 32;
+#pragma unroll
+  for (int q = 0; q < kPQ; ++q) p_wdma(src, smem, ds, w, q);
+  __builtin_amdgcn_sched_barrier(0);
   const char* ub = smem + slot * kPUnit;
   int fbu = fb;
   asm volatile("" : "+v"(fbu));
@@ -186,7 +188,6 @@ __device__ __forceinline__ void p_unit(const PnnArgs& p, char* smem, char* wl, c
 #pragma unroll
   for (int tt = 0; tt < kPNT; ++tt) {
     if (tt + PF < kPNT) bq[(tt + PF) % (PF + 1)] = *reinterpret_cast<const f32x4*>(ub + fbu + (tt + PF) * 1024);
-    if (tt % 4 == 0 && tt / 4 < kPQ) p_wdma(src, smem, ds, w, tt / 4);
     // pair e: rows read at tile 3 e, dot at tile 3 e + 2; row i of quad u at tiles 0 / 12 (quad 1's row
     // replaces quad 0's after pair 3's dot at tile 11)
     if (ipn) {
@@ -217,16 +218,8 @@ __global__ __launch_bounds__(kPThreads, 1) void pnn_head_kernel(PnnArgs p) {
   const char* rl = wl + r16 * 16;  // this lane's sample in the row image
   const int nit = (int)blockIdx.x < p.nblk ? (p.nblk - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int fb = q_fbase(lane);
-  // bias of this lane's columns n = 16 t + 4 g .. + 3, in registers (zero past N1)
-  f32x4 bias[kPNT];
-#pragma unroll
-  for (int t = 0; t < kPNT; ++t) {
-    const int n0 = 16 * t + 4 * g;
-    f32x4 v = *reinterpret_cast<const f32x4*>(p.b + n0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = n0 + r < p.N1 ? v[r] : 0.f;
-    bias[t] = v;
-  }
+  // PNN's layer-1 bias is one scalar broadcast over the N1 columns (CAdd(1): bias_mode 2)
+  const float b0 = __int_as_float(p_sld(reinterpret_cast<const int32_t*>(p.b), 0));
   if (nit > 0) {
     for (int c = 0; c < p.KSX; ++c) {
       const int a = p_sld(p.pro, c);
@@ -259,7 +252,10 @@ __global__ __launch_bounds__(kPThreads, 1) void pnn_head_kernel(PnnArgs p) {
       for (int t = 0; t < kPNT; ++t) {
         int n0 = 16 * t + 4 * g;
         asm volatile("" : "+v"(n0));
-        *reinterpret_cast<bf16x4*>(hrow + n0) = __builtin_convertvector(relu4(acc[t] + bias[t]), bf16x4);
+        f32x4 v = acc[t];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = n0 + r < p.N1 && v[r] + b0 > 0.f ? v[r] + b0 : 0.f;
+        *reinterpret_cast<bf16x4*>(hrow + n0) = __builtin_convertvector(v, bf16x4);
       }
     }
   }

@@ -55,6 +55,24 @@ __device__ __forceinline__ void q_dma(const bf16_t* src, char* lds, int slot, in
                                    0, 0);
 }
 
+// LDS DMA (global_load_lds, `BYTES` per lane; lane L lands at dst + BYTES * L) issued through inline asm.
+// With the builtin the compiler counts the DMA as an LGKM event of unknown order, so every later wait for
+// an LDS read becomes lgkmcnt(0) and drains the prefetched fragments (checked on gfx950 ISA); hidden in
+// asm, the reads keep their counted waits.  The kernels that use it order the DMAs themselves (explicit
+// vmcnt waits + barriers), issue no compiler-visible vector-memory loads in their loops, and keep no value
+// in M0 (every DMA sets it).
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)dst));
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(a), "v"(src) : "memory");
+  else if constexpr (BYTES == 4)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(a), "v"(src) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off" ::"s"(a), "v"(src) : "memory");
+}
+
 __device__ __forceinline__ int q_next(int s) { return s == kQSlots - 1 ? 0 : s + 1; }
 
 // per-lane byte offset of the weight fragments (row r16 of a tile, logical slot g), opaque so the
