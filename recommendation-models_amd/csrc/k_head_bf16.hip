@@ -58,8 +58,7 @@ __device__ __forceinline__ void b_wdma(const bf16_t* src, char* lds, int slot, i
   int lo = (threadIdx.x & 63) >> 2;  // row of the tile; physical slot lane & 3 -> logical swz_slot(row, .)
   lo = lo * 32 + swz_slot(lo, threadIdx.x & 3) * 8;
   asm volatile("" : "+v"(lo));
-  __builtin_amdgcn_global_load_lds(src + ins * 16 * 32 + lo,
-                                   (__attribute__((address_space(3))) void*)(lds + slot * kBUnit + ins * 1024), 16, 0, 0);
+  lds_dma<16>(src + ins * 16 * 32 + lo, lds + slot * kBUnit + ins * 1024);
 }
 
 // ids of K step c of row block rb into id slot `slot` (lanes 0 .. 31: field 2c + (L >> 4) of sample L & 15)
@@ -70,7 +69,7 @@ __device__ __forceinline__ void b_id_dma(const HeadBArgs& p, char* wl, int rb, i
   const bool ok = rb < p.nblk && m < p.M && fld < p.F;
   const int32_t* src = ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1;
   if (lane < 32)
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wl + kBA + slot * 128), 4, 0, 0);
+    lds_dma<4>(src, wl + kBA + slot * 128);
 }
 
 // rows of the wave's step s (one DMA: lane L = field L >> 5, sample (L >> 1) & 15, half L & 1 of the
@@ -82,10 +81,9 @@ __device__ __forceinline__ void b_row_dma(const HeadBArgs& p, char* wl, int s, i
   const int id = ids[f * 16 + r], idw = ids[lw];
   const void* src = id >= 0 ? (const void*)(p.table + ((int64_t)id << p.gsh) + 8 * hf) : (const void*)g_rmx_zero16;
   const void* sw = idw >= 0 ? (const void*)(p.wtab + ((int64_t)idw << p.wsh)) : (const void*)g_rmx_zero16;
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wl + (s & 3) * 1024), 16, 0, 0);
+  lds_dma<16>(src, wl + (s & 3) * 1024);
   if (lane < 32)
-    __builtin_amdgcn_global_load_lds(sw, (__attribute__((address_space(3))) void*)(wl + kBA + kBId + (s & 3) * 128), 2,
-                                     0, 0);
+    lds_dma<2>(sw, wl + kBA + kBId + (s & 3) * 128);
 }
 
 template <int N>

@@ -62,7 +62,7 @@ __device__ __forceinline__ void h_id_dma(const HeadS3Args& p, char* wl, int rb, 
   const bool ok = rb < p.nblk && m < p.M && fld < p.F;
   const int32_t* src = ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1;
   if (lane < 32)
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wl + kHA + slot * 128), 4, 0, 0);
+    lds_dma<4>(src, wl + kHA + slot * 128);
 }
 
 // rows (2 DMAs: field f = instruction, lane L: sample L >> 2, physical 16-B slot L & 3 = logical slot
@@ -78,11 +78,10 @@ __device__ __forceinline__ void h_row_dma(const HeadS3Args& p, char* wl, int s, 
   const float* s1 = id1 >= 0 ? p.table + ((int64_t)id1 << p.gsh) + 4 * g : zero16;
   const float* sw = idw >= 0 ? p.wtab + ((int64_t)idw << p.wsh) : zero16;
   char* a = wl + (s & 1) * 2048;
-  __builtin_amdgcn_global_load_lds(s0, (__attribute__((address_space(3))) void*)a, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds(s1, (__attribute__((address_space(3))) void*)(a + 1024), 16, 0, 0);
+  lds_dma<16>(s0, a);
+  lds_dma<16>(s1, a + 1024);
   if (lane < 32)
-    __builtin_amdgcn_global_load_lds(sw, (__attribute__((address_space(3))) void*)(wl + kHA + kHId + (s & 1) * 128), 4,
-                                     0, 0);
+    lds_dma<4>(sw, wl + kHA + kHId + (s & 1) * 128);
 }
 
 __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args p) {

@@ -40,21 +40,6 @@ static_assert(kQQ == 5 && kQIns == 39, "the static vmcnt counts assume 5 weight 
 #define RMX_QTAIL_DSTRIDE 1
 #endif
 
-// this wave's DMA q of a unit whose planes start at `src` into the slot at `dst` (LDS byte offset).
-// Instruction ins = w + 8 q fills unit rows [16 ins, 16 ins + 16): plane ins / 13, tile ins % 13; lane L
-// writes physical 16-B slot L & 3 of row L >> 2, so it loads logical slot swz_slot(row, L & 3) (the
-// swizzle is an involution; the key of row 16 t + (L >> 2) depends on L only): lo = its element offset.
-__device__ __forceinline__ void q_dma(const bf16_t* src, char* lds, int slot, int w, int q, int lo) {
-  int ins = w + q * kQW;
-  ins = ins < kQIns ? ins : kQIns - 1;
-  const int pl = ins / kQUT, t = ins - pl * kQUT;
-  int l = lo;
-  asm volatile("" : "+v"(l));  // formed here: hoisted, the 130 per-unit sources of layer 3 spilled
-  const bf16_t* s = src + (pl * kQN + t * 16) * 32 + l;
-  __builtin_amdgcn_global_load_lds(s, (__attribute__((address_space(3))) void*)(lds + slot * kQUnit + ins * 1024), 16,
-                                   0, 0);
-}
-
 // LDS DMA (global_load_lds, `BYTES` per lane; lane L lands at dst + BYTES * L) issued through inline asm.
 // With the builtin the compiler counts the DMA as an LGKM event of unknown order, so every later wait for
 // an LDS read becomes lgkmcnt(0) and drains the prefetched fragments (checked on gfx950 ISA); hidden in
@@ -71,6 +56,20 @@ __device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(a), "v"(src) : "memory");
   else
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off" ::"s"(a), "v"(src) : "memory");
+}
+
+// this wave's DMA q of a unit whose planes start at `src` into the slot at `dst` (LDS byte offset).
+// Instruction ins = w + 8 q fills unit rows [16 ins, 16 ins + 16): plane ins / 13, tile ins % 13; lane L
+// writes physical 16-B slot L & 3 of row L >> 2, so it loads logical slot swz_slot(row, L & 3) (the
+// swizzle is an involution; the key of row 16 t + (L >> 2) depends on L only): lo = its element offset.
+__device__ __forceinline__ void q_dma(const bf16_t* src, char* lds, int slot, int w, int q, int lo) {
+  int ins = w + q * kQW;
+  ins = ins < kQIns ? ins : kQIns - 1;
+  const int pl = ins / kQUT, t = ins - pl * kQUT;
+  int l = lo;
+  asm volatile("" : "+v"(l));  // formed here: hoisted, the 130 per-unit sources of layer 3 spilled
+  const bf16_t* s = src + (pl * kQN + t * 16) * 32 + l;
+  lds_dma<16>(s, lds + slot * kQUnit + ins * 1024);
 }
 
 __device__ __forceinline__ int q_next(int s) { return s == kQSlots - 1 ? 0 : s + 1; }

@@ -100,9 +100,7 @@ __device__ __forceinline__ void q_h1_dma(const TailS3Args& p, const float* zrow,
     const uint32_t ok = (rb < p.nblk && m < p.M) ? 1u : 0u;
     const uintptr_t base = (uintptr_t)zrow + (uintptr_t)ok * ((uintptr_t)p.H - (uintptr_t)zrow);
     const float* row = reinterpret_cast<const float*>(base) + (uint32_t)(m * (int)ok) * (uint32_t)p.lda;
-    __builtin_amdgcn_global_load_lds(row + 32 * c + 4 * j,
-                                     (__attribute__((address_space(3))) void*)(hlds + ds * 2048 + i * 1024), 16, 0,
-                                     0);
+    lds_dma<16>(row + 32 * c + 4 * j, hlds + ds * 2048 + i * 1024);
   }
 }
 // the h1 fragment of step c from the wave's slot: a0 = columns 32 c + 4 g .., a1 = 32 c + 16 + 4 g ..
