@@ -62,13 +62,15 @@ __device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
 // Instruction ins = w + 8 q fills unit rows [16 ins, 16 ins + 16): plane ins / 13, tile ins % 13; lane L
 // writes physical 16-B slot L & 3 of row L >> 2, so it loads logical slot swz_slot(row, L & 3) (the
 // swizzle is an involution; the key of row 16 t + (L >> 2) depends on L only): lo = its element offset.
+// (PS: rows of W per plane and K step -- 416 for the tower layers, 208 for the CIN's)
+template <int PS = kQN>
 __device__ __forceinline__ void q_dma(const bf16_t* src, char* lds, int slot, int w, int q, int lo) {
   int ins = w + q * kQW;
   ins = ins < kQIns ? ins : kQIns - 1;
   const int pl = ins / kQUT, t = ins - pl * kQUT;
   int l = lo;
   asm volatile("" : "+v"(l));  // formed here: hoisted, the 130 per-unit sources of layer 3 spilled
-  const bf16_t* s = src + (pl * kQN + t * 16) * 32 + l;
+  const bf16_t* s = src + (pl * PS + t * 16) * 32 + l;
   lds_dma<16>(s, lds + slot * kQUnit + ins * 1024);
 }
 
@@ -85,7 +87,7 @@ __device__ __forceinline__ int q_fbase(int lane) {
 // One unit: NT column tiles (local tiles 0 .. NT - 1 of the unit's half) of one K step.  acc[T0 + t] +=
 // W_t h^T on the split planes (ah, am, al) of this wave's 16 rows; dma(q) issues the wave's q-th DMA of
 // unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.
-template <int NT, int T0, int NA, int PF = 2>
+template <int NT, int T0, int NA, int PF = 2, int PS = kQN>
 __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                        f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo) {
   f32x4 bq[PF + 1][3];
@@ -104,7 +106,7 @@ __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah,
     constexpr int kD0 = RMX_QTAIL_DOFF, kDS = RMX_QTAIL_DSTRIDE;
     static_assert(kD0 + (kQQ - 1) * kDS < kQUT - 1, "every unit (12 or 13 tiles) carries all its DMAs");
     if (t >= kD0 && (t - kD0) % kDS == 0 && (t - kD0) / kDS < kQQ && !(RMX_QTAIL_DIAG & 1))
-      q_dma(dsrc, lds, dslot, w, (t - kD0) / kDS, lo);
+      q_dma<PS>(dsrc, lds, dslot, w, (t - kD0) / kDS, lo);
     __builtin_amdgcn_sched_barrier(0);
     const f32x4* b = bq[t % (PF + 1)];
     const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);

@@ -457,6 +457,7 @@ void model_release(rmx_model& m) {
   dev_free(m.wo_x);
   dev_free(m.pairs);
   pnn_head_release(m.pnn);
+  cin_row_release(m.cinrow);
   dev_free(m.h[0]);
   dev_free(m.h[1]);
   dev_free(m.y12);
@@ -558,6 +559,8 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
     if ((st = copy_slice(s, m.mats_dev + c.b_off, c.H, c.Npad, c.b))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.wo_off, c.H, c.Npad, c.wo))) return st;
   }
+  // xDeepFM fp32: the CIN stack's weights for the row-owner kernel (k_cin_row.hip)
+  if (!m.cin_layers.empty() && m.precision == kF32 && (st = cin_row_prepare(s, m.mats_dev, m, m.cinrow))) return st;
   if (m.type == RMX_MODEL_DCN) {
     const int D = m.F * m.k;
     if (m.cross_depth <= kMaxFusedCross) {
@@ -802,7 +805,12 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   const bool pnn_head = m.type == RMX_MODEL_PNN && in.ids && !in.y1 && in.dtype == kBF16 && m.precision == kBF16 &&
                         m.layers.size() > 1 && pnn_head_usable(m.pnn, m.layers[0], B, F, k, true);
 
-  if (m.type == RMX_MODEL_XDEEPFM) {
+  if (m.type == RMX_MODEL_XDEEPFM && in.dtype == kF32 && cin_row_usable(m.cinrow, m, B, in.ids != nullptr)) {
+    StageTimer t(m, s, "cin");
+    if ((st = launch_cin_row(s, m.cinrow, m, B, in.ids, (const float*)in.table, m.rowdot))) return st;
+    oa.rowsum = m.rowdot;
+    oa.rowsum_k = k;
+  } else if (m.type == RMX_MODEL_XDEEPFM) {
     const float* uprev = nullptr;
     for (size_t l = 0; l < m.cin_layers.size(); ++l) {
       StageTimer t(m, s, l == 0 ? "cin_layer1" : (l == 1 ? "cin_layer2" : "cin_layer3+"));
