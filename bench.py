@@ -47,7 +47,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 PEAK_S3_TFLOPS = PEAK_BF16_TFLOPS / 6
 # stages whose GEMMs run on the split (f32_split on): priced against its peak.  The backward stages
 # (dW and dX on the split; the CIN backward's rocBLAS part is fp32) take the higher peak too.
-S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "cin_layer", "tower_back", "cin_back")
+S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "cin", "tower_back")
 
 
 def parse():
@@ -136,6 +136,9 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * (k1 * FC[0] + FC[0] * FC[1] + FC[1] * FC[2] + FC[2])
     if stage == "tower_tail":  # layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip, k_tail_s3.hip)
         return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
+    if stage == "cin":  # the whole CIN stack in one launch (csrc/k_cin_row.hip)
+        hps = [F] + CIN[:-1]
+        return "flop", sum(2.0 * B * K * F * hp * h for hp, h in zip(hps, CIN))
     if stage.startswith("cin_layer"):
         idx = {"cin_layer1": 0, "cin_layer2": 1, "cin_layer3+": 2}[stage]
         hp = F if idx == 0 else CIN[idx - 1]
@@ -580,7 +583,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     roof["traffic"] = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
-        ent = json.load(open(tpath)).get(workload, {}).get(dom if not dom.startswith("cin") else "cin_layer")
+        ent = json.load(open(tpath)).get(workload, {}).get("cin_layer" if dom.startswith("cin_layer") else dom)
         if ent and ent.get("batch") == B:
             roof["traffic"] = ent["hbm_bytes"]
             roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
