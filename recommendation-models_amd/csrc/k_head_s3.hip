@@ -34,7 +34,8 @@ constexpr size_t kHLds = (size_t)kQSlots * kQUnit + (size_t)kQW * kHWave + sizeo
 static_assert(kHLds <= 160 * 1024, "LDS budget");
 
 struct HeadS3Args {
-  int M, nblk, F, KS;     // KS = ceil(F / 2) K steps
+  int M, F, KS;           // KS = ceil(F / 2) K steps
+  QRows rows;             // full / half row blocks (k_rowown.hpp)
   const int32_t* ids;     // [M][F]
   const float* table;     // row of id at table + (id << gsh) (16 fp32: k = 16)
   int gsh;
@@ -53,13 +54,14 @@ __device__ __forceinline__ const bf16_t* h_unit_src(const HeadS3Args& p, int u) 
   return p.W + (int64_t)(c * 3 * kQN + half * kQUT * 16) * 32;
 }
 
-// ids of K step c of row block rb into id slot `slot` (lanes 0 .. 31: field 2c + (L >> 4) of sample L & 15;
-// past M or F, or past the last row block: -1)
-__device__ __forceinline__ void h_id_dma(const HeadS3Args& p, char* wl, int rb, int c, int slot, int w, int lane) {
+// ids of K step c of the row block at row0 (nw waves own rows) into id slot `slot` (lanes 0 .. 31: field
+// 2c + (L >> 4) of sample L & 15; past M or F, or for a wave without rows: -1)
+__device__ __forceinline__ void h_id_dma(const HeadS3Args& p, char* wl, int row0, int nw, int c, int slot, int w,
+                                         int lane) {
   int f = lane >> 4, r = lane & 15;
   asm volatile("" : "+v"(f), "+v"(r));
-  const int m = rb * kQBM + w * 16 + r, fld = 2 * c + f;
-  const bool ok = rb < p.nblk && m < p.M && fld < p.F;
+  const int m = row0 + w * 16 + r, fld = 2 * c + f;
+  const bool ok = w < nw && m < p.M && fld < p.F;
   const int32_t* src = ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1;
   if (lane < 32)
     lds_dma<4>(src, wl + kHA + slot * 128);
@@ -91,7 +93,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
   const int g = lane >> 4, r16 = lane & 15;
   char* wl = hsmem + kQSlots * kQUnit + w * kHWave;  // this wave's rows / ids / weights
   float* bl = reinterpret_cast<float*>(hsmem + kQSlots * kQUnit + kQW * kHWave);
-  const int nit = (int)blockIdx.x < p.nblk ? (p.nblk - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nit = p.rows.nit(blockIdx.x);
   const int KS = p.KS, NU = 2 * KS;  // units per row block
 
   for (int i = tid; i < kQN; i += kQThreads) bl[i] = p.b ? p.b[i] : 0.f;
@@ -103,8 +105,9 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
   // blockIdx.x + (s / KS) gridDim.x (none past the last); its ring slots are s & 3 (ids) and s & 1
   auto id_dma = [&](int s) {
     const int it = s / KS, c = s - it * KS;
-    const int rb = it < nit ? (int)blockIdx.x + it * (int)gridDim.x : p.nblk;
-    h_id_dma(p, wl, rb, c, s & 3, w, lane);
+    int row0, nw;
+    p.rows.desc(blockIdx.x, it, row0, nw);
+    h_id_dma(p, wl, row0, nw, c, s & 3, w, lane);
   };
   if (nit > 0) {
     for (int s = 0; s < 3; ++s) id_dma(s);
@@ -122,7 +125,28 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
 
   int slot = 0, s = 0;
   for (int it = 0; it < nit; ++it) {
-    const int rb = blockIdx.x + it * gridDim.x;
+    int row0, nw;
+    p.rows.desc(blockIdx.x, it, row0, nw);
+    if (w >= nw) {
+      // a half block's waves 4 .. 7: the same units, barriers and DMAs (ids of no rows), no MFMAs -- one
+      // branch per row block (per-unit branches spilled the accumulators)
+#pragma unroll 1
+      for (int c = 0; c < KS; ++c, ++s) {
+        q_enter<5>();
+        id_dma(s + 3);
+        h_row_dma(p, wl, s + 1, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        const int u = 2 * c;
+        int dslot = slot == 0 ? 2 : slot - 1;
+        q_dma_only(h_unit_src(p, u + 2 < NU ? u + 2 : u + 2 - NU), lds, dslot, w, lo);
+        slot = q_next(slot);
+        q_enter<9>();
+        dslot = slot == 0 ? 2 : slot - 1;
+        q_dma_only(h_unit_src(p, u + 3 < NU ? u + 3 : u + 3 - NU), lds, dslot, w, lo);
+        slot = q_next(slot);
+      }
+      continue;
+    }
     f32x4 acc[kQNT];
 #pragma unroll
     for (int t = 0; t < kQNT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -166,7 +190,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
     }
     __builtin_amdgcn_sched_barrier(0);
     // epilogue: h1 = ReLU(acc + b1) to HBM (columns 400 .. 415 zero), fm_y
-    const int m = rb * kQBM + w * 16 + r16;
+    const int m = row0 + w * 16 + r16;
     int g4 = 4 * g;
     asm volatile("" : "+v"(g4));
     if (m < p.M) {
@@ -199,7 +223,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
 bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids) {
   if (M <= 0 || !ids || k != 16 || F < 1 || F > kHMaxF || !L1.W3 || L1.W16 || !f32_split_enabled()) return false;
   if (!(L1.K == 16 * F && L1.N == 400 && L1.Npad == kQN && L1.N1 < 0 && L1.bias_mode == 1 && L1.K1 < 0)) return false;
-  // knob "s3_head": 0 off, 2 always, 1 (default) when the row blocks fill every CU at least once
+  // knob "s3_head": 0 off, 2 always, 1 when the (half) row blocks fill every CU at least once
   const int knob = tuning_get("s3_head", 0);  // (default flipped on once measured on the GPU)
   if (knob == 0) return false;
   if (knob == 2) return true;
@@ -207,7 +231,7 @@ bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return (M + kQBM - 1) / kQBM >= ncu;
+  return (M + kQBM / 2 - 1) / (kQBM / 2) >= ncu;  // (half blocks: k_rowown.hpp QRows)
 }
 
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
@@ -229,7 +253,8 @@ int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, cons
                               (int)kHLds));
   HeadS3Args p{};
   p.M = M;
-  p.nblk = (M + kQBM - 1) / kQBM;
+  int grid = 0;
+  p.rows = q_rows(M, ncu, grid);
   p.F = F;
   p.KS = (F + 1) / 2;
   p.ids = ids;
@@ -242,7 +267,6 @@ int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, cons
   p.H = H;
   p.fm_y = fm_y;
   p.fm_sums = fm_sums;
-  const int grid = std::min(p.nblk, std::max(ncu, 1));
   hipLaunchKernelGGL(tower_head_s3_kernel, dim3(grid), dim3(kQThreads), kHLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;

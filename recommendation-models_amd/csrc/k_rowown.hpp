@@ -48,8 +48,9 @@ static_assert(kQQ == 5 && kQIns == 39, "the static vmcnt counts assume 5 weight 
 // in M0 (every DMA sets it).
 template <int BYTES>
 __device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
-  const unsigned a = __builtin_amdgcn_readfirstlane(
-      (unsigned)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)dst));
+  // (the low 32 bits of a generic pointer into LDS are the LDS address; the address-space cast's null
+  // check tripped an instruction-selection bug, "V_CMP_NE_U32 ... src_shared_base")
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(dst));
   if constexpr (BYTES == 16)
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(a), "v"(src) : "memory");
   else if constexpr (BYTES == 4)
@@ -89,7 +90,8 @@ __device__ __forceinline__ int q_fbase(int lane) {
 // unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.
 template <int NT, int T0, int NA, int PF = 2, int PS = kQN>
 __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
-                                       f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo) {
+                                       f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo,
+                                       bool mm = true) {
   f32x4 bq[PF + 1][3];
   int fbu = fb;
   asm volatile("" : "+v"(fbu));
@@ -116,6 +118,7 @@ __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah,
       acc[T0 + t] += b[0] + b[1] + b[2] + __builtin_bit_cast(f32x4, ah);
       continue;
     }
+    if (!mm) continue;  // a wave without rows this row block (QRows half blocks): DMAs only
     f32x4 d = acc[T0 + t];
     // the engine's product order (k_gemm.hpp compute_step_s3), operands swapped: smallest terms first
     d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am, d, 0, 0, 0);
@@ -125,6 +128,56 @@ __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah,
     d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, d, 0, 0, 0);
     acc[T0 + t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, d, 0, 0, 0);
   }
+}
+
+// the DMAs of q_unit without its MFMAs: a wave that owns no rows this row block (a half block's waves
+// 4 .. 7) keeps the ring and the static vmcnt counts
+template <int PS = kQN>
+__device__ __forceinline__ void q_dma_only(const bf16_t* dsrc, char* lds, int dslot, int w, int lo) {
+#pragma unroll
+  for (int q = 0; q < kQQ; ++q) q_dma<PS>(dsrc, lds, dslot, w, q, lo);
+}
+
+// Row blocks of a persistent row-owner launch (grid G): full 128-row blocks, round-robin.  When the last
+// round would leave at least half the CUs idle, its rows go out as 64-row half blocks instead: waves 0 .. 3
+// own the rows, waves 4 .. 7 keep the weight ring and the barriers but run no MFMAs, so the round costs
+// about half a round (B = 49,152 on 256 CUs: 1.5 rounds instead of 2; B = 16,384: half a round, not one).
+struct QRows {
+  int M, G, nfull, nhalf;  // nfull full blocks, then nhalf half blocks from row nfull * 128
+  __device__ __forceinline__ int nf(int b) const { return b < nfull ? (nfull - 1 - b) / G + 1 : 0; }
+  __device__ __forceinline__ int nit(int b) const { return nf(b) + (b < nhalf ? 1 : 0); }
+  // iteration it of block b: first row and the number of waves that own rows (0: none -- past the end)
+  __device__ __forceinline__ void desc(int b, int it, int& row0, int& nw) const {
+    const int n = nf(b);
+    if (it < n) {
+      row0 = (b + it * G) * kQBM;
+      nw = kQW;
+    } else if (it == n && b < nhalf) {
+      row0 = nfull * kQBM + b * (kQBM / 2);
+      nw = kQW / 2;
+    } else {
+      row0 = M;
+      nw = 0;
+    }
+  }
+};
+
+// host: the row blocks of M rows on ncu CUs and the grid that runs them (knob "half_blocks", default 1)
+inline QRows q_rows(int M, int ncu, int& grid) {
+  QRows r{M, 1, 0, 0};
+  const int nb = (M + kQBM - 1) / kQBM;
+  ncu = ncu > 0 ? ncu : 1;
+  const int R = (nb + ncu - 1) / ncu, last = nb - (R - 1) * ncu;
+  if (tuning_get("half_blocks", 1) != 0 && 2 * last <= ncu) {
+    r.nfull = (R - 1) * ncu;
+    r.nhalf = (M - r.nfull * kQBM + kQBM / 2 - 1) / (kQBM / 2);
+    grid = r.nfull > 0 ? ncu : (r.nhalf < ncu ? r.nhalf : ncu);
+  } else {
+    r.nfull = nb;
+    grid = nb < ncu ? nb : ncu;
+  }
+  r.G = grid;
+  return r;
 }
 
 // unit start: this unit's DMAs (issued two units ago) have landed for this wave (N = vector-memory

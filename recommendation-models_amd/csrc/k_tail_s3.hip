@@ -64,7 +64,8 @@ static_assert(kQLds <= 160 * 1024, "LDS budget");
 __device__ __attribute__((aligned(16))) float g_qzero_row[kQN];
 
 struct TailS3Args {
-  int M, nblk;
+  int M;
+  QRows rows;  // full / half row blocks (k_rowown.hpp)
   const float* H;  // layer input [M][lda] fp32 (columns >= 400 read as zero)
   int lda;
   const bf16_t* W2;  // [13][3][416][32] bf16 planes (DenseLayer::W3)
@@ -88,16 +89,16 @@ __device__ __forceinline__ const bf16_t* q_unit_src(const TailS3Args& p, int u) 
 // slot L & 7, which holds logical slot j = (L & 7) ^ (r & 7), i.e. columns 32 c + 4 j .. + 3 (j < 4:
 // the fragment's a0 part, j >= 4: a1).  Only the issuing wave reads these rows: its own vmcnt orders
 // them, no barrier.
-__device__ __forceinline__ void q_h1_dma(const TailS3Args& p, const float* zrow, char* hlds, int rb, int c, int ds,
-                                         int w, int lane) {
+__device__ __forceinline__ void q_h1_dma(const TailS3Args& p, const float* zrow, char* hlds, int row0, int nw, int c,
+                                         int ds, int w, int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     int r = 8 * i + (lane >> 3), j = (lane & 7) ^ ((lane >> 3) & 7);
     asm volatile("" : "+v"(r), "+v"(j));  // formed here (not hoisted)
     // branch-free (an exec-masked address branch split the unit into basic blocks): rows past M
     // read the zero row at the same column offset (M * lda < 2^31: launch check)
-    const int m = rb * kQBM + w * 16 + r;
-    const uint32_t ok = (rb < p.nblk && m < p.M) ? 1u : 0u;
+    const int m = row0 + w * 16 + r;
+    const uint32_t ok = (w < nw && m < p.M) ? 1u : 0u;
     const uintptr_t base = (uintptr_t)zrow + (uintptr_t)ok * ((uintptr_t)p.H - (uintptr_t)zrow);
     const float* row = reinterpret_cast<const float*>(base) + (uint32_t)(m * (int)ok) * (uint32_t)p.lda;
     lds_dma<16>(row + 32 * c + 4 * j, hlds + ds * 2048 + i * 1024);
@@ -120,7 +121,7 @@ __device__ __forceinline__ void q_h1_read(const char* hlds, int c, int lane, f32
 // also loads the next row block's h1 step 0.
 template <int HF>
 __device__ __forceinline__ void q_layer3(const TailS3Args& p, char* lds, const float* prm, f32x4 (&h2)[kQNT], int& slot,
-                                         int w, int lane, int lo, int fb, const float* zrow, char* hlds, int rb_next,
+                                         int w, int lane, int lo, int fb, const float* zrow, char* hlds, int it,
                                          float& part) {
   const int g = lane >> 4;
   f32x4 acc[kQUT];
@@ -138,7 +139,9 @@ __device__ __forceinline__ void q_layer3(const TailS3Args& p, char* lds, const f
     const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
     split3(h2[2 * c], 2 * c + 1 < kQNT ? h2[2 * c + 1] : z, ah, am, al);
     if (u == kQUnits - 2) {  // the next row block's step 0 (two units ahead of its first use)
-      q_h1_dma(p, zrow, hlds, rb_next, 0, 0, w, lane);
+      int row0n, nwn;  // the next row block's (formed here: live across layer 3 it spilled)
+      p.rows.desc(blockIdx.x, it + 1, row0n, nwn);
+      q_h1_dma(p, zrow, hlds, row0n, nwn, 0, 0, w, lane);
       __builtin_amdgcn_sched_barrier(0);
     }
     const int u2 = u + 2 >= kQUnits ? u + 2 - kQUnits : u + 2;
@@ -171,6 +174,43 @@ __device__ __forceinline__ void q_layer3(const TailS3Args& p, char* lds, const f
   asm volatile("" : "+v"(part));
 }
 
+// A row block without MFMAs, for a wave that owns no rows in it (QRows half blocks): the same 52 units,
+// barriers and vector-memory instructions as the computing waves (h1 loads of zero rows included), so
+// the ring and every static vmcnt count stay in step.
+__device__ __forceinline__ void q_idle_block(const TailS3Args& p, char* lds, int& slot, int w, int lane, int lo,
+                                             const float* zrow, char* hlds, int it, int row0, int nw) {
+#pragma unroll 1
+  for (int c = 0; c < kQKS; ++c) {
+    q_enter<5>();
+    q_h1_dma(p, zrow, hlds, row0, nw, c + 1 < kQKS ? c + 1 : c, (c + 1) & 1, w, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    int dslot = slot == 0 ? 2 : slot - 1;
+    q_dma_only(q_unit_src(p, 2 * c + 2), lds, dslot, w, lo);
+    slot = q_next(slot);
+    q_enter<7>();
+    dslot = slot == 0 ? 2 : slot - 1;
+    q_dma_only(q_unit_src(p, 2 * c + 3), lds, dslot, w, lo);
+    slot = q_next(slot);
+  }
+#pragma unroll 1
+  for (int u = kQL3; u < kQUnits; ++u) {
+    if (u == kQUnits - 1)
+      q_enter<7>();
+    else
+      q_enter<5>();
+    if (u == kQUnits - 2) {
+      int row0n, nwn;
+      p.rows.desc(blockIdx.x, it + 1, row0n, nwn);
+      q_h1_dma(p, zrow, hlds, row0n, nwn, 0, 0, w, lane);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int u2 = u + 2 >= kQUnits ? u + 2 - kQUnits : u + 2;
+    const int dslot = slot == 0 ? 2 : slot - 1;
+    q_dma_only(q_unit_src(p, u2), lds, dslot, w, lo);
+    slot = q_next(slot);
+  }
+}
+
 __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args p) {
   extern __shared__ __attribute__((aligned(16))) char qsmem[];
   char* lds = qsmem;
@@ -182,7 +222,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args 
 #if RMX_QTAIL_PRIO
   if (w >= kQW / 2) __builtin_amdgcn_s_setprio(1);  // (timing A/B) the second-dispatched half at priority 1
 #endif
-  const int nit = (int)blockIdx.x < p.nblk ? (p.nblk - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int nit = p.rows.nit(blockIdx.x);
   const OutArgs& oa = p.oa;
 
   for (int i = tid; i < kQPrm; i += kQThreads) {
@@ -196,7 +236,11 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args 
   const int fb = q_fbase(lane);
 
   char* hlds = qsmem + kQSlots * kQUnit + w * 4096;  // this wave's h1 step slots
-  q_h1_dma(p, zrow, hlds, blockIdx.x, 0, 0, w, lane);
+  {
+    int row0, nw;
+    p.rows.desc(blockIdx.x, 0, row0, nw);
+    q_h1_dma(p, zrow, hlds, row0, nw, 0, 0, w, lane);
+  }
   if (nit > 0) {
     const bf16_t* s0 = q_unit_src(p, 0);
     const bf16_t* s1 = q_unit_src(p, 1);
@@ -210,7 +254,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args 
 
   int slot = 0;
   for (int it = 0; it < nit; ++it) {
-    const int rb = blockIdx.x + it * gridDim.x;
+    int row0, nw;
+    p.rows.desc(blockIdx.x, it, row0, nw);
+    if (w >= nw) {  // a half block's waves 4 .. 7: the ring only (one branch per row block: per-unit
+      q_idle_block(p, lds, slot, w, lane, lo, zrow, hlds, it, row0, nw);  // branches spilled)
+      continue;
+    }
     // ---- layer 2: units (c, half 0), (c, half 1) ----
     f32x4 h2[kQNT];
 #pragma unroll
@@ -226,7 +275,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args 
       }
       // the next step's h1 (two units ahead of its use; at c = 12 a harmless reload of step 12 into slot 1,
       // which is next written by the next row block's step 1)
-      q_h1_dma(p, zrow, hlds, rb, c + 1 < kQKS ? c + 1 : c, (c + 1) & 1, w, lane);
+      q_h1_dma(p, zrow, hlds, row0, nw, c + 1 < kQKS ? c + 1 : c, (c + 1) & 1, w, lane);
       __builtin_amdgcn_sched_barrier(0);  // the h1 loads ahead of this unit's DMAs (the static vmcnt counts)
       const int u = 2 * c;
       int dslot = slot == 0 ? 2 : slot - 1;
@@ -248,12 +297,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_tail_s3_kernel(TailS3Args 
     }
     // ---- layer 3 + the output dot ----
     float part = 0.f;
-    q_layer3<0>(p, lds, prm, h2, slot, w, lane, lo, fb, zrow, hlds, rb + gridDim.x, part);
-    q_layer3<1>(p, lds, prm, h2, slot, w, lane, lo, fb, zrow, hlds, rb + gridDim.x, part);
+    q_layer3<0>(p, lds, prm, h2, slot, w, lane, lo, fb, zrow, hlds, it, part);
+    q_layer3<1>(p, lds, prm, h2, slot, w, lane, lo, fb, zrow, hlds, it, part);
     // ---- head: the four lane groups' columns, then bias, CAddTable, sigmoid (out_finish_kernel's order) ----
     part += __shfl_xor(part, 16);
     part += __shfl_xor(part, 32);
-    const int m = rb * kQBM + w * 16 + r16;
+    const int m = row0 + w * 16 + r16;
     if (g == 0 && m < p.M) {
       float y = part;
       if (oa.has_bo) y = y + oa.bo;
@@ -282,7 +331,7 @@ bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int
         (L2.Kpad + 31) / 32 == kQKS && (L3.Kpad + 31) / 32 == kQKS && L2.N1 < 0 && L3.N1 < 0 && L2.bias_mode == 1 && L3.bias_mode == 1 &&
         lda >= kQN && lda % 4 == 0))
     return false;
-  // knob "s3_tail": 0 off, 2 always, 1 (default) when the row blocks fill every CU at least once
+  // knob "s3_tail": 0 off, 2 always, 1 (default) when the (half) row blocks fill every CU at least once
   const int knob = tuning_get("s3_tail", 1);
   if (knob == 0) return false;
   if (knob == 2) return true;
@@ -290,7 +339,7 @@ bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return (M + kQBM - 1) / kQBM >= ncu;
+  return (M + kQBM / 2 - 1) / (kQBM / 2) >= ncu;  // (half blocks: k_rowown.hpp QRows)
 }
 
 int launch_tower_tail_s3(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const float* H, int lda,
@@ -312,7 +361,8 @@ int launch_tower_tail_s3(hipStream_t s, const DenseLayer& L2, const DenseLayer& 
                               (int)kQLds));
   TailS3Args p{};
   p.M = M;
-  p.nblk = (M + kQBM - 1) / kQBM;
+  int grid = 0;
+  p.rows = q_rows(M, ncu, grid);
   p.H = H;
   p.lda = lda;
   p.W2 = L2.W3;
@@ -320,7 +370,6 @@ int launch_tower_tail_s3(hipStream_t s, const DenseLayer& L2, const DenseLayer& 
   p.W3 = L3.W3;
   p.b3 = L3.b;
   p.oa = oa;
-  const int grid = std::min(p.nblk, std::max(ncu, 1));
   hipLaunchKernelGGL(tower_tail_s3_kernel, dim3(grid), dim3(kQThreads), kQLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;

@@ -32,7 +32,7 @@ def ctx():
 def _restore_knobs():
     rmx.set_tuning("s3_small", 0)  # (small batches would run the whole-tower kernel, k_small_s3.hip)
     yield
-    for k in ("s3_head", "s3_tail", "table_lines", "s3_small"):
+    for k in ("s3_head", "s3_tail", "table_lines", "s3_small", "half_blocks"):
         rmx.set_tuning(k, None)
 
 
@@ -97,3 +97,18 @@ def test_fp32_head_reads_line_tables_bitwise(ctx):
     a = _run(ctx, B, V, mats, heads=(2,), lines=0)[(2, 2)]
     b = _run(ctx, B, V, mats, heads=(2,), lines=1)[(2, 2)]
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("B", [16384, 40000, 49152])
+def test_fp32_head_half_blocks_bitwise(ctx, B):
+    """Half row blocks (k_rowown.hpp QRows, knob half_blocks) in the head: bitwise the full-block launch."""
+    V = 50000
+    mats = rmx.DeepFM(V, F, K, list(FC)).initMats(SEED_MATS)
+    res = {}
+    try:
+        for hb in (0, 1):
+            rmx.set_tuning("half_blocks", hb)
+            res[hb] = _run(ctx, B, V, mats, heads=(2,), tails=(2,))[(2, 2)]
+    finally:
+        rmx.set_tuning("half_blocks", None)
+    assert np.array_equal(res[0], res[1])

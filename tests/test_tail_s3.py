@@ -120,3 +120,39 @@ def test_fp32_tail_is_the_default_at_the_bench_batch(ctx):
     ctx.sync()
     stages, _ = m.get_timing()
     assert "tower_tail" in stages and "tower_layer2" not in stages, stages
+
+
+@pytest.mark.parametrize("B", [16384, 40000, 49152])
+def test_fp32_tail_half_blocks_bitwise(ctx, B):
+    """The last round of row blocks as 64-row half blocks (k_rowown.hpp QRows, knob half_blocks: waves 4 .. 7
+    keep the ring without MFMAs) computes every row with the same instructions: bitwise the full-block
+    launch, at B = 16,384 (all half), 40,000 (one full round + a partial half round) and 49,152 (one full
+    round + a full half round)."""
+    V = 50000
+    m = rmx.DeepFM(V, F, K, list(FC))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids_dev = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids_dev)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    res = {}
+    try:
+        rmx.set_tuning("s3_tail", 2)
+        for hb in (0, 1):
+            rmx.set_tuning("half_blocks", hb)
+            m.forward_ids(table, B, ids_dev, out)
+            ctx.sync()
+            res[hb] = out.numpy().copy()
+    finally:
+        rmx.set_tuning("half_blocks", None)
+    assert np.array_equal(res[0], res[1])
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    om = oc.make_model(oc.DEEPFM, F, K, fc=FC)
+    r0, n = B - 100, 100
+    ids = oc.gen_ids(SEED_IDS, r0, n, F, V).astype(np.int64)
+    w, e = oc.gather(wt, et, 1, ids)
+    ref = oc.forward(om, n, np.repeat(np.arange(n, dtype=np.int64), F), np.array([0.01], np.float32), w, e, mats, 1)
+    assert np.abs(res[1][r0:] - ref).max() <= TOL
