@@ -231,7 +231,7 @@ bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return (M + kQBM / 2 - 1) / (kQBM / 2) >= ncu;  // (half blocks: k_rowown.hpp QRows)
+  return q_fills(M, ncu);  // (with half blocks, k_rowown.hpp QRows, from M >= 64 ncu)
 }
 
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,

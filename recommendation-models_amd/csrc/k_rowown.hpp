@@ -162,13 +162,14 @@ struct QRows {
   }
 };
 
-// host: the row blocks of M rows on ncu CUs and the grid that runs them (knob "half_blocks", default 1)
+// host: the row blocks of M rows on ncu CUs and the grid that runs them (knob "half_blocks"; default 0
+// until measured on the GPU)
 inline QRows q_rows(int M, int ncu, int& grid) {
   QRows r{M, 1, 0, 0};
   const int nb = (M + kQBM - 1) / kQBM;
   ncu = ncu > 0 ? ncu : 1;
   const int R = (nb + ncu - 1) / ncu, last = nb - (R - 1) * ncu;
-  if (tuning_get("half_blocks", 1) != 0 && 2 * last <= ncu) {
+  if (tuning_get("half_blocks", 0) != 0 && 2 * last <= ncu) {
     r.nfull = (R - 1) * ncu;
     r.nhalf = (M - r.nfull * kQBM + kQBM / 2 - 1) / (kQBM / 2);
     grid = r.nfull > 0 ? ncu : (r.nhalf < ncu ? r.nhalf : ncu);
@@ -178,6 +179,13 @@ inline QRows q_rows(int M, int ncu, int& grid) {
   }
   r.G = grid;
   return r;
+}
+
+// host: whether the launch's (half) row blocks occupy every CU at least once
+inline bool q_fills(int M, int ncu) {
+  int grid = 0;
+  (void)q_rows(M, ncu, grid);
+  return grid >= ncu;
 }
 
 // unit start: this unit's DMAs (issued two units ago) have landed for this wave (N = vector-memory

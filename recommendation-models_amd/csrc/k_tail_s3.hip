@@ -339,7 +339,7 @@ bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return (M + kQBM / 2 - 1) / (kQBM / 2) >= ncu;  // (half blocks: k_rowown.hpp QRows)
+  return q_fills(M, ncu);  // (with half blocks, k_rowown.hpp QRows, from M >= 64 ncu)
 }
 
 int launch_tower_tail_s3(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const float* H, int lda,

@@ -106,7 +106,7 @@ def test_fp32_head_half_blocks_bitwise(ctx, B):
     mats = rmx.DeepFM(V, F, K, list(FC)).initMats(SEED_MATS)
     res = {}
     try:
-        for hb in (0, 1):
+        for hb in (0, 1):  # (knob 1 forces half blocks on)
             rmx.set_tuning("half_blocks", hb)
             res[hb] = _run(ctx, B, V, mats, heads=(2,), tails=(2,))[(2, 2)]
     finally:

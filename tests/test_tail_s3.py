@@ -141,7 +141,7 @@ def test_fp32_tail_half_blocks_bitwise(ctx, B):
     res = {}
     try:
         rmx.set_tuning("s3_tail", 2)
-        for hb in (0, 1):
+        for hb in (0, 1):  # (knob 1 forces half blocks on)
             rmx.set_tuning("half_blocks", hb)
             m.forward_ids(table, B, ids_dev, out)
             ctx.sync()
