@@ -86,7 +86,10 @@ def test_small_tower_first_order_and_fm_bitwise(ctx, B):
     assert np.array_equal(res[2], res[0])
 
 
-def test_small_tower_is_the_default_at_4096(ctx):
+def test_small_tower_auto_selection_at_4096(ctx):
+    """knob s3_small 1 (auto) takes the whole-tower kernel below the batch whose 128-row blocks fill every CU:
+    at B = 4,096 the forward is the one launch."""
+    rmx.set_tuning("s3_small", 1)
     B, V = 4096, 50000
     m = rmx.DeepFM(V, F, K, list(FC))
     m.setMats(m.initMats(SEED_MATS))
