@@ -333,8 +333,16 @@ int cin_row_prepare(hipStream_t s, const float* mats_dev, const rmx_model& m, Ci
 
 bool cin_row_usable(const CinRow& cr, const rmx_model& m, int B, bool ids) {
   if (B <= 0 || !ids || !cr.W || cr.L != (int)m.cin_layers.size() || m.k != 16 || !f32_split_enabled()) return false;
-  // knob "cin_row": 0 off, 1 on (default flipped on once measured on the GPU)
-  return tuning_get("cin_row", 0) != 0;
+  // knob "cin_row": 0 off, 2 always, 1 when the groups of 8 samples fill every CU at least once (default
+  // flipped on once measured on the GPU)
+  const int knob = tuning_get("cin_row", 0);
+  if (knob == 0) return false;
+  if (knob == 2) return true;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    ncu = 256;
+  return (B + kQW - 1) / kQW >= ncu;
 }
 
 int launch_cin_row(hipStream_t s, const CinRow& cr, const rmx_model& m, int B, const int32_t* ids, const float* table,
