@@ -239,6 +239,25 @@ struct EpiGeom {
   static constexpr int FLOATS = RW * LD * T::NW;
 };
 
+// LDS DMA (global_load_lds, `BYTES` per lane; lane L lands at dst + BYTES * L) issued through inline asm.
+// With the builtin the compiler counts the DMA as an LGKM event of unknown order, so every later wait for
+// an LDS read becomes lgkmcnt(0) and drains the prefetched fragments (checked on gfx950 ISA); hidden in
+// asm, the reads keep their counted waits.  The kernels that use it order the DMAs themselves (explicit
+// vmcnt waits + barriers), issue no compiler-visible vector-memory loads in their loops, and keep no value
+// in M0 (every DMA sets it).
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
+  // (the low 32 bits of a generic pointer into LDS are the LDS address; the address-space cast's null
+  // check tripped an instruction-selection bug, "V_CMP_NE_U32 ... src_shared_base")
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(dst));
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(a), "v"(src) : "memory");
+  else if constexpr (BYTES == 4)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(a), "v"(src) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off" ::"s"(a), "v"(src) : "memory");
+}
+
 // x (8 fp32 as two float4) = hi + mid + lo exactly, each a bf16x8 (kPrecS3)
 __device__ __forceinline__ void split3(const f32x4& x0, const f32x4& x1, bf16x8& hi, bf16x8& mi, bf16x8& lo) {
 #pragma unroll
@@ -802,7 +821,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                        : (const void*)(p.Wp + ((uint32_t)(c * p.Npad + n0 + n) * 16u + (uint32_t)(g * 4)));
             }
           }
-          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
+          lds_dma<16>(src, buf + ins * 256);
         }
       }
     };
@@ -859,7 +878,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
                 ((uint32_t)((cs * (S3 ? 3 : 1) + cc) * p.Npad + n0 + n) * 32u + (uint32_t)(g * 8));
           if ((q + 1) * NW > NINS) src = ins < NINS ? src : (const void*)zero16;  // padding instruction
         }
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + ins * 256), 16, 0, 0);
+        lds_dma<16>(src, buf + ins * 256);
       }
     };
     auto issue = [&](int c) {
@@ -877,8 +896,7 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       if (kQID * NW == 2 * BM / 64 || ins < 2 * BM / 64) {
         const int v = ins * 64 + lane, part = v / BM, r = v - part * BM, m = m0 + r, f = 2 * c + part;
         const void* src = (m < M && f < F) ? (const void*)(p.ga.ids + (int64_t)m * F + f) : (const void*)neg1;
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(idring + (c & 1) * 2 * BM + ins * 64),
-                                         4, 0, 0);
+        lds_dma<4>(src, idring + (c & 1) * 2 * BM + ins * 64);
       }
     };
     // the first-order weights of stage c (ids of slot c & 1 landed, or the id tile) -> w slot c & 1,
@@ -891,13 +909,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
         if (!S3 && p.fm_w_bf16) {  // (kPrecS3 models have fp32 tables: launch_tower_s3 checks)
           const void* src = id >= 0 ? (const void*)(reinterpret_cast<const bf16_t*>(p.fm_w) + ((int64_t)id << p.fm_wsh))
                                     : (const void*)zero16;
-          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 2, 0, 0);
+          lds_dma<2>(src, wring + e);
         } else {
           // (kPrecS3 issues this unconditionally: zeros when the launch fuses no first order)
           const bool ok = id >= 0 && (!S3 || wfuse);
           const void* src = ok ? (const void*)(reinterpret_cast<const float*>(p.fm_w) + ((int64_t)id << p.fm_wsh))
                                : (const void*)zero16;
-          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(wring + e), 4, 0, 0);
+          lds_dma<4>(src, wring + e);
         }
       }
     };

@@ -40,24 +40,6 @@ static_assert(kQQ == 5 && kQIns == 39, "the static vmcnt counts assume 5 weight 
 #define RMX_QTAIL_DSTRIDE 1
 #endif
 
-// LDS DMA (global_load_lds, `BYTES` per lane; lane L lands at dst + BYTES * L) issued through inline asm.
-// With the builtin the compiler counts the DMA as an LGKM event of unknown order, so every later wait for
-// an LDS read becomes lgkmcnt(0) and drains the prefetched fragments (checked on gfx950 ISA); hidden in
-// asm, the reads keep their counted waits.  The kernels that use it order the DMAs themselves (explicit
-// vmcnt waits + barriers), issue no compiler-visible vector-memory loads in their loops, and keep no value
-// in M0 (every DMA sets it).
-template <int BYTES>
-__device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
-  // (the low 32 bits of a generic pointer into LDS are the LDS address; the address-space cast's null
-  // check tripped an instruction-selection bug, "V_CMP_NE_U32 ... src_shared_base")
-  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(dst));
-  if constexpr (BYTES == 16)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(a), "v"(src) : "memory");
-  else if constexpr (BYTES == 4)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(a), "v"(src) : "memory");
-  else
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off" ::"s"(a), "v"(src) : "memory");
-}
 
 // this wave's DMA q of a unit whose planes start at `src` into the slot at `dst` (LDS byte offset).
 // Instruction ins = w + 8 q fills unit rows [16 ins, 16 ins + 16): plane ins / 13, tile ins % 13; lane L

@@ -267,7 +267,7 @@ __device__ __forceinline__ void tail_issue(const TailArgs& p, char* img, const S
     const int m = m0 + row, kk = c * 32 + swz_slot(row, lane & 3) * 8;
     const void* src = (m < p.M && kk < p.K2) ? (const void*)(p.H + (int64_t)m * p.lda + kk) : (const void*)zero16;
     char* dst = img + slot_at(sm, c) * kTStep + q * 1024;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    lds_dma<16>(src, dst);
   }
 }
 
