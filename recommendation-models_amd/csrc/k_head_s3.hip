@@ -223,8 +223,10 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
 bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids) {
   if (M <= 0 || !ids || k != 16 || F < 1 || F > kHMaxF || !L1.W3 || L1.W16 || !f32_split_enabled()) return false;
   if (!(L1.K == 16 * F && L1.N == 400 && L1.Npad == kQN && L1.N1 < 0 && L1.bias_mode == 1 && L1.K1 < 0)) return false;
-  // knob "s3_head": 0 off, 2 always, 1 when the (half) row blocks fill every CU at least once
-  const int knob = tuning_get("s3_head", 0);  // (default flipped on once measured on the GPU)
+  // knob "s3_head": 0 off, 2 always, 1 (default) when the (half) row blocks fill every CU at least once
+  // (default 1 since measured: DeepFM B = 65,536 186.0 -> 188.2 M examples/s, layer 1 0.182 -> 0.173 ms,
+  // profiles/r04/ab_round4_first.txt)
+  const int knob = tuning_get("s3_head", 1);
   if (knob == 0) return false;
   if (knob == 2) return true;
   int dev = 0, ncu = 256;

@@ -144,14 +144,14 @@ struct QRows {
   }
 };
 
-// host: the row blocks of M rows on ncu CUs and the grid that runs them (knob "half_blocks"; default 0
-// until measured on the GPU)
+// host: the row blocks of M rows on ncu CUs and the grid that runs them (knob "half_blocks", default 1 since
+// measured: DeepFM B = 49,152 137-161 -> 180-182 M examples/s, profiles/r04/ab_round4_first.txt)
 inline QRows q_rows(int M, int ncu, int& grid) {
   QRows r{M, 1, 0, 0};
   const int nb = (M + kQBM - 1) / kQBM;
   ncu = ncu > 0 ? ncu : 1;
   const int R = (nb + ncu - 1) / ncu, last = nb - (R - 1) * ncu;
-  if (tuning_get("half_blocks", 0) != 0 && 2 * last <= ncu) {
+  if (tuning_get("half_blocks", 1) != 0 && 2 * last <= ncu) {
     r.nfull = (R - 1) * ncu;
     r.nhalf = (M - r.nfull * kQBM + kQBM / 2 - 1) / (kQBM / 2);
     grid = r.nfull > 0 ? ncu : (r.nhalf < ncu ? r.nhalf : ncu);

@@ -230,7 +230,8 @@ bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids) {
     if (L.K != (l == 0 ? 16 * F : 400)) return false;
   }
   // knob "s3_small": 0 off, 2 always, 1 (default) below the batch whose 128-row blocks fill every CU
-  const int knob = tuning_get("s3_small", 0);  // (default flipped on once measured on the GPU)
+  // (default 1 since measured: DeepFM B = 4,096 40.8 -> 50.1 M examples/s, profiles/r04/ab_round4_first.txt)
+  const int knob = tuning_get("s3_small", 1);
   if (knob == 0) return false;
   if (knob == 2) return true;
   int dev = 0, ncu = 256;
