@@ -303,5 +303,9 @@ def test_line_table_forward_bitwise_equals_row_table(kind, B):
         outs.append((o.numpy(), p.numpy()))
         t.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
-    assert np.array_equal(outs[0][0], outs[0][1])
+    # forward (one launch of B) against the predict loop (launches of B / 3): a batch's size picks its tower
+    # kernels (row-owner head / tail from the batch that fills every CU, the whole-tower kernel below it),
+    # whose output dots sum in different orders -- equal to fp32 rounding, not bitwise (test_metric.py
+    # holds the loop bitwise to forwards of the same batches)
+    assert float(np.abs(outs[0][0] - outs[0][1]).max()) <= 2e-6
 
