@@ -229,7 +229,7 @@ bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids) {
     if (!L.W3 || L.W16 || L.N != 400 || L.Npad != kSN || L.N1 >= 0 || L.bias_mode != 1 || L.K1 >= 0) return false;
     if (L.K != (l == 0 ? 16 * F : 400)) return false;
   }
-  // knob "s3_small": 0 off, 2 always, 1 (default) below the batch whose 128-row blocks fill every CU
+  // knob "s3_small": 0 off, 2 always, 1 (default) up to one 16-sample block per CU
   // (default 1 since measured: DeepFM B = 4,096 40.8 -> 50.1 M examples/s, profiles/r04/ab_round4_first.txt)
   const int knob = tuning_get("s3_small", 1);
   if (knob == 0) return false;
@@ -238,7 +238,10 @@ bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return M <= tuning_get("s3_small_max", 16384) && (M + 127) / 128 < ncu;
+  // one round of 16-sample blocks (B <= 4,096 on 256 CUs): every block streams all three layers' weights,
+  // so a second round costs a whole round again (B = 16,384: 53 M examples/s, against ~170 M on the
+  // row-owner head + tail's half blocks, profiles/r04/grid_summary.txt)
+  return M <= tuning_get("s3_small_max", 16 * ncu);
 }
 
 int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,

@@ -339,7 +339,9 @@ bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return q_fills(M, ncu);  // (with half blocks, k_rowown.hpp QRows, from M >= 64 ncu)
+  // (half) row blocks that fill every CU, or -- with half blocks -- any batch above the whole-tower kernel's
+  // one round (k_small_s3.hip: M <= 16 ncu): half blocks on part of the chip still beat three engine launches
+  return q_fills(M, ncu) || (tuning_get("half_blocks", 1) != 0 && M > 16 * ncu);
 }
 
 int launch_tower_tail_s3(hipStream_t s, const DenseLayer& L2, const DenseLayer& L3, int M, const float* H, int lda,
