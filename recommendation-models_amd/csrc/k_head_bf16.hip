@@ -144,14 +144,15 @@ __global__ __launch_bounds__(kBThreads, 1) void tower_head_bf16_kernel(HeadBArgs
     const int nu = nit * KS;
 #pragma unroll 1
     for (int u = 0; u < nu; ++u) {
+      // unit u's barrier (the compute waves' at the start of unit u: the slots of step u - 1 are free)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       // the ids of step u + 7 (issued 6 units ago, first in that unit) have landed
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBWaitIds) : "memory");
       b_ld_ids(p, bsmem, nit, u + kBDId, lw, lane);
       b_ld_rows(p, bsmem, u + kBDRow, lw, lane);
-      // the rows / weights of step u + 1 (issued 6 units ago) have landed before the next unit's barrier
+      // the rows / weights of step u + 1 (issued 6 units ago) have landed before unit u + 1's barrier
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBWaitRows) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
