@@ -50,6 +50,7 @@ constexpr int kBLOps = 8;
 constexpr int kBWaitIds = (kBDId - kBDRow - 1) * kBLOps + 6;  // ids issued kBDId - kBDRow units ago
 constexpr int kBWaitRows = (kBDRow - 1) * kBLOps;             // rows of the next step (kBDRow - 1 units ago)
 static_assert(kBWaitIds <= 63 && kBWaitRows <= 63, "vmcnt holds 6 bits");
+static_assert(kBIS >= kBDRow, "the prologue's rows read ids of steps 0 .. kBDRow - 1 from the ring");
 
 struct HeadBArgs {
   int M, nblk, F, KS;
@@ -135,9 +136,11 @@ __global__ __launch_bounds__(kBThreads, 1) void tower_head_bf16_kernel(HeadBArgs
     // ---- loader waves: ids 13 steps and rows / weights 7 steps ahead of their use ----
     const int lw = w - kQW;
     if (nit > 0) {
-      for (int x = 0; x < kBDId; ++x) b_ld_ids(p, bsmem, nit, x, lw, lane);
+      // (the id ring holds 7 steps: the rows of steps 0 .. 6 read their ids before steps 7 .. 12 refill it)
+      for (int x = 0; x < kBIS; ++x) b_ld_ids(p, bsmem, nit, x, lw, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       for (int x = 0; x < kBDRow; ++x) b_ld_rows(p, bsmem, x, lw, lane);
+      for (int x = kBIS; x < kBDId; ++x) b_ld_ids(p, bsmem, nit, x, lw, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
