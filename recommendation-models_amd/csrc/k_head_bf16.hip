@@ -25,32 +25,16 @@ using namespace rowown;
 constexpr int kBNT = 26;                      // column tiles computed: hidden columns + the cross columns
 constexpr int kBUnit = kBNT * 1024;           // bytes per unit: 26 tiles x [16 rows][64 B] of one bf16 plane
 constexpr int kBIns = kBUnit / 1024;          // 26 DMA instructions
-constexpr int kBQ = (kBIns + kQW - 1) / kQW;  // 4 per compute wave (the last ones repeat instruction 25)
+constexpr int kBQ = (kBIns + kQW - 1) / kQW;  // 4 per wave (the last ones repeat instruction 25)
 constexpr int kBSlots = 3;
 constexpr int kBMaxF = 40;
-// loader waves and their rings (see the header)
-constexpr int kBLW = 2;                       // loader waves: samples 64 lw .. 64 lw + 63 of the row block
-constexpr int kBThreads = (kQW + kBLW) * 64;
-constexpr int kBDRow = 7;                     // rows of step x are gathered at unit x - 7
-constexpr int kBDId = 2 * kBDRow - 1;         // ids of step x at unit x - 13 (see the waits)
-constexpr int kBAS = kBDRow + 1;              // row / weight ring slots
-constexpr int kBIS = kBDId - kBDRow + 1;      // id ring slots
-constexpr int kBAStep = 2 * kQBM * 32;        // [2 fields][128 samples][32 B]
-constexpr int kBWStep = 2 * kQBM * 4;         // [2 fields][128 samples] dwords (2-byte DMAs, zero-extended)
-constexpr int kBIStep = 2 * kQBM * 4;         // [2 fields][128 samples] ids
-constexpr int kBOffA = kBSlots * kBUnit;
-constexpr int kBOffW = kBOffA + kBAS * kBAStep;
-constexpr int kBOffI = kBOffW + kBAS * kBWStep;
-constexpr int kBOffB = kBOffI + kBIS * kBIStep;
-constexpr size_t kBLds = (size_t)kBOffB + sizeof(float) * kQN;
+constexpr int kBA = 4 * 1024;                 // per wave: 4 step slots x [2 fields][16 samples][32 B]
+constexpr int kBId = 4 * 128;                 // per wave: 4 slots x [2 fields][16] ids
+constexpr int kBWr = 4 * 128;                 // per wave: 4 slots x [2 fields][16] first-order weights (dwords)
+constexpr int kBWave = kBA + kBId + kBWr;
+constexpr size_t kBLds = (size_t)kBSlots * kBUnit + (size_t)kQW * kBWave + sizeof(float) * kQN;
 static_assert(kBLds <= 160 * 1024, "LDS budget");
-static_assert(kBQ == 4, "the compute waves' static vmcnt count assumes 4 weight DMAs per unit");
-// loader vmcnt counts: per unit a loader issues 2 id DMAs, then 4 row + 2 weight DMAs (8)
-constexpr int kBLOps = 8;
-constexpr int kBWaitIds = (kBDId - kBDRow - 1) * kBLOps + 6;  // ids issued kBDId - kBDRow units ago
-constexpr int kBWaitRows = (kBDRow - 1) * kBLOps;             // rows of the next step (kBDRow - 1 units ago)
-static_assert(kBWaitIds <= 63 && kBWaitRows <= 63, "vmcnt holds 6 bits");
-static_assert(kBIS >= kBDRow, "the prologue's rows read ids of steps 0 .. kBDRow - 1 from the ring");
+static_assert(kBQ == 4, "the static vmcnt counts below assume 4 weight DMAs per wave per unit");
 
 struct HeadBArgs {
   int M, nblk, F, KS;
@@ -77,97 +61,65 @@ __device__ __forceinline__ void b_wdma(const bf16_t* src, char* lds, int slot, i
   lds_dma<16>(src + ins * 16 * 32 + lo, lds + slot * kBUnit + ins * 1024);
 }
 
-// step x of a block (global across its row blocks): K step x % KS of row block blockIdx.x + (x / KS) G
-__device__ __forceinline__ void b_step(const HeadBArgs& p, int nit, int x, int& rb, int& c) {
-  const int it = x / p.KS;
-  c = x - it * p.KS;
-  rb = it < nit ? (int)blockIdx.x + it * (int)gridDim.x : p.nblk;
+// ids of K step c of row block rb into id slot `slot` (lanes 0 .. 31: field 2c + (L >> 4) of sample L & 15)
+__device__ __forceinline__ void b_id_dma(const HeadBArgs& p, char* wl, int rb, int c, int slot, int w, int lane) {
+  int f = lane >> 4, r = lane & 15;
+  asm volatile("" : "+v"(f), "+v"(r));
+  const int m = rb * kQBM + w * 16 + r, fld = 2 * c + f;
+  const bool ok = rb < p.nblk && m < p.M && fld < p.F;
+  const int32_t* src = ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1;
+  if (lane < 32)
+    lds_dma<4>(src, wl + kBA + slot * 128);
 }
 
-// loader lw: the ids of step x (2 DMAs: field f, lane L = sample 64 lw + L)
-__device__ __forceinline__ void b_ld_ids(const HeadBArgs& p, char* smem, int nit, int x, int lw, int lane) {
-  int rb, c;
-  b_step(p, nit, x, rb, c);
-  char* dst = smem + kBOffI + (x % kBIS) * kBIStep + lw * 256;
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int m = rb * kQBM + lw * 64 + lane, fld = 2 * c + f;
-    const bool ok = rb < p.nblk && m < p.M && fld < p.F;
-    lds_dma<4>(ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1, dst + f * 512);
-  }
+// rows of the wave's step s (one DMA: lane L = field L >> 5, sample (L >> 1) & 15, half L & 1 of the
+// 32-B row) and its first-order weights (lanes 0 .. 31: a 2-byte DMA lands zero-extended in a dword)
+__device__ __forceinline__ void b_row_dma(const HeadBArgs& p, char* wl, int s, int lane) {
+  const int* ids = reinterpret_cast<const int*>(wl + kBA + (s & 3) * 128);
+  int f = lane >> 5, r = (lane >> 1) & 15, hf = lane & 1, lw = lane & 31;
+  asm volatile("" : "+v"(f), "+v"(r), "+v"(hf), "+v"(lw));
+  const int id = ids[f * 16 + r], idw = ids[lw];
+  const void* src = id >= 0 ? (const void*)(p.table + ((int64_t)id << p.gsh) + 8 * hf) : (const void*)g_rmx_zero16;
+  const void* sw = idw >= 0 ? (const void*)(p.wtab + ((int64_t)idw << p.wsh)) : (const void*)g_rmx_zero16;
+  lds_dma<16>(src, wl + (s & 3) * 1024);
+  if (lane < 32)
+    lds_dma<2>(sw, wl + kBA + kBId + (s & 3) * 128);
 }
 
-// loader lw: rows (4 DMAs: field f, 32-sample half j; lane L = sample 64 lw + 32 j + (L >> 1), half L & 1)
-// and first-order weights (2 DMAs: field f, lane L = sample 64 lw + L) of step x, from its ids in LDS
-__device__ __forceinline__ void b_ld_rows(const HeadBArgs& p, char* smem, int x, int lw, int lane) {
-  const int* ids = reinterpret_cast<const int*>(smem + kBOffI + (x % kBIS) * kBIStep);
-  char* da = smem + kBOffA + (x % kBAS) * kBAStep;
-  char* dw = smem + kBOffW + (x % kBAS) * kBWStep;
-  int sl = lw * 64 + (lane >> 1), hf = lane & 1, sw = lw * 64 + lane;
-  asm volatile("" : "+v"(sl), "+v"(hf), "+v"(sw));
-#pragma unroll
-  for (int f = 0; f < 2; ++f)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int id = ids[f * kQBM + sl + 32 * j];
-      const void* src = id >= 0 ? (const void*)(p.table + ((int64_t)id << p.gsh) + 8 * hf) : (const void*)g_rmx_zero16;
-      lds_dma<16>(src, da + f * 4096 + (lw * 64 + 32 * j) * 32);
-    }
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const int id = ids[f * kQBM + sw];
-    const void* src = id >= 0 ? (const void*)(p.wtab + ((int64_t)id << p.wsh)) : (const void*)g_rmx_zero16;
-    lds_dma<2>(src, dw + f * 512 + lw * 256);
-  }
+template <int N>
+__device__ __forceinline__ void b_enter() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
-__global__ __launch_bounds__(kBThreads, 1) void tower_head_bf16_kernel(HeadBArgs p) {
+__global__ __launch_bounds__(kQThreads, 1) void tower_head_bf16_kernel(HeadBArgs p) {
   extern __shared__ __attribute__((aligned(16))) char bsmem[];
   char* lds = bsmem;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  float* bl = reinterpret_cast<float*>(bsmem + kBOffB);
+  char* wl = bsmem + kBSlots * kBUnit + w * kBWave;
+  float* bl = reinterpret_cast<float*>(bsmem + kBSlots * kBUnit + kQW * kBWave);
   const int nit = (int)blockIdx.x < p.nblk ? (p.nblk - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int KS = p.KS;
-  for (int i = tid; i < kQN; i += kBThreads) bl[i] = p.b ? p.b[i] : 0.f;
-  auto wsrc = [&](int x) { return p.W + (int64_t)(x % KS) * kQN * 32; };
-
-  if (w >= kQW) {
-    // ---- loader waves: ids 13 steps and rows / weights 7 steps ahead of their use ----
-    const int lw = w - kQW;
-    if (nit > 0) {
-      // (the id ring holds 7 steps: the rows of steps 0 .. 6 read their ids before steps 7 .. 12 refill it)
-      for (int x = 0; x < kBIS; ++x) b_ld_ids(p, bsmem, nit, x, lw, lane);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (int x = 0; x < kBDRow; ++x) b_ld_rows(p, bsmem, x, lw, lane);
-      for (int x = kBIS; x < kBDId; ++x) b_ld_ids(p, bsmem, nit, x, lw, lane);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int nu = nit * KS;
-#pragma unroll 1
-    for (int u = 0; u < nu; ++u) {
-      // unit u's barrier (the compute waves' at the start of unit u: the slots of step u - 1 are free)
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      // the ids of step u + 7 (issued 6 units ago, first in that unit) have landed
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBWaitIds) : "memory");
-      b_ld_ids(p, bsmem, nit, u + kBDId, lw, lane);
-      b_ld_rows(p, bsmem, u + kBDRow, lw, lane);
-      // the rows / weights of step u + 1 (issued 6 units ago) have landed before unit u + 1's barrier
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBWaitRows) : "memory");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-
-  // ---- compute waves: 16 samples x all 416 columns each, the weights through the 3-slot ring ----
+  for (int i = tid; i < kQN; i += kQThreads) bl[i] = p.b ? p.b[i] : 0.f;
   const int fb = q_fbase(lane);
+
+  // the wave's steps s = 0, 1, ... over its row blocks (step s: K step s % KS of row block
+  // blockIdx.x + (s / KS) gridDim.x, none past the last); ring slots s & 3, weight-ring slot s % 3
+  auto id_dma = [&](int s) {
+    const int it = s / KS, c = s - it * KS;
+    const int rb = it < nit ? (int)blockIdx.x + it * (int)gridDim.x : p.nblk;
+    b_id_dma(p, wl, rb, c, s & 3, w, lane);
+  };
+  auto wsrc = [&](int s) { return p.W + (int64_t)(s % KS) * kQN * 32; };
   if (nit > 0) {
+    for (int s = 0; s < 3; ++s) id_dma(s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int s = 0; s < 2; ++s) {
+      b_row_dma(p, wl, s, lane);
 #pragma unroll
-    for (int q = 0; q < kBQ; ++q) {
-      b_wdma(wsrc(0), lds, 0, w, q);
-      b_wdma(wsrc(1), lds, 1, w, q);
+      for (int q = 0; q < kBQ; ++q) b_wdma(wsrc(s), lds, s, w, q);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -182,20 +134,17 @@ __global__ __launch_bounds__(kBThreads, 1) void tower_head_bf16_kernel(HeadBArgs
     float y1 = 0.f;
 #pragma unroll 1
     for (int c = 0; c < KS; ++c, ++s) {
-      // this wave's weight DMAs of unit s (issued two units ago) have landed; the barrier: every wave's,
-      // and the loaders' rows of step s
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBQ) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const char* sa = bsmem + kBOffA + (s % kBAS) * kBAStep;
-      int o = (g >> 1) * 4096 + (w * 16 + r16) * 32 + (g & 1) * 16;
+      b_enter<6>();  // all but the previous unit's last 6 DMAs: its ids (for step s + 2) have landed
+      int o = (g >> 1) * 512 + r16 * 32 + (g & 1) * 16;
       asm volatile("" : "+v"(o));
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(sa + o);
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(wl + (s & 3) * 1024 + o);
       {
-        const uint32_t* wr = reinterpret_cast<const uint32_t*>(bsmem + kBOffW + (s % kBAS) * kBWStep);
-        y1 += __uint_as_float(wr[w * 16 + r16] << 16);  // first order, field order (encoder_k16_kernel<0>)
-        y1 += __uint_as_float(wr[kQBM + w * 16 + r16] << 16);
+        const uint32_t* wr = reinterpret_cast<const uint32_t*>(wl + kBA + kBId + (s & 3) * 128);
+        y1 += __uint_as_float(wr[r16] << 16);  // first order, field order (encoder_k16_kernel<0>)
+        y1 += __uint_as_float(wr[16 + r16] << 16);
       }
+      id_dma(s + 3);
+      b_row_dma(p, wl, s + 2, lane);
       __builtin_amdgcn_sched_barrier(0);
       const int ds = slot == 0 ? 2 : slot - 1;  // (slot + 2) mod 3
       const bf16_t* src = wsrc(s + 2);
@@ -292,7 +241,7 @@ int launch_tower_head_bf16(hipStream_t s, const DenseLayer& L1, int M, int F, co
   p.xld = xc ? xc->ld : 0;
   p.fm_y = fm_y;
   const int grid = std::min(p.nblk, std::max(ncu, 1));
-  hipLaunchKernelGGL(tower_head_bf16_kernel, dim3(grid), dim3(kBThreads), kBLds, s, p);
+  hipLaunchKernelGGL(tower_head_bf16_kernel, dim3(grid), dim3(kQThreads), kBLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }
