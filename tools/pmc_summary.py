@@ -70,7 +70,10 @@ def stage_of(kernel, workload=""):
                     ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
                     ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
                     ("owner_gather", "shard_exchange"), ("own_rows_kernel", "shard_exchange"),
-                    ("own_gather", "shard_exchange"), ("tower_tail_bf16_kernel", "tower_tail")):
+                    ("own_gather", "shard_exchange"), ("tower_tail_bf16_kernel", "tower_tail"),
+                    ("tower_tail_s3_kernel", "tower_tail"), ("tower_head_s3_kernel", "tower_layer1"),
+                    ("tower_small_s3_kernel", "tower_small"), ("tower_head_bf16_kernel", "tower_layer1"),
+                    ("pnn_head_kernel", "tower_layer1"), ("cin_row_kernel", "cin")):
         if kernel.startswith(pat):
             return st
     return None
