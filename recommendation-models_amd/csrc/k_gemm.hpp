@@ -245,8 +245,21 @@ struct EpiGeom {
 // asm, the reads keep their counted waits.  The kernels that use it order the DMAs themselves (explicit
 // vmcnt waits + barriers), issue no compiler-visible vector-memory loads in their loops, and keep no value
 // in M0 (every DMA sets it).
+#ifndef RMX_LDS_DMA_BUILTIN
+#define RMX_LDS_DMA_BUILTIN 0  // (1: the builtin, timing A/B builds only)
+#endif
 template <int BYTES>
 __device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
+#if RMX_LDS_DMA_BUILTIN
+  __attribute__((address_space(3))) void* d = (__attribute__((address_space(3))) void*)(uintptr_t)(unsigned)(uintptr_t)dst;
+  if constexpr (BYTES == 16)
+    __builtin_amdgcn_global_load_lds(src, d, 16, 0, 0);
+  else if constexpr (BYTES == 4)
+    __builtin_amdgcn_global_load_lds(src, d, 4, 0, 0);
+  else
+    __builtin_amdgcn_global_load_lds(src, d, 2, 0, 0);
+  return;
+#endif
   // (the low 32 bits of a generic pointer into LDS are the LDS address; the address-space cast's null
   // check tripped an instruction-selection bug, "V_CMP_NE_U32 ... src_shared_base")
   const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(dst));

@@ -19,6 +19,9 @@
 //                     s + 3, rows + weights of step s + 1 (from ids already in LDS), 5 weight-plane DMAs
 //   unit (c, half 1): wait, barrier; 5 weight-plane DMAs
 // so every unit's vector-memory count is static (9 / 5) and each wait is a compile-time vmcnt.
+// LDS DMAs through the builtin in this translation unit (k_gemm.hpp lds_dma): measured faster here than
+// the asm form, DeepFM 196.1-196.4 vs 193.4-194.0 M with the asm form (profiles/r04/ab_lds_dma_form.txt)
+#define RMX_LDS_DMA_BUILTIN 1
 #include "k_rowown.hpp"
 
 namespace rmx {

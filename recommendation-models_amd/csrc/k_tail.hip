@@ -31,6 +31,9 @@
 // The sums are the unfused kernels' up to the order of the final logit reduction: h2 is the same
 // bf16 (RNE) of the same fp32 accumulations (K steps in order), so parity is held to the same bar
 // against the oracle's bf16 emulation (tests/test_bf16.py).
+// LDS DMAs through the builtin in this translation unit (k_gemm.hpp lds_dma): measured faster here than
+// the asm form, bf16 tail 0.042 vs 0.048 ms with the asm form (profiles/r04/ab_lds_dma_form.txt)
+#define RMX_LDS_DMA_BUILTIN 1
 #include "k_gemm.hpp"
 
 namespace rmx {
