@@ -214,6 +214,10 @@ int rmx_auc(rmx_ctx* ctx, int64_t n, const float* d_labels, const float* d_score
 int rmx_gen_ids_zipf(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, int32_t n_fields,
                      int64_t num_rows, double exponent, int32_t* d_ids, void* stream);
 
+/* Test hook: fill the LDS of every CU with a 32-bit pattern (e.g. 0x7FC00000, a NaN) on the stream, so a
+ * kernel launched next that reads LDS it never wrote reads that pattern (tests/test_small_s3.py). */
+int rmx_debug_fill_lds(rmx_ctx* ctx, uint32_t pattern, void* stream);
+
 /* Debug gather: d_w[n] = weights[ids[n]], d_emb[n*k+j] = emb[ids[n]][j] (makeWeights /
  * makeEmbeddings, ParRecModel.scala:279-306).  Bit-exact copies (as fp32 for a bf16 table). */
 int rmx_gather(const rmx_table* t, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,

@@ -408,6 +408,27 @@ extern "C" int rmx_gen_ids(rmx_ctx* c, uint64_t seed, int64_t row0, int32_t B, i
   return launch_gen_ids(stream ? (hipStream_t)stream : c->stream, seed, row0, B, F, V, d_ids);
 }
 
+// Test hook: every workgroup takes a whole CU's LDS (160 KiB) and fills it with `pattern`, so a kernel
+// launched next that reads LDS it never wrote sees that pattern rather than a benign leftover.
+__global__ __launch_bounds__(1024) void fill_lds_kernel(uint32_t pattern, int words) {
+  extern __shared__ uint32_t fl_lds[];
+  volatile uint32_t* l = fl_lds;  // (volatile: stores nothing reads back)
+  for (int i = threadIdx.x; i < words; i += blockDim.x) l[i] = pattern;
+}
+
+extern "C" int rmx_debug_fill_lds(rmx_ctx* c, uint32_t pattern, void* stream) {
+  CHECK_ARG(c, "rmx_debug_fill_lds: NULL context");
+  RMX_HIP(hipSetDevice(c->device));
+  int ncu = 256;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) ncu = 256;
+  const int lds = 160 * 1024;  // gfx950: the whole LDS of a CU
+  RMX_HIP(hipFuncSetAttribute((const void*)fill_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipLaunchKernelGGL(fill_lds_kernel, dim3(4 * ncu), dim3(1024), (size_t)lds, stream ? (hipStream_t)stream : c->stream,
+                     pattern, lds / 4);
+  RMX_HIP(hipGetLastError());
+  return RMX_OK;
+}
+
 extern "C" int rmx_gen_ids_zipf(rmx_ctx* c, uint64_t seed, int64_t row0, int32_t B, int32_t F, int64_t V,
                                 double exponent, int32_t* d_ids, void* stream) {
   CHECK_ARG(c && d_ids && B >= 0 && F > 0 && V >= F && exponent > 0.0 && exponent != 1.0,

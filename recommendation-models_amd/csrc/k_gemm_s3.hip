@@ -209,6 +209,18 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // 4: 32-row waves, 4-wave blocks on a single-buffered 55 KiB stage, two blocks per CU (the partner
   // wave on a SIMD belongs to the other block, so one block's DMA wait / epilogue meets the other's MFMAs)
   if (var == 4) return launch_epi<Tile<2, kS3NT, 4, 1, 1, 2, 1>, kPrecS3>(s, p, amode, epi);
+  // knob "s3_narrow" (default 1): 2-wave blocks (32 rows x 208 columns) when the 8-wave tile's blocks would
+  // leave CUs idle -- small launch batches (B = 4,096: 64 -> 256 blocks).  Same products in the same K
+  // order (bitwise).  DeepFM's layers on the engine at B = 4,096: 0.0486 / 0.0288 / 0.0270 ->
+  // 0.0444 / 0.0265 / 0.0249 ms (profiles/r04/ab_small_rt.txt)
+  if (tuning_get("s3_narrow", 1) != 0 && !s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr)) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+    const int64_t blocks8 = (int64_t)(p.M + 127) / 128 * (p.Npad / (kS3NT * 16));
+    if (blocks8 < ncu) return launch_epi<Tile<1, kS3NT, 2, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
+  }
   if (s3_mt2(p.M, p.Npad, amode, p.ga.ids != nullptr)) {
     // knob "s3_dense" (dense-A layers at this size; all accumulate in the same K order: equal bits):
     //   5 (default) 16 waves of 16 rows, 4 per SIMD, 2-deep ring (the CIN's s3_cin 4 shape; DeepFM at

@@ -1,17 +1,19 @@
-// k_small_s3.hip -- DeepFM's whole fp32 tower for small launch batches: one block per 16 samples, all
-// three layers + the FM / first order + the head in one launch, on the split GEMM (gfx950).
+// k_small_s3.hip -- DeepFM's whole fp32 tower for small launch batches: one block per 16 or 32 samples,
+// all three layers + the FM / first order + the head in one launch, on the split GEMM (gfx950).
 //
 // The tower (model/encoder/HigherOrderEncoder.scala:34-59: Linear(F k -> 400) + ReLU, 400 -> 400 + ReLU,
 // 400 -> 400 + ReLU, Linear(400 -> 1)), the first order (bnn/Scatter.scala:17-36), the FM second order
 // (SecondOrderEncoder.scala:19-34) and DeepFM's head (DeepFM.scala:54-80: CAddTable + Sigmoid).
 // Why: below ~32 K samples the row-owner kernels (k_head_s3 / k_tail_s3: 128 rows per block) and the
 // column-sliced split GEMM (128-row blocks x 2 slices) launch far fewer blocks than the 256 CUs -- at
-// B = 4,096 layer 1 ran 64 blocks -- and each layer is its own launch.  Here a block owns only 16 samples
-// (B = 4,096 -> 256 blocks) and keeps them on the CU through all three layers: the gathered x tile and the
-// activations live in LDS, the 8 waves split the 25 column tiles (wave w: tiles w, w + 8, w + 16, w + 24),
-// and each wave streams its own weight fragments (1 KiB contiguous per plane, K step and tile) straight
-// from L2 into registers one K step ahead -- a fragment is read by exactly one wave of the block, so LDS
-// staging would buy no reuse.  The bound is that L2 stream: ~3.6 MB of split planes per block.
+// B = 4,096 layer 1 ran 64 blocks -- and each layer is its own launch.  Here a block owns RT row tiles of
+// 16 samples (B = 4,096 -> 256 blocks of 16) and keeps them on the CU through all three layers: the
+// gathered x tile and the activations live in LDS, the 8 waves split the 25 column tiles (wave w: tiles
+// w, w + 8, w + 16, w + 24), and each wave streams its own weight fragments (1 KiB contiguous per plane,
+// K step and tile) straight from L2 into registers one K step ahead, each fragment feeding the RT row
+// tiles -- a fragment is read by exactly one wave of the block, so LDS staging would buy no reuse.  The
+// bound is that stream: ~3.6 MB of split planes per block at ~70 GB/s per CU (a K step two ahead
+// measured no faster), so a block's time hardly depends on RT.
 // Arithmetic: the engine's split products in the engine's order per K step (k_gemm.hpp kPrecS3, operands
 // swapped as in k_rowown.hpp), the FM / first order in encoder_k16_kernel<1>'s order (bit-identical).
 #include "k_gemm.hpp"
@@ -19,7 +21,6 @@
 namespace rmx {
 namespace {
 
-constexpr int kSR = 16;                   // samples per block
 constexpr int kSW = 8;                    // waves
 constexpr int kSThreads = kSW * 64;
 constexpr int kSN = 416;                  // Npad of the 400-wide layers
@@ -29,9 +30,13 @@ constexpr int kSMaxF = 40;
 constexpr int kSXS = kSMaxF * 16 + 4;     // x tile row stride (floats): +4 keeps the 16-B reads conflict-free
 constexpr int kSHS = kSN + 4;             // activation tile row stride
 constexpr int kSTW = 4;                   // max column tiles per wave (wave 0: 4, the others 3)
-constexpr size_t kSLds =
-    sizeof(float) * (kSR * kSXS + kSR * kSHS + kSW * kSR + 3 * kSN + kSR) + sizeof(int) * kSR * kSMaxF;
-static_assert(kSLds <= 80 * 1024, "LDS budget");
+// RT row tiles of 16 samples per block (kSR samples): each weight fragment loaded feeds RT MFMA row tiles
+template <int RT>
+constexpr size_t small_lds() {
+  return sizeof(float) * (16 * RT * kSXS + 16 * RT * kSHS + kSW * 16 * RT + 3 * kSN + 16 * RT) +
+         sizeof(int) * 16 * RT * kSMaxF;
+}
+static_assert(small_lds<2>() <= 160 * 1024, "LDS budget");
 
 struct SmallArgs {
   int M, F;
@@ -47,13 +52,19 @@ struct SmallArgs {
 };
 
 // one layer: acc[j] (column tile w + 8 j) = sum over K steps of W_t x^T on the split planes, x from LDS
-// (row stride XS floats); weight fragments of step c + 1 loaded during step c
-template <int NTW>
+// (row stride XS floats); weight fragments of step c + 1 loaded during step c.  PAD (the 400-wide
+// layers): the upper half of the last step, columns 400 .. 415, is K padding that no wave writes (25 of
+// the 26 tiles are computed) -- read as zeros, as the tails do: its weights are zero, but the LDS there
+// holds whatever an earlier workgroup left, and 0 x a leftover NaN / Inf is NaN, which ReLU turns into a
+// silently wrong 0 (seen as one wrong row in some blocks, depending on what ran before on the CU)
+template <int NTW, int RT, bool PAD>
 __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const float* xin, int xs, int KS, int w, int lane,
-                                        f32x4 (&acc)[kSTW]) {
+                                        f32x4 (&acc)[RT][kSTW]) {
   const int g = lane >> 4, r16 = lane & 15;
 #pragma unroll
-  for (int j = 0; j < kSTW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int j = 0; j < kSTW; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int wo = r16 * 32 + g * 8;  // lane's element of a fragment
   asm volatile("" : "+v"(wo));
   auto ldw = [&](int c, f32x4 (&b)[NTW][3]) {
@@ -69,22 +80,29 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
   asm volatile("" : "+v"(xo));
   auto step = [&](int c, f32x4 (&cur)[NTW][3], f32x4 (&nxt)[NTW][3]) {
     if (c + 1 < KS) ldw(c + 1, nxt);
-    const f32x4 a0 = *reinterpret_cast<const f32x4*>(xin + xo + 32 * c);
-    const f32x4 a1 = *reinterpret_cast<const f32x4*>(xin + xo + 32 * c + 16);
-    bf16x8 ah, am, al;
-    split3(a0, a1, ah, am, al);
+    bf16x8 ah[RT], am[RT], al[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(xin + xo + 16 * t * xs + 32 * c);
+      f32x4 a1 = *reinterpret_cast<const f32x4*>(xin + xo + 16 * t * xs + 32 * c + 16);
+      if (PAD && c == KS - 1) a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      split3(a0, a1, ah[t], am[t], al[t]);
+    }
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const bf16x8 bh = __builtin_bit_cast(bf16x8, cur[j][0]);
       const bf16x8 bm = __builtin_bit_cast(bf16x8, cur[j][1]);
       const bf16x8 bl = __builtin_bit_cast(bf16x8, cur[j][2]);
-      f32x4 d = acc[j];
-      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am, d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am, d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, d, 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, d, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        f32x4 d = acc[t][j];
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am[t], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[t], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[t], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am[t], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah[t], d, 0, 0, 0);
+        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[t], d, 0, 0, 0);
+      }
     }
   };
 #pragma unroll 1
@@ -95,61 +113,70 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
 }
 
 // ReLU(acc + b) of the wave's tiles into the activation tile (lane: row r16, columns 16 t + 4 g .. + 3)
-template <int NTW>
-__device__ __forceinline__ void s_store_h(const f32x4 (&acc)[kSTW], const float* bl, float* h, int w, int lane) {
+template <int NTW, int RT>
+__device__ __forceinline__ void s_store_h(const f32x4 (&acc)[RT][kSTW], const float* bl, float* h, int w, int lane) {
   const int g = lane >> 4, r16 = lane & 15;
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
     const int n0 = 16 * (w + 8 * j) + 4 * g;
     const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + n0);
-    f32x4 v = acc[j] + bb;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-    *reinterpret_cast<f32x4*>(h + r16 * kSHS + n0) = v;
-  }
-}
-
-template <int NTW>
-__device__ void s_wave(const SmallArgs& p, float* x, float* h, float* prm, float* red, int w, int lane) {
-  const int g = lane >> 4, r16 = lane & 15;
-  f32x4 acc[kSTW];
-  // layer 1: x tile (row stride kSXS) -> h
-  s_layer<NTW>(p.W[0], x, kSXS, p.KS1, w, lane, acc);
-  s_store_h<NTW>(acc, prm, h, w, lane);
-  __syncthreads();
-  // layer 2: h -> the x region (stride kSHS)
-  s_layer<NTW>(p.W[1], h, kSHS, 13, w, lane, acc);
-  __syncthreads();  // every wave has read h ... (the x region is free since layer 1)
-  s_store_h<NTW>(acc, prm + kSN, x, w, lane);
-  __syncthreads();
-  // layer 3 + the output dot over the wave's columns
-  s_layer<NTW>(p.W[2], x, kSHS, 13, w, lane, acc);
-  float part = 0.f;
+    for (int t = 0; t < RT; ++t) {
+      f32x4 v = acc[t][j] + bb;
 #pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int n0 = 16 * (w + 8 * j) + 4 * g;
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(prm + 2 * kSN + n0);
-    const f32x4 wv = *reinterpret_cast<const f32x4*>(p.oa.wo + n0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = acc[j][r] + bb[r];
-      v = v > 0.f ? v : 0.f;
-      part += v * wv[r];
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+      *reinterpret_cast<f32x4*>(h + (16 * t + r16) * kSHS + n0) = v;
     }
   }
-  part += __shfl_xor(part, 16);
-  part += __shfl_xor(part, 32);
-  if (g == 0) red[w * kSR + r16] = part;
 }
 
+template <int NTW, int RT>
+__device__ void s_wave(const SmallArgs& p, float* x, float* h, float* prm, float* red, int w, int lane) {
+  constexpr int kSR = 16 * RT;
+  const int g = lane >> 4, r16 = lane & 15;
+  f32x4 acc[RT][kSTW];
+  // layer 1: x tile (row stride kSXS) -> h
+  s_layer<NTW, RT, false>(p.W[0], x, kSXS, p.KS1, w, lane, acc);  // (x: every column written)
+  s_store_h<NTW, RT>(acc, prm, h, w, lane);
+  __syncthreads();
+  // layer 2: h -> the x region (stride kSHS)
+  s_layer<NTW, RT, true>(p.W[1], h, kSHS, 13, w, lane, acc);
+  __syncthreads();  // every wave has read h ... (the x region is free since layer 1)
+  s_store_h<NTW, RT>(acc, prm + kSN, x, w, lane);
+  __syncthreads();
+  // layer 3 + the output dot over the wave's columns
+  s_layer<NTW, RT, true>(p.W[2], x, kSHS, 13, w, lane, acc);
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n0 = 16 * (w + 8 * j) + 4 * g;
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(prm + 2 * kSN + n0);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(p.oa.wo + n0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[t][j][r] + bb[r];
+        v = v > 0.f ? v : 0.f;
+        part += v * wv[r];
+      }
+    }
+    part += __shfl_xor(part, 16);
+    part += __shfl_xor(part, 32);
+    if (g == 0) red[w * kSR + 16 * t + r16] = part;
+  }
+}
+
+template <int RT>
 __global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs p) {
+  constexpr int kSR = 16 * RT;
   extern __shared__ __attribute__((aligned(16))) float ssmem[];
-  float* x = ssmem;                       // [16][kSXS] gathered rows; later layer 2's output
-  float* h = x + kSR * kSXS;              // [16][kSHS] layer 1's output
-  float* red = h + kSR * kSHS;            // [8 waves][16] partial logits
+  float* x = ssmem;                       // [kSR][kSXS] gathered rows; later layer 2's output
+  float* h = x + kSR * kSXS;              // [kSR][kSHS] layer 1's output
+  float* red = h + kSR * kSHS;            // [8 waves][kSR] partial logits
   float* prm = red + kSW * kSR;           // b1 | b2 | b3
-  float* fmv = prm + 3 * kSN;             // [16] first order + FM (y1 + y2) per sample
-  int* sid = reinterpret_cast<int*>(fmv + kSR);  // [16][F] ids
+  float* fmv = prm + 3 * kSN;             // [kSR] first order + FM (y1 + y2) per sample
+  int* sid = reinterpret_cast<int*>(fmv + kSR);  // [kSR][F] ids
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = blockIdx.x * kSR, F = p.F;
   for (int i = tid; i < 3 * kSN; i += kSThreads) {
@@ -173,11 +200,12 @@ __global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs 
     *reinterpret_cast<float4*>(x + r * kSXS + 16 * f + 4 * q) = v;
   }
   __syncthreads();
-  // first order + FM of sample r (wave 0, 16 lanes per sample, lane j of the group: column j), in
-  // encoder_k16_kernel<1>'s order: s_j, q_j over the fields in order, a = sum_j (s_j^2 - q_j) in j order
-  if (w == 0) {
+  // first order + FM of sample r (16 lanes per sample, lane j of the group: column j; wave w takes samples
+  // 4 w .. 4 w + 3, then + 32), in encoder_k16_kernel<1>'s order: s_j, q_j over the fields in order,
+  // a = sum_j (s_j^2 - q_j) in j order
+  {
 #pragma clang fp contract(off)
-    for (int rr = 0; rr < kSR; rr += 4) {
+    for (int rr = 4 * w; rr < kSR; rr += 4 * kSW) {
       const int r = rr + (lane >> 4), j = lane & 15;
       float s = 0.f, q = 0.f;
       for (int f = 0; f < F; ++f) {
@@ -199,9 +227,9 @@ __global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs 
   }
   __syncthreads();
   if (w == 0)
-    s_wave<4>(p, x, h, prm, red, w, lane);
+    s_wave<4, RT>(p, x, h, prm, red, w, lane);
   else
-    s_wave<3>(p, x, h, prm, red, w, lane);
+    s_wave<3, RT>(p, x, h, prm, red, w, lane);
   __syncthreads();
   if (tid < kSR) {
     const int m = m0 + tid;
@@ -238,10 +266,10 @@ bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids) {
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  // one round of 16-sample blocks (B <= 4,096 on 256 CUs): every block streams all three layers' weights,
-  // so a second round costs a whole round again (B = 16,384: 53 M examples/s, against ~170 M on the
-  // row-owner head + tail's half blocks, profiles/r04/grid_summary.txt)
-  return M <= tuning_get("s3_small_max", 16 * ncu);
+  // one round of 16- or 32-sample blocks (B <= 8,192 on 256 CUs): every block streams all three layers'
+  // weights, so a second round costs a whole round again (B = 16,384: 53 M examples/s, against ~156 M on
+  // the row-owner head + tail's half blocks, profiles/r04/grid_summary.txt)
+  return M <= tuning_get("s3_small_max", 32 * ncu);
 }
 
 int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,
@@ -252,8 +280,19 @@ int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const
     set_error("fp32 small tower: table / weight strides must be powers of two, and an output head");
     return RMX_E_INVALID;
   }
-  RMX_HIP(hipFuncSetAttribute((const void*)tower_small_s3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kSLds));
+  // knob "s3_small_rt": row tiles of 16 samples per block, 1 or 2; 0 (default) = 1 while 16-sample blocks
+  // fit one round on the CUs, else 2.  Each CU streams the whole tower's split weights at ~70 GB/s whatever
+  // its row count, and a second row tile costs only its MFMAs: B = 8,192 one round of 32-sample blocks
+  // 0.072 ms (111 M examples/s) against the head + tail's 0.102 ms; B = 4,096 16-sample blocks 0.0645 vs
+  // 0.071 ms (profiles/r04/ab_small_rt.txt)
+  int rt = tuning_get("s3_small_rt", 0);
+  if (rt != 1 && rt != 2) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+    rt = M <= 16 * ncu ? 1 : 2;
+  }
   SmallArgs p{};
   p.M = M;
   p.F = F;
@@ -268,7 +307,15 @@ int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const
   }
   p.KS1 = (F + 1) / 2;
   p.oa = oa;
-  hipLaunchKernelGGL(tower_small_s3_kernel, dim3((M + kSR - 1) / kSR), dim3(kSThreads), kSLds, s, p);
+  if (rt == 2) {
+    RMX_HIP(hipFuncSetAttribute((const void*)tower_small_s3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)small_lds<2>()));
+    hipLaunchKernelGGL(tower_small_s3_kernel<2>, dim3((M + 31) / 32), dim3(kSThreads), small_lds<2>(), s, p);
+  } else {
+    RMX_HIP(hipFuncSetAttribute((const void*)tower_small_s3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)small_lds<1>()));
+    hipLaunchKernelGGL(tower_small_s3_kernel<1>, dim3((M + 15) / 16), dim3(kSThreads), small_lds<1>(), s, p);
+  }
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -379,6 +379,11 @@ def gen_ids(ctx, seed, row0, batch, n_fields, num_rows, ids_dev, stream=None, zi
                                ids_dev.ptr, stream))
 
 
+def debug_fill_lds(ctx, pattern=0x7FC00000, stream=None):
+    """Test hook: fill every CU's LDS with a 32-bit pattern (default a NaN) on the stream."""
+    check(_lib.lib.rmx_debug_fill_lds(ctx.handle, int(pattern) & 0xFFFFFFFF, stream))
+
+
 # ------------------------------------------------------------------ models ---
 class RecModel:
     """abstract class RecModel(type) -- yr/model/RecModel.scala:6-127."""

@@ -84,6 +84,7 @@ SIGNATURES = [
     ("rmx_backward_ids", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_gen_ids", c_int, [c_vp, c_u64, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp]),
     ("rmx_gen_ids_zipf", c_int, [c_vp, c_u64, c_i64, c_i32, c_i32, c_i64, ctypes.c_double, c_vp, c_vp]),
+    ("rmx_debug_fill_lds", c_int, [c_vp, ctypes.c_uint32, c_vp]),
     ("rmx_gather", c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("rmx_forward_ids", c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
     ("rmx_model_set_timing", c_int, [c_vp, c_int]),

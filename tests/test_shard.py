@@ -360,7 +360,10 @@ def test_group_exchange_forward_bitwise_equals_replicated(N, zipf, dedupe):
         ref = rmx.DeviceArray(ctx, B, np.float32)
         m.forward_ids(table, B, ids, ref)
         ctx.sync()
-        assert np.array_equal(got, ref.numpy()), r
+        rv = ref.numpy()
+        bad = np.flatnonzero(got != rv)
+        assert bad.size == 0, "rank %d: %d rows differ (first %s, max |d| %.3g)" % (
+            r, bad.size, bad[:8].tolist(), float(np.abs(got - rv).max()))
         assert sent == (len(np.unique(h_ids)) if dedupe else B * F), r
 
 
