@@ -25,7 +25,7 @@ EOF
 for part in $PARTS; do
   case $part in
     deepfm)
-      for B in 1024 4096 16384 32768 49152 65536 98304 131072; do
+      for B in 1024 4096 8192 16384 32768 49152 65536 98304 131072; do
         steps=100; [ $B -le 16384 ] && steps=400
         line deepfm_b$B --batch $B --steps $steps --warmup 20
       done ;;
