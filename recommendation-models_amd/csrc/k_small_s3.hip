@@ -33,7 +33,7 @@ constexpr int kSTW = 4;                   // max column tiles per wave (wave 0: 
 // RT row tiles of 16 samples per block (kSR samples): each weight fragment loaded feeds RT MFMA row tiles
 template <int RT>
 constexpr size_t small_lds() {
-  return sizeof(float) * (16 * RT * kSXS + 16 * RT * kSHS + kSW * 16 * RT + 3 * kSN + 16 * RT) +
+  return sizeof(float) * (16 * RT * kSXS + 16 * RT * kSHS + kSW * 16 * RT + 3 * kSN + 16 * RT + 16 * RT * kSMaxF) +
          sizeof(int) * 16 * RT * kSMaxF;
 }
 static_assert(small_lds<2>() <= 160 * 1024, "LDS budget");
@@ -51,15 +51,27 @@ struct SmallArgs {
   OutArgs oa;             // wo [416], bo, beta, out (pre: ignored -- the first order + FM are computed here)
 };
 
+// the wave's weight fragments of K step c (tiles w + 8 j, three planes; lane: 16 B of each 1-KiB fragment)
+template <int NTW>
+__device__ __forceinline__ void s_ldw(const bf16_t* __restrict__ W, int c, int w, int wo, f32x4 (&b)[NTW][3]) {
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      b[j][pl] = *reinterpret_cast<const f32x4*>(W + ((int64_t)(c * 3 + pl) * kSN + 16 * (w + 8 * j)) * 32 + wo);
+}
+
 // one layer: acc[j] (column tile w + 8 j) = sum over K steps of W_t x^T on the split planes, x from LDS
-// (row stride XS floats); weight fragments of step c + 1 loaded during step c.  PAD (the 400-wide
+// (row stride XS floats); weight fragments of step c + 1 loaded during step c.  bp: on entry step 0's
+// fragments (loaded by the caller, ahead of the barriers before the layer); on exit, when Wn is not null,
+// the next layer's step 0, loaded during this layer's last step.  PAD (the 400-wide
 // layers): the upper half of the last step, columns 400 .. 415, is K padding that no wave writes (25 of
 // the 26 tiles are computed) -- read as zeros, as the tails do: its weights are zero, but the LDS there
 // holds whatever an earlier workgroup left, and 0 x a leftover NaN / Inf is NaN, which ReLU turns into a
 // silently wrong 0 (seen as one wrong row in some blocks, depending on what ran before on the CU)
 template <int NTW, int RT, bool PAD>
 __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const float* xin, int xs, int KS, int w, int lane,
-                                        f32x4 (&acc)[RT][kSTW]) {
+                                        f32x4 (&acc)[RT][kSTW], f32x4 (&bp)[NTW][3], const bf16_t* __restrict__ Wn) {
   const int g = lane >> 4, r16 = lane & 15;
 #pragma unroll
   for (int t = 0; t < RT; ++t)
@@ -67,19 +79,18 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
     for (int j = 0; j < kSTW; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int wo = r16 * 32 + g * 8;  // lane's element of a fragment
   asm volatile("" : "+v"(wo));
-  auto ldw = [&](int c, f32x4 (&b)[NTW][3]) {
-#pragma unroll
-    for (int j = 0; j < NTW; ++j)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        b[j][pl] = *reinterpret_cast<const f32x4*>(W + ((int64_t)(c * 3 + pl) * kSN + 16 * (w + 8 * j)) * 32 + wo);
-  };
   f32x4 b0[NTW][3], b1[NTW][3];  // (two named buffers: a [2][..] array indexed by c & 1 went to scratch)
-  ldw(0, b0);
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) b0[j][pl] = bp[j][pl];
   int xo = r16 * xs + 4 * g;
   asm volatile("" : "+v"(xo));
   auto step = [&](int c, f32x4 (&cur)[NTW][3], f32x4 (&nxt)[NTW][3]) {
-    if (c + 1 < KS) ldw(c + 1, nxt);
+    if (c + 1 < KS)
+      s_ldw<NTW>(W, c + 1, w, wo, nxt);
+    else if (Wn)
+      s_ldw<NTW>(Wn, 0, w, wo, nxt);
     bf16x8 ah[RT], am[RT], al[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -110,6 +121,12 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
     step(c, b0, b1);
     if (c + 1 < KS) step(c + 1, b1, b0);
   }
+  // the last step (KS - 1) loaded the next layer's step 0 into b1 when it was an even step, else into b0
+  const bool odd = (KS & 1) != 0;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) bp[j][pl] = odd ? b1[j][pl] : b0[j][pl];
 }
 
 // ReLU(acc + b) of the wave's tiles into the activation tile (lane: row r16, columns 16 t + 4 g .. + 3)
@@ -130,22 +147,88 @@ __device__ __forceinline__ void s_store_h(const f32x4 (&acc)[RT][kSTW], const fl
   }
 }
 
+// the whole block (every wave runs it, NTW = the wave's tile count): layer 1's first weight fragments are
+// requested before the prologue (ids, the gathered rows, the first-order weights, FM), so their latency
+// overlaps it; each layer's last K step requests the next layer's first fragments.
 template <int NTW, int RT>
-__device__ void s_wave(const SmallArgs& p, float* x, float* h, float* prm, float* red, int w, int lane) {
+__device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lane) {
   constexpr int kSR = 16 * RT;
+  float* x = ssmem;                       // [kSR][kSXS] gathered rows; later layer 2's output
+  float* h = x + kSR * kSXS;              // [kSR][kSHS] layer 1's output
+  float* red = h + kSR * kSHS;            // [8 waves][kSR] partial logits
+  float* prm = red + kSW * kSR;           // b1 | b2 | b3
+  float* fmv = prm + 3 * kSN;             // [kSR] first order + FM (y1 + y2) per sample
+  float* swt = fmv + kSR;                 // [kSR][F] first-order weights of the ids
+  int* sid = reinterpret_cast<int*>(swt + kSR * kSMaxF);  // [kSR][F] ids
   const int g = lane >> 4, r16 = lane & 15;
+  const int m0 = blockIdx.x * kSR, F = p.F;
+  f32x4 bp[NTW][3];
+  {
+    int wo = r16 * 32 + g * 8;
+    asm volatile("" : "+v"(wo));
+    s_ldw<NTW>(p.W[0], 0, w, wo, bp);
+  }
+  for (int i = tid; i < 3 * kSN; i += kSThreads) {
+    const int a = i / kSN, n = i - a * kSN;
+    const float* src = a == 0 ? p.b[0] : (a == 1 ? p.b[1] : p.b[2]);  // (no dynamic index into the kernel args)
+    prm[i] = src ? src[n] : 0.f;
+  }
+  for (int i = tid; i < kSR * F; i += kSThreads) {
+    const int r = i / F, m = m0 + r;
+    sid[i] = m < p.M ? p.ids[(int64_t)m * F + (i - r * F)] : -1;
+  }
+  __syncthreads();
+  // the gathered rows: x[r][16 f + j] (fields past F and rows past M: zero); the first-order weights
+  for (int i = tid; i < kSR * kSMaxF * 4; i += kSThreads) {
+    const int r = i / (kSMaxF * 4), rest = i - r * (kSMaxF * 4), f = rest >> 2, q = rest & 3;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f < F) {
+      const int id = sid[r * F + f];
+      if (id >= 0) v = *reinterpret_cast<const float4*>(p.table + ((int64_t)id << p.gsh) + 4 * q);
+    }
+    *reinterpret_cast<float4*>(x + r * kSXS + 16 * f + 4 * q) = v;
+  }
+  for (int i = tid; i < kSR * F; i += kSThreads) {
+    const int id = sid[i];
+    swt[i] = id >= 0 ? p.wtab[(int64_t)id << p.wsh] : 0.f;
+  }
+  __syncthreads();
+  // first order + FM of sample r (16 lanes per sample, lane j of the group: column j; wave w takes samples
+  // 4 w .. 4 w + 3, then + 32), in encoder_k16_kernel<1>'s order: s_j, q_j over the fields in order,
+  // a = sum_j (s_j^2 - q_j) in j order, y1 = the first-order weights summed in field order
+  {
+#pragma clang fp contract(off)
+    for (int rr = 4 * w; rr < kSR; rr += 4 * kSW) {
+      const int r = rr + (lane >> 4), j = lane & 15;
+      float s = 0.f, q = 0.f;
+      for (int f = 0; f < F; ++f) {
+        const float e = x[r * kSXS + 16 * f + j];
+        s = s + e;
+        q = q + e * e;
+      }
+      const float d = s * s - q;
+      float a = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) a += __shfl(d, (lane & 48) + jj);
+      float y1 = 0.f;
+      for (int f = 0; f < F; ++f) y1 += swt[r * F + f];
+      if (j == 0) fmv[r] = y1 + 0.5f * (a / 16.0f);
+    }
+  }
+  __syncthreads();
+
   f32x4 acc[RT][kSTW];
   // layer 1: x tile (row stride kSXS) -> h
-  s_layer<NTW, RT, false>(p.W[0], x, kSXS, p.KS1, w, lane, acc);  // (x: every column written)
+  s_layer<NTW, RT, false>(p.W[0], x, kSXS, p.KS1, w, lane, acc, bp, p.W[1]);  // (x: every column written)
   s_store_h<NTW, RT>(acc, prm, h, w, lane);
   __syncthreads();
   // layer 2: h -> the x region (stride kSHS)
-  s_layer<NTW, RT, true>(p.W[1], h, kSHS, 13, w, lane, acc);
+  s_layer<NTW, RT, true>(p.W[1], h, kSHS, 13, w, lane, acc, bp, p.W[2]);
   __syncthreads();  // every wave has read h ... (the x region is free since layer 1)
   s_store_h<NTW, RT>(acc, prm + kSN, x, w, lane);
   __syncthreads();
   // layer 3 + the output dot over the wave's columns
-  s_layer<NTW, RT, true>(p.W[2], x, kSHS, 13, w, lane, acc);
+  s_layer<NTW, RT, true>(p.W[2], x, kSHS, 13, w, lane, acc, bp, nullptr);
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     float part = 0.f;
@@ -165,71 +248,6 @@ __device__ void s_wave(const SmallArgs& p, float* x, float* h, float* prm, float
     part += __shfl_xor(part, 32);
     if (g == 0) red[w * kSR + 16 * t + r16] = part;
   }
-}
-
-template <int RT>
-__global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs p) {
-  constexpr int kSR = 16 * RT;
-  extern __shared__ __attribute__((aligned(16))) float ssmem[];
-  float* x = ssmem;                       // [kSR][kSXS] gathered rows; later layer 2's output
-  float* h = x + kSR * kSXS;              // [kSR][kSHS] layer 1's output
-  float* red = h + kSR * kSHS;            // [8 waves][kSR] partial logits
-  float* prm = red + kSW * kSR;           // b1 | b2 | b3
-  float* fmv = prm + 3 * kSN;             // [kSR] first order + FM (y1 + y2) per sample
-  int* sid = reinterpret_cast<int*>(fmv + kSR);  // [kSR][F] ids
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m0 = blockIdx.x * kSR, F = p.F;
-  for (int i = tid; i < 3 * kSN; i += kSThreads) {
-    const int a = i / kSN, n = i - a * kSN;
-    const float* src = a == 0 ? p.b[0] : (a == 1 ? p.b[1] : p.b[2]);  // (no dynamic index into the kernel args)
-    prm[i] = src ? src[n] : 0.f;
-  }
-  for (int i = tid; i < kSR * F; i += kSThreads) {
-    const int r = i / F, m = m0 + r;
-    sid[i] = m < p.M ? p.ids[(int64_t)m * F + (i - r * F)] : -1;
-  }
-  __syncthreads();
-  // the gathered rows: x[r][16 f + j] (fields past F and rows past M: zero)
-  for (int i = tid; i < kSR * kSMaxF * 4; i += kSThreads) {
-    const int r = i / (kSMaxF * 4), rest = i - r * (kSMaxF * 4), f = rest >> 2, q = rest & 3;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (f < F) {
-      const int id = sid[r * F + f];
-      if (id >= 0) v = *reinterpret_cast<const float4*>(p.table + ((int64_t)id << p.gsh) + 4 * q);
-    }
-    *reinterpret_cast<float4*>(x + r * kSXS + 16 * f + 4 * q) = v;
-  }
-  __syncthreads();
-  // first order + FM of sample r (16 lanes per sample, lane j of the group: column j; wave w takes samples
-  // 4 w .. 4 w + 3, then + 32), in encoder_k16_kernel<1>'s order: s_j, q_j over the fields in order,
-  // a = sum_j (s_j^2 - q_j) in j order
-  {
-#pragma clang fp contract(off)
-    for (int rr = 4 * w; rr < kSR; rr += 4 * kSW) {
-      const int r = rr + (lane >> 4), j = lane & 15;
-      float s = 0.f, q = 0.f;
-      for (int f = 0; f < F; ++f) {
-        const float e = x[r * kSXS + 16 * f + j];
-        s = s + e;
-        q = q + e * e;
-      }
-      const float d = s * s - q;
-      float a = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) a += __shfl(d, (lane & 48) + jj);
-      float y1 = 0.f;
-      for (int f = 0; f < F; ++f) {
-        const int id = sid[r * F + f];
-        y1 += id >= 0 ? p.wtab[(int64_t)id << p.wsh] : 0.f;
-      }
-      if (j == 0) fmv[r] = y1 + 0.5f * (a / 16.0f);
-    }
-  }
-  __syncthreads();
-  if (w == 0)
-    s_wave<4, RT>(p, x, h, prm, red, w, lane);
-  else
-    s_wave<3, RT>(p, x, h, prm, red, w, lane);
   __syncthreads();
   if (tid < kSR) {
     const int m = m0 + tid;
@@ -244,6 +262,16 @@ __global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs 
       oa.out[m] = 1.0f / (1.0f + expf(-t));
     }
   }
+}
+
+template <int RT>
+__global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float ssmem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (w == 0)
+    s_wave<4, RT>(p, ssmem, tid, w, lane);
+  else
+    s_wave<3, RT>(p, ssmem, tid, w, lane);
 }
 
 }  // namespace
