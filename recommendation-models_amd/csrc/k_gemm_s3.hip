@@ -258,6 +258,24 @@ int launch_cin_s3(hipStream_t s, GemmArgs& p) {
   p.nt_store = tuning_get("gemm_nt_store", 0);
   if (var == 1) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 3>, kCinOuter, kEpiCin, kPrecS3>(s, p);
   if (var == 2) {
+    // knob "cin_narrow" (default 1): when the 256-row blocks would leave CUs idle (B * k rows < 256 CUs x
+    // 256: xDeepFM below B = 4,096), the largest of 128-, 64- and 32-row blocks that still gives every
+    // CU one (MT = 1, 8 / 4 / 2 waves).  Each block then streams all of C_l's planes for fewer rows, but
+    // every CU does.  Same products in the same K order (bitwise).  xDeepFM at B = 1,024: CIN layers 2 / 3
+    // 0.735 -> 0.301 ms, 0.61 -> 1.38 M examples/s; B = 2,048: 1.21 -> 1.99 M (profiles/r04/ab_cin_narrow.txt)
+    if (tuning_get("cin_narrow", 1) != 0 && tuning_get("s3_stagger", 1) != 2) {
+      int dev = 0, ncu = 256;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        ncu = 256;
+      const int64_t nslice = p.Npad / (kS3NT * 16);
+      auto blocks = [&](int rows) { return (int64_t)(p.M + rows - 1) / rows * nslice; };
+      if (blocks(256) < ncu) {
+        if (blocks(128) >= ncu) return launch_cfg<Tile<1, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+        if (blocks(64) >= ncu) return launch_cfg<Tile<1, kS3NT, 4, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+        return launch_cfg<Tile<1, kS3NT, 2, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
+      }
+    }
     if (tuning_get("s3_stagger", 1) == 2)
       return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2, 1>, kCinOuter, kEpiCin, kPrecS3>(s, p);
     return launch_cfg<Tile<2, kS3NT, 8, 1, 1, 2, 2>, kCinOuter, kEpiCin, kPrecS3>(s, p);
