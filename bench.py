@@ -136,9 +136,6 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * (k1 * FC[0] + FC[0] * FC[1] + FC[1] * FC[2] + FC[2])
     if stage == "tower_tail":  # layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip, k_tail_s3.hip)
         return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
-    if stage == "cin":  # the whole CIN stack in one launch (csrc/k_cin_row.hip)
-        hps = [F] + CIN[:-1]
-        return "flop", sum(2.0 * B * K * F * hp * h for hp, h in zip(hps, CIN))
     if stage.startswith("cin_layer"):
         idx = {"cin_layer1": 0, "cin_layer2": 1, "cin_layer3+": 2}[stage]
         hp = F if idx == 0 else CIN[idx - 1]

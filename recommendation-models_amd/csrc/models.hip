@@ -456,8 +456,6 @@ void model_release(rmx_model& m) {
   dev_free(m.cross_b);
   dev_free(m.wo_x);
   dev_free(m.pairs);
-  pnn_head_release(m.pnn);
-  cin_row_release(m.cinrow);
   dev_free(m.h[0]);
   dev_free(m.h[1]);
   dev_free(m.y12);
@@ -497,7 +495,6 @@ static int copy_slice(hipStream_t s, const float* src, int n, int npad, float* d
 int model_set_precision(rmx_model& m, int dtype) {
   RMX_HIP(hipSetDevice(m.ctx->device));
   RMX_HIP(hipStreamSynchronize(m.ctx->stream));
-  pnn_head_release(m.pnn);
   for (auto& L : m.layers) {
     dev_free(L.W);
     dev_free(L.W16);
@@ -539,10 +536,6 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
     if (L.W3 && (st = launch_pack_split3(s, L.W, L.Kpad / kChunk, L.Npad, L.W3))) return st;
     if (L.WT && (st = launch_pack_linear_t(s, m.mats_dev, L))) return st;
   }
-  // PNN bf16 at k = 16: layer 1's weights in the on-chip-product kernel's K order (k_pnn_head.hip)
-  if (m.type == RMX_MODEL_PNN && m.precision == kBF16 && m.k == 16 && m.layers.size() > 1 &&
-      (st = pnn_head_prepare(s, m.mats_dev, m.layers[0], m.F, m.pnn)))
-    return st;
   if (!m.layers.empty()) {
     const auto& last = m.layers.back();
     if ((st = copy_slice(s, m.mats_dev + m.wo_off, last.N, last.Npad, m.wo))) return st;
@@ -559,8 +552,6 @@ int model_load_mats(rmx_model& m, const float* host_mats, bool sync) {
     if ((st = copy_slice(s, m.mats_dev + c.b_off, c.H, c.Npad, c.b))) return st;
     if ((st = copy_slice(s, m.mats_dev + c.wo_off, c.H, c.Npad, c.wo))) return st;
   }
-  // xDeepFM fp32: the CIN stack's weights for the row-owner kernel (k_cin_row.hip)
-  if (!m.cin_layers.empty() && m.precision == kF32 && (st = cin_row_prepare(s, m.mats_dev, m, m.cinrow))) return st;
   if (m.type == RMX_MODEL_DCN) {
     const int D = m.F * m.k;
     if (m.cross_depth <= kMaxFusedCross) {
@@ -761,11 +752,6 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // (k_head_s3.hip; knob "s3_head")
   const bool head_s3 = deepfm && in.ids && !in.y1 && gather_first && in.dtype == kF32 && k == 16 &&
                        m.layers.size() > 1 && tower_head_s3_usable(m.layers[0], B, F, k, true);
-  // bf16 towers with a gathered k = 16 layer 1 (DCN: the cross dots ride as raw columns): the row-owner
-  // layer 1 (k_head_bf16.hip; knob "bf16_head")
-  const bool head_bf16 = !deepfm && m.type != RMX_MODEL_PNN && m.type != RMX_MODEL_XDEEPFM && in.ids && !in.y1 &&
-                         gather_first && in.dtype == kBF16 && m.precision == kBF16 && k == 16 && m.layers.size() > 1 &&
-                         tower_head_bf16_usable(m.layers[0], B, F, k, true);
   const bool fm_add = !head_s3 && fm_fused && deepfm &&
                       (fm_y1 == 0 || (fm_y1 == 2 && !tower_wring(m.layers[0], B, &ga)));
   if (fm_add) {
@@ -801,16 +787,8 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   oa.part = m.opart;
   const float* A = nullptr;
   int lda = 0;
-  size_t i0 = 0;  // first tower layer the loop below runs
-  const bool pnn_head = m.type == RMX_MODEL_PNN && in.ids && !in.y1 && in.dtype == kBF16 && m.precision == kBF16 &&
-                        m.layers.size() > 1 && pnn_head_usable(m.pnn, m.layers[0], B, F, k, true);
 
-  if (m.type == RMX_MODEL_XDEEPFM && in.dtype == kF32 && cin_row_usable(m.cinrow, m, B, in.ids != nullptr)) {
-    StageTimer t(m, s, "cin");
-    if ((st = launch_cin_row(s, m.cinrow, m, B, in.ids, (const float*)in.table, m.rowdot))) return st;
-    oa.rowsum = m.rowdot;
-    oa.rowsum_k = k;
-  } else if (m.type == RMX_MODEL_XDEEPFM) {
+  if (m.type == RMX_MODEL_XDEEPFM) {
     const float* uprev = nullptr;
     for (size_t l = 0; l < m.cin_layers.size(); ++l) {
       StageTimer t(m, s, l == 0 ? "cin_layer1" : (l == 1 ? "cin_layer2" : "cin_layer3+"));
@@ -831,16 +809,6 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
         return st;
     }
     oa.pre2 = m.pre2;
-  } else if (m.type == RMX_MODEL_PNN && pnn_head) {
-    // layer 1 with the products generated on chip: [x | ip] never reaches HBM (k_pnn_head.hip)
-    StageTimer t(m, s, "tower_layer1");
-    if ((st = launch_pnn_head(s, m.pnn, m.layers[0], B, F, in.ids, (const bf16_t*)in.table,
-                              reinterpret_cast<bf16_t*>(m.h[0]), m.layers[0].Npad)))
-      return st;
-    A = m.h[0];
-    lda = m.layers[0].Npad;
-    gather_first = false;
-    i0 = 1;
   } else if (m.type == RMX_MODEL_PNN) {
     StageTimer t(m, s, "product");
     if ((st = launch_product(s, B, F, k, in.ids, in.table, in.dtype, m.pairs, F * (F - 1) / 2, m.xbuf, m.precision,
@@ -860,7 +828,7 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
 
   // 3. tower (the last layer runs the output head: dot + bias + CAddTable + Sigmoid)
   static const char* names[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
-  for (size_t i = i0; i < m.layers.size(); ++i) {
+  for (size_t i = 0; i < m.layers.size(); ++i) {
     const bool last = i + 1 == m.layers.size();
     const DenseLayer& L = m.layers[i];
     // bf16: the last hidden layer and the output layer in one persistent kernel (k_tail.hip)
@@ -878,17 +846,6 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     }
     float* C = m.h[i & 1];
     StageTimer t(m, s, names[std::min<size_t>(i, 3)]);
-    if (i == 0 && head_bf16) {
-      XColArgs xc{m.xcol, L.N1, m.cross_depth + 1};
-      if ((st = launch_tower_head_bf16(s, L, B, F, in.ids, (const bf16_t*)in.table, in.ld, (const bf16_t*)in.wtab,
-                                       in.wld, reinterpret_cast<bf16_t*>(C), L.Npad, m.dcn_fused ? &xc : nullptr,
-                                       fm_fused ? m.y12 : nullptr)))
-        return st;
-      if (m.dcn_fused && (st = launch_cross_finish(s, B, m.cross_depth, m.xcol, m.cross_scalars, m.pre2))) return st;
-      A = C;
-      lda = L.Npad;
-      continue;
-    }
     if (i == 0 && head_s3) {
       if ((st = launch_tower_head_s3(s, L, B, F, in.ids, (const float*)in.table, in.ld, (const float*)in.wtab, in.wld, C,
                                      L.Npad, m.y12, 1)))

@@ -140,25 +140,6 @@ int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer
 bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids);
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
                          int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums);
-// bf16 tower layer 1 (DCN: + the cross dots as raw columns N1 .. into xc, + first order) as a row-owner
-// kernel (k_head_bf16.hip): H [M][416] bf16
-bool tower_head_bf16_usable(const DenseLayer& L1, int M, int F, int k, bool ids);
-int launch_tower_head_bf16(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const bf16_t* table,
-                           int ld, const bf16_t* wtab, int wld, bf16_t* H, int ldc, const XColArgs* xc, float* fm_y);
-// PNN bf16 tower layer 1 with the inner products generated on chip (k_pnn_head.hip): the layer's weights in
-// the kernel's K order and its per-unit DMA schedule, built at set_mats
-struct PnnHead {
-  bf16_t* W = nullptr;       // [KS][416][32]
-  int32_t* quads = nullptr;  // [(KS - KSX) * 8] i | j0 << 8
-  int32_t* sched = nullptr;  // [KS] per-unit row / id DMAs (+ the packing column map behind it)
-  int32_t* pro = nullptr;    // [KSX] prologue actions
-  int F = 0, KSX = 0, KS = 0;
-};
-int pnn_head_prepare(hipStream_t s, const float* mats_dev, const DenseLayer& L0, int F, PnnHead& ph);
-void pnn_head_release(PnnHead& ph);
-bool pnn_head_usable(const PnnHead& ph, const DenseLayer& L0, int M, int F, int k, bool ids);
-int launch_pnn_head(hipStream_t s, const PnnHead& ph, const DenseLayer& L0, int M, int F, const int32_t* ids,
-                    const bf16_t* table, bf16_t* H, int ldc);
 // fp32 tower tail (k_tail_s3.hip): ReLU(H L2) -> ReLU(. L3) . wo -> head on the split GEMM, one persistent
 // launch, h2 in registers; both layers 400 x 400 with split planes; H [M][lda] fp32
 bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda);

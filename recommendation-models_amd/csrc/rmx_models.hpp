@@ -79,16 +79,6 @@ struct CinLayer {
   int KTpad = 0, NTpad = 0;
 };
 
-// xDeepFM's CIN stack as one row-owner kernel (k_cin_row.hip): every layer's split weights in the kernel's
-// padded chunk order, concatenated in unit order, and the per-h-chunk unit schedule
-struct CinRow {
-  bf16_t* W = nullptr;   // [S][3][208][32]
-  float* bw = nullptr;   // [L][2][208]: b_l | wo_l
-  int S = 0, L = 0, nhc1 = 0;
-  int nu1[4] = {}, f01[4] = {}, pr1[4] = {};
-  int nu2[13] = {}, f02[13] = {}, pr2[13] = {};
-};
-
 }  // namespace rmx
 
 struct rmx_model {
@@ -109,7 +99,6 @@ struct rmx_model {
   float bo = 0.f;
   bool has_bo = false;
   std::vector<rmx::CinLayer> cin_layers;    // xDeepFM
-  rmx::CinRow cinrow;                       // xDeepFM: the CIN stack as one row-owner kernel
   int64_t wo_cin_off = -1;                  // start of the pooled-CIN slice of W_out
   int64_t cross_w_off = -1, cross_b_off = -1, wo_x_off = -1;  // DCN
   float* cross_w = nullptr;                 // [L][D]
@@ -119,7 +108,6 @@ struct rmx_model {
   rmx::CrossScalars cross_scalars{};
   float* xcol = nullptr;                    // [B][L + 1] raw fused cross dots
   int32_t* pairs = nullptr;                 // PNN (row, col) pairs [P][2]
-  rmx::PnnHead pnn;                         // PNN bf16: layer 1 with on-chip products (k_pnn_head.hip)
   int precision = 0;                        // kF32 / kBF16 (rmx_model_set_precision)
   bool params_ready = false;
   float beta = 0.f;
@@ -269,10 +257,4 @@ bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids);
 int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,
                           int ld, const float* wtab, int wld, const OutArgs& oa);
 int cin_npad_for(int H);
-// xDeepFM's CIN stack in one launch (k_cin_row.hip): rowdot [B * 16] of every layer
-int cin_row_prepare(hipStream_t s, const float* mats_dev, const rmx_model& m, CinRow& cr);
-void cin_row_release(CinRow& cr);
-bool cin_row_usable(const CinRow& cr, const rmx_model& m, int B, bool ids);
-int launch_cin_row(hipStream_t s, const CinRow& cr, const rmx_model& m, int B, const int32_t* ids, const float* table,
-                   float* rowdot);
 }  // namespace rmx
