@@ -243,8 +243,9 @@ struct EpiGeom {
 // With the builtin the compiler counts the DMA as an LGKM event of unknown order, so every later wait for
 // an LDS read becomes lgkmcnt(0) and drains the prefetched fragments (checked on gfx950 ISA); hidden in
 // asm, the reads keep their counted waits.  The kernels that use it order the DMAs themselves (explicit
-// vmcnt waits + barriers), issue no compiler-visible vector-memory loads in their loops, and keep no value
-// in M0 (every DMA sets it).
+// vmcnt waits + barriers) and issue no compiler-visible vector-memory loads in their loops.  M0 is an asm
+// operand ("{m0}"): the compiler writes it before the asm and knows it holds the LDS address after it
+// (a hand-written s_mov_b32 m0 inside the asm was invisible to the register allocator).
 #ifndef RMX_LDS_DMA_BUILTIN
 #define RMX_LDS_DMA_BUILTIN 0  // (1: the builtin, timing A/B builds only)
 #endif
@@ -264,11 +265,11 @@ __device__ __forceinline__ void lds_dma(const void* src, const void* dst) {
   // check tripped an instruction-selection bug, "V_CMP_NE_U32 ... src_shared_base")
   const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<uintptr_t>(dst));
   if constexpr (BYTES == 16)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(a), "v"(src) : "memory");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(a) : "memory");
   else if constexpr (BYTES == 4)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(a), "v"(src) : "memory");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "{m0}"(a) : "memory");
   else
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off" ::"s"(a), "v"(src) : "memory");
+    asm volatile("s_nop 0\n\tglobal_load_lds_ushort %0, off" ::"v"(src), "{m0}"(a) : "memory");
 }
 
 // x (8 fp32 as two float4) = hi + mid + lo exactly, each a bf16x8 (kPrecS3)
