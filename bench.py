@@ -249,6 +249,37 @@ def parity_check(workload, got, row0, n=512, vocab=V, ids_host=None):
     return {"rows": n, "row0": row0, "max_abs_diff": err, "tol": tol, "against": against, "ok": err <= tol}
 
 
+# exit status of a rank whose line reports a failed check (after the line is printed): the driver and
+# launch_ranks see it, not only a string inside the line
+STATUS_PARITY_MISS = 5
+STATUS_COMPANION_FAILED = 6
+
+
+def _pc_ok(p):
+    """one rank's parity record: {"ok": ...} or {"deepfm": {...}, "xdeepfm": {...}}"""
+    if p is None:
+        return True
+    return p["ok"] if "ok" in p else all(q["ok"] for q in p.values())
+
+
+def job_status(parity_ranks=None, sub=None, cpu=None, cpu2=None):
+    """The status every rank exits with once the line is out: STATUS_PARITY_MISS when any rank's rows missed
+    the oracle (the main workload, its xDeepFM companion or the sharded sub-record), STATUS_COMPANION_FAILED
+    when the sharded sub-record raised (its watchdog exits 124 itself), else 0.  parity_ranks and the
+    sub-record's checks are gathered over the ranks, so every rank computes the same status."""
+    if parity_ranks and not all(_pc_ok(p) for p in parity_ranks):
+        return STATUS_PARITY_MISS
+    for c in (cpu, cpu2):
+        if c and c.get("parity_check") and not c["parity_check"]["ok"]:
+            return STATUS_PARITY_MISS
+    if sub is not None:
+        if "error" in sub:
+            return STATUS_COMPANION_FAILED
+        if not sub.get("parity_ok", True):
+            return STATUS_PARITY_MISS
+    return 0
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -839,7 +870,7 @@ def main():
             "roofline": r["roofline"],
             "cpu_baseline": cpu,
             **({"parity_check_ranks": parity_ranks,
-                "parity_ok": all(p["ok"] if "ok" in p else all(q["ok"] for q in p.values()) for p in parity_ranks)}
+                "parity_ok": all(_pc_ok(p) for p in parity_ranks)}
                if parity_ranks else {}),
             **({"predict_auc": r["predict_auc"]} if r.get("predict_auc") else {}),
             **({"auc": r["auc"]} if "auc" in r else {}),
@@ -867,15 +898,24 @@ def main():
     # exchange per batch, as a sub-record of the default line -- so the driver's multi-GPU runs execute
     # and check the exchange.  A watchdog bounds it: past --companion-timeout it aborts the RCCL
     # communicator, prints the line with the sub-record marked as timed out and ends the process.
+    sub = None
     if (args.workload == "deepfm" and not args.no_companion and not args.no_sharded_companion and not args.zipf
             and ((world > 1 and world <= ndev) or args.sharded_companion)):
         sub = sharded_companion(args, rmx, ctx, rank, world, dist, line if rank == 0 else None)
         if rank == 0:
             line.setdefault("models", {})["deepfm_sharded"] = sub
+    status = job_status(parity_ranks, sub, cpu, cpu2)
     if rank == 0:
+        if status:
+            line["status"] = {"exit": status, "reason": "parity miss" if status == STATUS_PARITY_MISS
+                              else "sharded sub-record failed"}
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+    if status:
+        sys.stderr.write("bench.py: rank %d exits %d (%s)\n" % (rank, status, "parity miss" if status == STATUS_PARITY_MISS
+                                                                 else "sharded sub-record failed"))
+        raise SystemExit(status)
 
 
 def sharded_companion(args, rmx, ctx, rank, world, dist, line):

@@ -251,6 +251,12 @@ int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32
  * carries its overflow flag).  The overflow check is made when the slot is consumed (or, for
  * rmx_forward_ids_sharded / rmx_shard_gather, after the forward / copy is queued, which then runs again).
  * An id outside [0, num_rows) reads a zero row on every path.
+ * An exchange that fails on a rank at nranks > 1 (e.g. out of device memory while routing) leaves that
+ * rank's collectives out of step with its peers': every later exchange on the shard returns RMX_E_COMM at
+ * once.  Abort the shard on every rank (rmx_shard_abort, then rmx_shard_destroy) and create a new one;
+ * peers already waiting in the failed exchange are released by their own abort (e.g. a watchdog).
+ * The first exchange of a shard has no agreed bucket capacity yet, so all of its ids take the counted
+ * overflow round (one extra round, once; timed under the "shard_exchange" stage).
  * CONTRACT CHANGE (round 3): the default owner function is the keyed permutation below, no longer
  * id mod nranks.  A caller that pre-partitions ids or rows must use rmx_owner_hash (or
  * rmx_shard_set_owner_hash(sh, 0) for id mod nranks). 
@@ -265,8 +271,9 @@ int rmx_shard_create(rmx_ctx* ctx, int64_t num_rows, int embedding_dim, int nran
 int rmx_shard_destroy(rmx_shard* sh);
 /* Abort the shard's RCCL communicator (ncclCommAbort) from any thread, e.g. a watchdog while an
  * exchange waits for a peer that never arrives: the pending exchange fails (or its kernels return)
- * and every later exchange returns RMX_E_COMM; only rmx_shard_destroy may follow.  Takes no lock.
- * A no-op returning RMX_OK for loopback and group shards. */
+ * and every later exchange returns RMX_E_COMM; only rmx_shard_destroy may follow.  Waits (at most 5 s)
+ * for an exchange's host-side RCCL calls in flight on another thread to finish first, so no ncclSend /
+ * ncclGroupEnd runs on the communicator while it is torn down.  A no-op returning RMX_OK for loopback and group shards. */
 int rmx_shard_abort(rmx_shard* sh);
 /* Owned rows from the same generator as rmx_table_fill_synthetic (bit-identical rows). */
 int rmx_shard_fill_synthetic(rmx_shard* sh, uint64_t seed);

@@ -173,6 +173,17 @@ struct rmx_shard {
   int32_t* recv_ovf = nullptr;
   float* ovf_emb = nullptr;
   float* ovf_w = nullptr;
+  // the overflow round runs on its slot's stream (shard_resolve), which need not be the stream of the
+  // ShardUse that called it (rmx_forward_pulled resolves outside one): the next exchange's stream waits
+  // on this event before its route rewrites send_ovf / the row scratch
+  hipEvent_t ovf_done = nullptr;
+  bool ovf_pending = false;
+  // RCCL calls between start() and end() of one grouped exchange hold this lock; rmx_shard_abort takes it
+  // (bounded wait) before ncclCommAbort, so no ncclSend / ncclGroupEnd runs on a comm being torn down
+  std::timed_mutex tr_mu;
+  // an exchange failed on this rank after or before posting part of its ops: its peers' collectives no
+  // longer pair up with this rank's, so every later exchange fails at once (abort and recreate the shard)
+  bool failed = false;
   // one exchange at a time per shard; the per-batch buffers are ordered across streams like a
   // model's workspace (rmx::ModelUse)
   std::mutex mu;
@@ -742,16 +753,30 @@ namespace {
 // Every call first checks the shard's communicator state: after rmx_shard_abort (or during destroy)
 // nothing more is posted on the torn-down communicator -- the exchange fails with RMX_E_COMM instead
 // (an abort while the exchange was in flight used to reach ncclSend on a freed comm)
+//  The check alone was check-then-act: an abort could free the comm between the check and
+// the call.  start() now takes the shard's transport lock and end() releases it, so the whole bracket --
+// check, posts, ncclGroupEnd -- runs with rmx_shard_abort held off; abort waits for the lock (bounded:
+// a host thread stuck inside an RCCL call is exactly what abort is for, RCCL's abort may then run beside it).
+// Every exchange passes start() and end() in pairs (also after a local error), so the lock is balanced.
 struct RcclTransport : Transport {
   ncclComm_t comm;
   const std::atomic<int>* state;
-  RcclTransport(ncclComm_t c, const std::atomic<int>* st) : comm(c), state(st) {}
+  std::timed_mutex* mu;
+  bool held = false;
+  RcclTransport(ncclComm_t c, const std::atomic<int>* st, std::timed_mutex* m) : comm(c), state(st), mu(m) {}
+  ~RcclTransport() override {
+    if (held) mu->unlock();
+  }
   int live() const {
     if (state->load() == 0) return RMX_OK;
     set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
     return RMX_E_COMM;
   }
   int start() override {
+    if (!held) {
+      mu->lock();
+      held = true;
+    }
     if (int e = live()) return e;
     RMX_NCCL(ncclGroupStart());
     return RMX_OK;
@@ -767,10 +792,18 @@ struct RcclTransport : Transport {
     return RMX_OK;
   }
   int end(hipStream_t) override {
-    // (a group already started is closed even after an abort: ncclGroupEnd only flushes this thread's
-    // group state; with the comm torn down the ops of the group were never posted)
+    struct Release {  // the bracket's lock, on every return
+      RcclTransport* t;
+      ~Release() {
+        if (t->held) {
+          t->held = false;
+          t->mu->unlock();
+        }
+      }
+    } rel{this};
+    // (with the lock held no abort can have run since start()'s check unless start() already failed; a
+    // group that start() opened is always closed)
     if (state->load() != 0) {
-      (void)ncclGroupEnd();
       set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
       return RMX_E_COMM;
     }
@@ -953,7 +986,7 @@ int shard_create(rmx_ctx* ctx, int64_t V, int k, int N, int rank, const void* un
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     RMX_NCCL(ncclCommInitRank(&sh->comm, N, id, rank));
-    sh->tr.reset(new RcclTransport(sh->comm, &sh->comm_state));
+    sh->tr.reset(new RcclTransport(sh->comm, &sh->comm_state, &sh->tr_mu));
   }
   *out = sh.release();
   return RMX_OK;
@@ -965,6 +998,7 @@ int shard_destroy(rmx_shard* sh) {
   (void)hipDeviceSynchronize();  // the exchange may have run on any stream
   sh->tr.reset();
   if (sh->ws_fence) (void)hipEventDestroy(sh->ws_fence);
+  if (sh->ovf_done) (void)hipEventDestroy(sh->ovf_done);
   int live = 0;  // claim the communicator: a concurrent rmx_shard_abort that got there first freed it
   if (sh->comm && sh->comm_state.compare_exchange_strong(live, 2)) ncclCommDestroy(sh->comm);
   if (sh->group) {
@@ -1222,6 +1256,14 @@ int shard_resolve(rmx_shard& sh, int slot, bool* ran = nullptr) {
   }
   keep(tr.end(s));
   if (err == RMX_OK && sh.ready[slot]) keep(hipEventRecord(sh.ready[slot], s) == hipSuccess ? RMX_OK : RMX_E_HIP);
+  // the scratch this round read (send_ovf, recv_ovf, ovf_*) is free once s passes here: the next exchange,
+  // on whatever stream, waits for it (shard_exchange)
+  if (!sh.ovf_done && hipEventCreateWithFlags(&sh.ovf_done, hipEventDisableTiming) != hipSuccess) sh.ovf_done = nullptr;
+  if (sh.ovf_done && hipEventRecord(sh.ovf_done, s) == hipSuccess)
+    sh.ovf_pending = true;
+  else
+    keep(RMX_E_HIP);
+  if (err != RMX_OK) sh.failed = true;
   return err;
 }
 
@@ -1239,13 +1281,24 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
   const int N = sh.N, k = sh.k;
   int st;
   bool dd = false;
+  if (sh.failed) {
+    set_error("shard exchange: an earlier exchange failed on this rank, so its collectives no longer pair up "
+              "with its peers'; abort the shard (rmx_shard_abort) and create a new one");
+    return RMX_E_COMM;
+  }
   if ((st = shard_resolve_all(sh))) return st;  // a pending overflow round uses the scratch below
+  if (sh.ovf_pending) {  // ... possibly on another stream
+    RMX_HIP(hipStreamWaitEvent(s, sh.ovf_done, 0));
+    sh.ovf_pending = false;
+  }
   if (fixed_eligible(sh)) {
     if (sh.comm_state.load() != 0) {
       set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
       return RMX_E_COMM;
     }
-    return shard_exchange_fixed(sh, s, nnz, d_ids, slot);
+    st = shard_exchange_fixed(sh, s, nnz, d_ids, slot);
+    if (st) sh.failed = true;
+    return st;
   }
   sh.last_fixed = -1;
   if (N == 1 && !sh.loopback && sh.dedupe != 1) {
@@ -1493,7 +1546,12 @@ extern "C" int rmx_shard_abort(rmx_shard* sh) {
   }
   int live = 0;  // claim the communicator (a destroy or an earlier abort got it first: nothing to do)
   if (!sh->comm || !sh->comm_state.compare_exchange_strong(live, 1)) return RMX_OK;
+  // no exchange bracket in flight on the host (RcclTransport): its calls finish, later brackets see the
+  // state and post nothing.  A thread blocked inside an RCCL call keeps the lock: after the bounded wait
+  // the abort goes ahead anyway, which is the case ncclCommAbort exists for.
+  const bool locked = sh->tr_mu.try_lock_for(std::chrono::seconds(5));
   const ncclResult_t r = ncclCommAbort(sh->comm);
+  if (locked) sh->tr_mu.unlock();
   if (r != ncclSuccess) {
     rmx::set_error(std::string("rmx_shard_abort: ") + ncclGetErrorString(r));
     return RMX_E_COMM;
@@ -1768,9 +1826,15 @@ extern "C" int rmx_forward_ids_sharded(rmx_model* m, rmx_shard* sh, int32_t B, c
   if (m->timing) --m->timed_calls;
   if (st) return st;
   // a fixed exchange's overflow check comes after the forward is queued (the host waits on a summary the
-  // GPU produced before the rows even moved); when the overflow round runs, the forward runs again
+  // GPU produced before the rows even moved); when the overflow round runs, the forward runs again.  The
+  // round is part of the exchange's stage (it used to fall outside every timer); the re-run
+  // forward's kernels add to their own stages, over the same call count.
   bool ran = false;
-  if ((st = shard_resolve(*sh, 0, &ran)) || !ran) return st;
+  {
+    StageTimer t(*m, s, "shard_exchange");
+    st = shard_resolve(*sh, 0, &ran);
+  }
+  if (st || !ran) return st;
   if (m->timing) ++m->timed_calls;
   st = model_forward(*m, s, in);
   if (m->timing) --m->timed_calls;

@@ -26,6 +26,22 @@ if mode == "gloo":  # a real rendezvous over the launcher's MASTER_ADDR / MASTER
     dist.all_gather_object(g, {"rank": r, "ok": True})
     env["gathered"] = g
     dist.destroy_process_group()
+if mode == "parity":  # every rank checks its rows; rank argv[2] misses -- bench.job_status decides the rc
+    import torch.distributed as dist
+    sys.path.insert(0, os.environ["BENCH_ROOT"])
+    import bench
+    dist.init_process_group("gloo")
+    bad = int(sys.argv[2])
+    pc = {"rows": 512, "max_abs_diff": 1.0 if r == bad else 5.96e-8, "tol": 1e-5, "ok": r != bad}
+    if len(sys.argv) > 3:  # the default line's shape: the DeepFM and xDeepFM records of each rank
+        pc = {"deepfm": dict(pc, ok=True), "xdeepfm": pc}
+    g = [None] * dist.get_world_size()
+    dist.all_gather_object(g, pc)
+    dist.destroy_process_group()
+    st = bench.job_status(g)
+    if r == 0:
+        print(json.dumps({"parity_ok": all(bench._pc_ok(p) for p in g)}), flush=True)
+    sys.exit(st)
 if mode == "fail" and r == int(sys.argv[2]):
     sys.exit(7)
 if mode == "fail":
@@ -60,6 +76,29 @@ def test_launcher_propagates_a_failing_rank(tmp_path, bad):
     st = bench.launch_ranks(2, ["fail", str(bad)], script=_script(tmp_path), grace_s=2.0)
     assert st == 7
     assert time.time() - t0 < 30  # the surviving rank was stopped, not waited out
+
+
+@pytest.mark.parametrize("bad,shape", [(1, "flat"), (0, "flat"), (1, "models"), (-1, "flat")])
+def test_launcher_fails_on_a_rank_parity_miss(tmp_path, bad, shape, monkeypatch, capfd):
+    """one rank's rows missing the oracle at N > 1 fail the whole job's exit status
+    (bench.STATUS_PARITY_MISS), not only a parity_ok: false inside the line; no miss exits 0."""
+    import bench
+    monkeypatch.setenv("BENCH_ROOT", ROOT)
+    argv = ["parity", str(bad)] + (["models"] if shape == "models" else [])
+    st = bench.launch_ranks(3, argv, script=_script(tmp_path), grace_s=2.0)
+    out = capfd.readouterr().out.strip().splitlines()
+    assert st == (0 if bad < 0 else bench.STATUS_PARITY_MISS)
+    assert json.loads(out[-1])["parity_ok"] == (bad < 0)
+
+
+def test_job_status_companion_and_cpu_records():
+    import bench
+    ok = {"ok": True}
+    assert bench.job_status([ok, ok]) == 0
+    assert bench.job_status([ok], {"error": "TimeoutError"}) == bench.STATUS_COMPANION_FAILED
+    assert bench.job_status([ok], {"parity_ok": False}) == bench.STATUS_PARITY_MISS
+    assert bench.job_status(None, None, {"parity_check": {"ok": False}}) == bench.STATUS_PARITY_MISS
+    assert bench.job_status(None, None, {"parity_check": {"ok": True}}, {"value": 1.0}) == 0
 
 
 def test_bench_cli_launcher_exit_status(tmp_path):

@@ -454,16 +454,20 @@ def test_group_exchange_100m_rows_vs_fp64_oracle():
 
 # ------------------------------------------- pull / forward_pulled (exchange beside forward) ----
 def _pipelined(m, sh, ids_all, B, nb, ctx, ctx_x):
-    """Batches 0..nb-1: pull(i + 1) on the exchange stream beside forward_pulled(i) on the main one."""
+    """Batches 0..nb-1: pull(i + 1) on the exchange stream beside forward_pulled(i) on the main one.
+    ctx_x may be a pair of contexts: slot q's pulls then run on ctx_x[q]'s stream (the
+    overflow round of a slot runs on that slot's stream, the next exchange on the other one)."""
     import rmx
+    xs = list(ctx_x) if isinstance(ctx_x, (list, tuple)) else [ctx_x, ctx_x]
     outs = [rmx.DeviceArray(ctx, B, np.float32) for _ in range(nb)]
-    sh.pull(ids_all.view(0, B * F), B * F, 0, ctx_x.stream)
+    sh.pull(ids_all.view(0, B * F), B * F, 0, xs[0].stream)
     for i in range(nb):
         if i + 1 < nb:
-            sh.pull(ids_all.view((i + 1) * B * F, B * F), B * F, (i + 1) % 2, ctx_x.stream)
+            sh.pull(ids_all.view((i + 1) * B * F, B * F), B * F, (i + 1) % 2, xs[(i + 1) % 2].stream)
         m.forward_pulled(sh, B, i % 2, outs[i], ctx.stream)
     ctx.sync()
-    ctx_x.sync()
+    for x in xs:
+        x.sync()
     return [o.numpy() for o in outs]
 
 
@@ -739,17 +743,20 @@ def test_rccl_single_rank_reads_partition_in_place(kind):
 
 
 # ------------------------------------ fixed-capacity exchange: overflow round, zero rows (round 4) ----
-def _group_forward_stats(kind, N, V, B, zipf, dedupe, h_ids_of=None, pipelined=False):
-    """_group_forward, also returning every rank's overflow-round count; h_ids_of(r) overrides the ids."""
+def _group_forward_stats(kind, N, V, B, zipf, dedupe, h_ids_of=None, pipelined=False, nbp=3):
+    """_group_forward, also returning every rank's overflow-round count; h_ids_of(r) overrides the ids.
+    pipelined = "alt": the pulls of the two slots on two different streams."""
     import rmx
     g = rmx.ExchangeGroup(N)
 
     def rank(r):
         ctx, ctx_x = rmx.Context(0), rmx.Context(0)
+        if pipelined == "alt":
+            ctx_x = (ctx_x, rmx.Context(0))
         sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
         sh.set_dedupe(dedupe)
         sh.fill_synthetic(SEED_TAB)
-        nb = 3 if pipelined else 1
+        nb = nbp if pipelined else 1
         ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
         if h_ids_of is not None:
             ids.upload(h_ids_of(r))
@@ -819,6 +826,27 @@ def test_fixed_exchange_overflow_round_bitwise(N, zipf, cap_pct, pipelined):
     if cap_pct < 100:
         assert rounds == {n_ex}
     nb = 3 if pipelined else 1
+    for r, (got, h_ids, _) in enumerate(outs):
+        ref = _replicated("deepfm", V, h_ids, B, nb)
+        for i in range(nb):
+            assert np.array_equal(got[i], ref[i]), (r, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [2, 4])
+def test_fixed_exchange_overflow_round_alternating_pull_streams(N):
+    """every bucket overflows (shard_cap_pct 30), so every exchange runs its overflow round on its
+    slot's stream -- and the two slots' pulls run on two different streams.  The next exchange's route
+    rewrites the overflow scratch the previous round sends from; it must wait for that round (the shard's
+    ovf_done event).  Every forward stays bitwise the replicated table's."""
+    import rmx
+    V, B, nb = 100_003, 1000, 6
+    rmx.set_tuning("shard_cap_pct", 30)
+    try:
+        outs = _group_forward_stats("deepfm", N, V, B, 0.0, False, pipelined="alt", nbp=nb)
+    finally:
+        rmx.set_tuning("shard_cap_pct", None)
+    assert {o[2] for o in outs} == {nb}
     for r, (got, h_ids, _) in enumerate(outs):
         ref = _replicated("deepfm", V, h_ids, B, nb)
         for i in range(nb):
