@@ -34,6 +34,11 @@ sys.path.insert(0, os.path.join(ROOT, "recommendation-models_amd"))
 F, K, V = 39, 16, 1_000_000
 FC = [400, 400, 400]
 CIN = [200, 200, 200]
+CIN1 = [200]  # xdeepfm_cin1: the only CIN the reference can run (CINEncoder.scala:150-176; L > 1 mis-shapes)
+
+
+def cin_of(workload):
+    return CIN1 if workload.startswith("xdeepfm_cin1") else CIN
 ROWS = 1 << 20  # the "1M-row synthetic" set
 SEED_IDS, SEED_TAB, SEED_MATS, SEED_LAB = 0x5EED2026, 0x7AB1E, 0x3A75, 0x1AB3
 PLUMB_ROWS, PLUMB_BATCH = 1000, 100  # configs[0]: 1k-row LIBSVM slice, batchSize 100 (LRLocalExample.scala:16)
@@ -55,9 +60,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "deepfm_sharded", "dcn_bf16", "pnn_bf16",
-                                           "deepfm_train", "xdeepfm_train", "lr_plumbing"],
+    ap.add_argument("--workload", choices=["deepfm", "xdeepfm", "xdeepfm_cin1", "deepfm_sharded", "dcn_bf16",
+                                           "pnn_bf16", "deepfm_train", "xdeepfm_train", "lr_plumbing", "encoder"],
                     default="deepfm")
+    ap.add_argument("--no-encoder-record", action="store_true",
+                    help="deepfm: skip the encoder sub-record (gather + first order + FM alone at V = 1M and 100M)")
     ap.add_argument("--no-companion", action="store_true",
                     help="deepfm: skip the xDeepFM sub-record (BASELINE.json's metric names both models)")
     ap.add_argument("--no-sharded-companion", action="store_true",
@@ -121,9 +128,10 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 4.0 * B * FC[0] * FC[1]
     if stage == "tower_back3":
         return "flop", 4.0 * B * FC[1] * FC[2]
+    cin = cin_of(workload)
     if stage == "cin_back":  # dC_l and dZ_l GEMMs of every CIN layer
-        hps = [F] + CIN[:-1]
-        return "flop", sum(4.0 * B * K * F * hp * h for hp, h in zip(hps, CIN))
+        hps = [F] + cin[:-1]
+        return "flop", sum(4.0 * B * K * F * hp * h for hp, h in zip(hps, cin))
     if stage == "gather_x":
         return "byte", B * (F * 4 + F * K * es + D * 4)
     if stage == "tower_layer1":
@@ -138,8 +146,8 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
     if stage.startswith("cin_layer"):
         idx = {"cin_layer1": 0, "cin_layer2": 1, "cin_layer3+": 2}[stage]
-        hp = F if idx == 0 else CIN[idx - 1]
-        return "flop", 2.0 * B * K * F * hp * CIN[idx]
+        hp = F if idx == 0 else cin[idx - 1]
+        return "flop", 2.0 * B * K * F * hp * cin[idx]
     return None, 0
 
 
@@ -151,7 +159,7 @@ def _oracle():
 
 def _oracle_model(oc, workload):
     if workload.startswith("xdeepfm"):
-        return oc.make_model(oc.XDEEPFM, F, K, fc=tuple(FC), cin=tuple(CIN))
+        return oc.make_model(oc.XDEEPFM, F, K, fc=tuple(FC), cin=tuple(cin_of(workload)))
     if workload == "dcn_bf16":
         return oc.make_model(oc.DCN, F, K, fc=tuple(FC), cross_depth=3)
     if workload == "pnn_bf16":
@@ -169,7 +177,7 @@ def cpu_baseline(workload, budget_s, threads):
     om = _oracle_model(oc, workload)
     # the oracle parallelises over 8-row blocks (oracle/rmx_oracle.c RB): xDeepFM (~45 rows/s per thread)
     # takes 8 rows per thread per batch so every thread has a block
-    B = 8 * max(threads, 1) if workload == "xdeepfm" else 4096
+    B = 8 * max(threads, 1) if workload == "xdeepfm" else (64 * max(threads, 1) if workload == "xdeepfm_cin1" else 4096)
     mats = oc.init_mats(om, SEED_MATS)
     done, t_tot, row0 = 0, 0.0, 0
     wt, et = oc.gen_table(SEED_TAB, V, K)
@@ -229,6 +237,8 @@ def parity_check(workload, got, row0, n=512, vocab=V, ids_host=None):
     om = _oracle_model(oc, workload)
     if workload == "xdeepfm":
         n = min(n, 64)
+    if workload == "xdeepfm_cin1":
+        n = min(n, 256)
     mats = oc.init_mats(om, SEED_MATS)
     # (ids_host: the bench's own ids read back, e.g. the Zipf(1.1) set, which the oracle has no generator for)
     ids = (ids_host[:n * F] if ids_host is not None else oc.gen_ids(SEED_IDS, row0, n, F, vocab)).astype(np.int64)
@@ -345,8 +355,8 @@ def cpu_baseline_sweep(workload, budget_s, short=False):
 
 def make_model(rmx, workload, Vw, ctx):
     base = workload[:-len("_train")] if workload.endswith("_train") else workload
-    if base == "xdeepfm":
-        return rmx.XDeepFM(Vw, F, K, FC, CIN, ctx=ctx)
+    if base in ("xdeepfm", "xdeepfm_cin1"):
+        return rmx.XDeepFM(Vw, F, K, FC, cin_of(base), ctx=ctx)
     if base == "dcn_bf16":  # configs[4]: DCN depth 3 + fcDims 400^3, bf16 table / weights
         return rmx.DCN(Vw, F, K, 3, FC, ctx=ctx)
     if base == "pnn_bf16":  # configs[4]: PNN (IPNN) D1 = 400, fcDims 400^3, bf16
@@ -420,6 +430,97 @@ def max_over_ranks(dist, t):
     return float(x.item())
 
 
+ENC_VOCABS = (1_000_000, 100_000_000)
+
+
+def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
+    """The encoder alone (rmx_encoder_ids: gather + first order + FM of DeepFM, encoder_k16_kernel<1>) at
+    vocabulary Vw, with the [V][k] row table + [V] weights and with the [V][32] line copy (one 128-B line per
+    id: knob table_lines), timed with HIP events on its stream: examples/s, algorithmic GB/s (2,812 B per
+    example) against the 8 TB/s HBM peak, and the 128-B line rate (a random 64-B row or 4-B
+    weight costs one full line: profiles/r02/fetch_calib.txt).  Bit-exact parity of y against the oracle's
+    first order + FM on rows of the first batch (V = 1M: the host table; V = 100M: the generated rows)."""
+    import ctypes
+    m = rmx.DeepFM(Vw, F, K, FC, ctx=ctx)
+    table = rmx.EmbeddingTable(ctx, Vw, K)
+    table.fill_synthetic(SEED_TAB)
+    nb = 16
+    ids = rmx.DeviceArray(ctx, nb * B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, nb * B, F, Vw, ids)
+    y = rmx.DeviceArray(ctx, nb * B, np.float32)
+    ctx.sync()
+    stream = ctx.stream
+    lib = rmx._lib.lib
+    ev0, ev1 = ctypes.c_void_p(), ctypes.c_void_p()
+    lib.rmx_event_create(ctypes.byref(ev0))
+    lib.rmx_event_create(ctypes.byref(ev1))
+    bpe = F * 4 + F * 4 + F * K * 4 + 4
+    rec = {"kernel": "encoder_k16_kernel<1, float>", "batch": B, "vocab": Vw,
+           "algorithmic_bytes_per_example": bpe, "peak_gbs": PEAK_HBM_GBS}
+    saved = rmx.get_tuning("table_lines", 0)
+    try:
+        for lines in (0, 1):
+            rmx.set_tuning("table_lines", lines)
+            table.refresh_lines()
+            ctx.sync()
+            t_end = time.perf_counter() + 0.3
+            i = 0
+            while time.perf_counter() < t_end:  # clock settle (DESIGN.md §6)
+                for _ in range(8):
+                    m.encoder_ids(table, B, ids.view((i % nb) * B * F, B * F), y.view((i % nb) * B, B), stream)
+                    i += 1
+                ctx.sync()
+            for j in range(warmup):
+                m.encoder_ids(table, B, ids.view((j % nb) * B * F, B * F), y.view((j % nb) * B, B), stream)
+            lib.rmx_event_record(ev0, stream)
+            for j in range(steps):
+                m.encoder_ids(table, B, ids.view((j % nb) * B * F, B * F), y.view((j % nb) * B, B), stream)
+            lib.rmx_event_record(ev1, stream)
+            ctx.sync()
+            ms = ctypes.c_float()
+            lib.rmx_event_elapsed_ms(ev0, ev1, ctypes.byref(ms))
+            avg_s = ms.value / 1e3 / steps
+            lines_per_ex = F if lines else 2 * F  # + the ids' own lines (156 B per example, streamed)
+            ent = {"avg_ms": round(avg_s * 1e3, 4), "examples_per_s": round(B / avg_s, 1),
+                   "achieved_gbs": round(B * bpe / avg_s / 1e9, 1),
+                   "frac": round(B * bpe / avg_s / 1e9 / PEAK_HBM_GBS, 4),
+                   "lines_per_example": lines_per_ex,
+                   "line_gbs": round(B * (lines_per_ex * 128 + F * 4 + 4) / avg_s / 1e9, 1),
+                   "line_frac": round(B * (lines_per_ex * 128 + F * 4 + 4) / avg_s / 1e9 / PEAK_HBM_GBS, 4)}
+            rec["line_table" if lines else "row_table"] = ent
+    finally:
+        rmx.set_tuning("table_lines", saved)
+    # parity (bit-exact): rows [0, n) of the first batch, y = y1 + y2 from the oracle's own gather + sums
+    m.encoder_ids(table, B, ids.view(0, B * F), y.view(0, B), stream)
+    ctx.sync()
+    got = y.numpy()[:256]
+    oc = _oracle()
+    n = 256
+    h_ids = ids.numpy()[:n * F].astype(np.int64)
+    if Vw == V:
+        wt, et = oc.gen_table(SEED_TAB, V, K)
+        w, e = oc.gather(wt, et, 1, h_ids)
+    else:
+        w, e = oc.gen_rows(SEED_TAB, Vw, K, h_ids)
+    ref = (oc.first_order(n, np.repeat(np.arange(n, dtype=np.int64), F), w) + oc.fm(n, F, K, e)).astype(np.float32)
+    rec["parity_check"] = {"rows": n, "bitwise_equal": bool(np.array_equal(got, ref)),
+                           "max_abs_diff": float(np.abs(got - ref).max()), "against": "oracle first order + FM (fp32)"}
+    table.close()
+    return rec
+
+
+def encoder_record(args, rmx, ctx, steps, warmup):
+    """models.encoder of the default line: the encoder alone at V = 1M (Infinity-Cache resident) and 100M."""
+    out = {"note": ("the DeepFM forward fuses this encoder into tower layer 1 (k_head_s3.hip); timed alone here "
+                    "for its HBM roofline (north_star, SURVEY.md §8d)")}
+    for Vw in ENC_VOCABS:
+        try:
+            out["V%dM" % (Vw // 1_000_000)] = run_encoder(args, rmx, ctx, steps, warmup, Vw)
+        except Exception as e:
+            out["V%dM" % (Vw // 1_000_000)] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
+    return out
+
+
 LIVE_SHARDS = []  # sharded tables of this process (the companion watchdog aborts their communicators)
 
 
@@ -429,7 +530,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     if workload == "lr_plumbing":
         return run_plumbing(args, rmx, ctx, rank, world, dist, steps, warmup)
     train = workload.endswith("_train")
-    B = B or args.batch or ({"xdeepfm": 16384, "xdeepfm_train": 4096}.get(workload, 65536))
+    B = B or args.batch or ({"xdeepfm": 16384, "xdeepfm_cin1": 65536, "xdeepfm_train": 4096}.get(workload, 65536))
     sharded = workload == "deepfm_sharded"
     Vw = args.vocab or (100_000_000 if sharded else V)
     stream = ctx.stream
@@ -672,7 +773,7 @@ def config_of(workload, r, world, zipf):
     return {"workload": "%s%s_F39_V%s_k16_fc400x3%s_B%d" % (
         workload, "" if r["bf16"] else "_fp32",
         ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else str(Vw),
-        {"xdeepfm": "_cin200x3", "dcn_bf16": "_cross3"}.get(base, ""), B),
+        {"xdeepfm": "_cin200x3", "xdeepfm_cin1": "_cin200x1", "dcn_bf16": "_cross3"}.get(base, ""), B),
         "global_batch": world * B, "rows_per_gpu_set": r["nrows"],
         "ids": ("zipf%g" % zipf) if zipf else "uniform",
         "parallelism": ("hashshard%d_rccl" % world) if workload == "deepfm_sharded" else "replicas%d" % world}
@@ -802,12 +903,34 @@ def main():
     rmx.set_device(local % ndev)
     ctx = rmx.default_context()
 
+    if args.workload == "encoder":
+        # the encoder alone (profiling / its own line): V = --vocab (default 100M), B = --batch (65,536)
+        Vw = args.vocab or 100_000_000
+        rec = run_encoder(args, rmx, ctx, args.steps, args.warmup, Vw, B=args.batch or 65536)
+        if rank == 0:
+            ent = rec["row_table"]
+            print(json.dumps({
+                "metric": "encoder (gather + first order + FM) examples/sec", "value": ent["examples_per_s"],
+                "unit": "examples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": ent["avg_ms"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32", "data": "synthetic", "config": {"workload": "encoder_fp32_F39_V%s_k16_B%d" % (
+                    ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else Vw, rec["batch"])},
+                "roofline": {"bound": "hbm", "achieved": ent["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": ent["frac"], "traffic": None, "kernel": rec["kernel"]},
+                "encoder": rec}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        raise SystemExit(0 if rec["parity_check"]["bitwise_equal"] else STATUS_PARITY_MISS)
     r = run(args, args.workload, rmx, ctx, rank, world, dist, args.steps, args.warmup)
     # BASELINE.json's metric names DeepFM AND xDeepFM: the default line measures both (xDeepFM as a
     # sub-record with its own steps, roofline, parity and CPU baseline; configs[2])
     companion = None
     if args.workload == "deepfm" and not args.no_companion:
         companion = run(args, "xdeepfm", rmx, ctx, rank, world, dist, args.steps, args.warmup, B=16384)
+    # the encoder alone (gather + first order + FM) at V = 1M and 100M: its HBM roofline
+    enc = None
+    if args.workload == "deepfm" and not args.no_encoder_record and not args.zipf and rank == 0:
+        enc = encoder_record(args, rmx, ctx, max(20, min(args.steps, 100)), max(5, args.warmup))
 
     cpu = cpu2 = None
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not train and not args.parity_only
@@ -885,6 +1008,8 @@ def main():
                 "roofline": companion["roofline"], "stages": companion["stages"],
                 "stage_sum_ms": companion["stage_sum_ms"], "cpu_baseline": cpu2,
                 **({"predict_auc": companion["predict_auc"]} if companion.get("predict_auc") else {})}}
+        if enc is not None:
+            line.setdefault("models", {})["encoder"] = enc
         if not train and args.workload != "lr_plumbing":
             # BASELINE.json asks for the HBM-roofline fraction too: the whole forward's algorithmic
             # bytes per example (ids + first-order weights + embedding rows + output)
@@ -905,6 +1030,9 @@ def main():
         if rank == 0:
             line.setdefault("models", {})["deepfm_sharded"] = sub
     status = job_status(parity_ranks, sub, cpu, cpu2)
+    if enc is not None and any(not e.get("parity_check", {}).get("bitwise_equal", False)
+                               for k_, e in enc.items() if k_.startswith("V")):
+        status = status or STATUS_PARITY_MISS
     if rank == 0:
         if status:
             line["status"] = {"exit": status, "reason": "parity miss" if status == STATUS_PARITY_MISS

@@ -487,7 +487,11 @@ extern "C" int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t B, cons
   RMX_HIP(hipSetDevice(m->ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : m->ctx->stream;
   const int mode = m->type == RMX_MODEL_DEEPFM ? 1 : 0;
-  return launch_encoder(s, mode, B, d_ids, t->emb, t->w, t->dtype, m->F, t->k, d_y, nullptr, nullptr);
+  // the table's [emb | w | pad] line copy when it has one (knob table_lines): one 128-B line per id
+  FwdInputs in;
+  table_inputs(*t, *m, in);
+  return launch_encoder(s, mode, B, d_ids, in.table, in.wtab, t->dtype, m->F, t->k, d_y, nullptr, nullptr, in.ld,
+                        in.wld);
 }
 
 // The params-map contract shared by RecModel.forward / backward (RecModel.scala:130-155):
