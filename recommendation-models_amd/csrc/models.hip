@@ -726,6 +726,21 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     return launch_tower_small_s3(s, m, B, F, in.ids, (const float*)in.table, in.ld, (const float*)in.wtab, in.wld, oa);
   }
 
+  // DeepFM fp32 at a batch that fills the GPU: the whole tower + first order + FM + head in one persistent
+  // row-owner launch, h1 and h2 in registers (k_fused_s3.hip; knob "s3_fused")
+  if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) && k == 16 &&
+      m.layers.size() == 3 && tower_fused_s3_usable(m.layers[0], m.layers[1], m.layers[2], B, F, k, true)) {
+    StageTimer t(m, s, "tower_fused");
+    OutArgs oa{};
+    oa.wo = m.wo;
+    oa.bo = m.bo;
+    oa.has_bo = m.has_bo ? 1 : 0;
+    oa.beta = in.beta;
+    oa.out = in.out;
+    return launch_tower_fused_s3(s, m.layers[0], m.layers[1], m.layers[2], B, F, in.ids, (const float*)in.table, in.ld,
+                                 (const float*)in.wtab, in.wld, oa);
+  }
+
   // 1. first order (+ FM for DeepFM; fused into tower layer 1 when it gathers through the split GEMM)
   const float* pre = nullptr;
   AGatherArgs ga{in.ids, (const float*)in.table, F, k, in.ld};

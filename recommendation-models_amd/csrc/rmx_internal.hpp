@@ -140,6 +140,13 @@ int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer
 bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids);
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
                          int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums);
+// DeepFM's whole fp32 tower in one persistent row-owner kernel (k_fused_s3.hip): gather (k = 16, ids [M][F])
+// + first order + FM + three 400-wide split-GEMM layers + the head, h1 and h2 in registers -> oa.out [M]
+bool tower_fused_s3_usable(const DenseLayer& L1, const DenseLayer& L2, const DenseLayer& L3, int M, int F, int k,
+                           bool ids);
+int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer& L2, const DenseLayer& L3, int M, int F,
+                          const int32_t* ids, const float* table, int ld, const float* wtab, int wld,
+                          const OutArgs& oa);
 // fp32 tower tail (k_tail_s3.hip): ReLU(H L2) -> ReLU(. L3) . wo -> head on the split GEMM, one persistent
 // launch, h2 in registers; both layers 400 x 400 with split planes; H [M][lda] fp32
 bool tower_tail_s3_usable(const DenseLayer& L2, const DenseLayer& L3, int M, int lda);

@@ -24,7 +24,7 @@ def ctx():
     return rmx.default_context()
 
 
-KNOBS = ("s3_head", "s3_tail")
+KNOBS = ("s3_head", "s3_tail", "s3_fused")
 
 
 @pytest.fixture(autouse=True)
@@ -79,6 +79,12 @@ def _check(ctx, kind, B, bf16=False, knobs=()):
 @pytest.mark.parametrize("kind", ["deepfm", "dnn", "dcn", "pnn", "lr"])
 def test_fp32_forward_ignores_lds_leftovers(ctx, kind, B):
     _check(ctx, kind, B)
+
+
+@pytest.mark.parametrize("B", [19217, 65536])
+def test_deepfm_head_and_tail_ignore_lds_leftovers(ctx, B):
+    """DeepFM on the head + tail pair (s3_fused 0) instead of the default fused tower."""
+    _check(ctx, "deepfm", B, knobs=(("s3_fused", 0),))
 
 
 @pytest.mark.parametrize("B", [1000, 16384])

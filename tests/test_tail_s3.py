@@ -38,9 +38,11 @@ def ctx():
 @pytest.fixture(autouse=True)
 def _restore_knobs():
     rmx.set_tuning("s3_small", 0)  # (small batches would run the whole-tower kernel, k_small_s3.hip)
+    rmx.set_tuning("s3_fused", 0)  # (and DeepFM batches that fill the GPU the fused tower, k_fused_s3.hip)
     yield
     rmx.set_tuning("s3_tail", None)
     rmx.set_tuning("s3_small", None)
+    rmx.set_tuning("s3_fused", None)
 
 
 def _model(kind, V):
@@ -105,7 +107,8 @@ def test_fp32_tail_matches_unfused_and_oracle(ctx, kind, B):
 
 
 def test_fp32_tail_is_the_default_at_the_bench_batch(ctx):
-    """configs[1] (DeepFM, B = 65,536) runs the tail by default (knob s3_tail 1: row blocks >= CUs)."""
+    """configs[1] (DeepFM, B = 65,536) without the fused tower (s3_fused 0) runs the tail by default (knob
+    s3_tail 1: row blocks >= CUs)."""
     B, V = 65536, 100000
     m = rmx.DeepFM(V, F, K, list(FC))
     m.setMats(m.initMats(SEED_MATS))

@@ -92,7 +92,7 @@ for s in $STEPS; do
          wl=${rest%%:*}; kv=${rest#*:}; knob=${kv%%=*}; vals=$(echo ${kv#*=} | tr '/' ' ')
          for i in 1 2; do
            for v in $vals; do
-             run abw_${wl}_${knob}_${v}_${i} 300 python bench.py --workload $wl --no-companion --no-cpu-baseline --steps 100 --warmup 10 --set $knob=$v || exit $?
+             run abw_${wl}_${knob}_${v}_${i} 300 python bench.py --workload $wl --no-companion --no-encoder-record --no-cpu-baseline --steps 100 --warmup 10 --set $knob=$v || exit $?
            done
          done ;;
     testk:*) k=${s#testk:}
