@@ -105,6 +105,106 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
   if (MODE == 3) y[b] = y[b] + y2;  // y holds y1 from the CSR kernel
 }
 
+// Round 5: the same lane layout and arithmetic (y1 + y2 bit-identical to encoder_k16_kernel), with fewer
+// dependent round trips to memory.  The kernel above loads 8 ids, then their 8 rows, then the next 8 ids:
+// 10 round trips for F = 39, each exposed (B = 65,536 gives only 16 waves per CU, so nothing else hides
+// them; V = 100M row table: 0.106 ms, 0.78 of the 128-B line rate of HBM).  Here the 4 lanes of a sample
+// load the sample's ids of a 40-field chunk once, coalesced (lane c: fields 4i + c), share them with a quad
+// DPP broadcast, and request the rows (+ first-order weights) in batches of U: 1 + ceil(F / U) round trips.
+// Forward modes only (0, 1, 2: ids given, no x / FM-sum outputs); the kernel above keeps the rest.
+__device__ __attribute__((aligned(16))) float g_enc_zero16[16];  // the zero row of fields past F
+
+template <int J>
+__device__ __forceinline__ int quad_bcast(int v) {  // every lane of a quad takes the quad's lane J
+  return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int quad_bcast(int v, int j) {  // (j is a constant after unrolling)
+  switch (j) {
+    case 0: return quad_bcast<0>(v);
+    case 1: return quad_bcast<1>(v);
+    case 2: return quad_bcast<2>(v);
+    default: return quad_bcast<3>(v);
+  }
+}
+
+template <int MODE, class T, int U>
+__global__ __launch_bounds__(256) void encoder_k16v2_kernel(int M, const int32_t* __restrict__ ids,
+                                                            const T* __restrict__ table,
+                                                            const T* __restrict__ wtab, int F,
+                                                            float* __restrict__ y, float beta,
+                                                            float* __restrict__ prob, int ld, int wld) {
+#pragma clang fp contract(off)
+  constexpr int NI = 10, CH = 4 * NI;  // ids per lane / fields per chunk
+  constexpr int NB = (CH + U - 1) / U;
+  constexpr bool FM = MODE == 1;
+  const int lane = threadIdx.x & 63;
+  const int s = lane >> 2, c = lane & 3;
+  const int b = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + s;
+  const bool valid = b < M;
+  const int32_t* irow = ids + (int64_t)(valid ? b : 0) * F;
+  float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = s4;
+  float y1 = 0.f;
+  // branch-free inside a batch (a per-lane or per-field branch around a load made the compiler wait for each
+  // load before the next): every lane loads every id / row / weight; a field past F reads a zero row and a
+  // zero weight (x + 0 = x: the sums keep their bits), whose address is selected, not branched to
+  const float* zero16 = g_enc_zero16;
+  for (int f0 = 0; f0 < F; f0 += CH) {
+    int idv[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int f = f0 + 4 * i + c;
+      idv[i] = irow[f < F ? f : F - 1];
+    }
+#pragma unroll
+    for (int h = 0; h < NB; ++h) {
+      if (f0 + h * U >= F) break;  // (wave-uniform, per batch)
+      float4 v[U];
+      float wv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int uu = h * U + u;
+        if (uu >= CH) break;  // (compile time)
+        // field f0 + uu: its id is lane (s, uu & 3)'s idv[uu >> 2] -- a quad_perm(j, j, j, j) broadcast
+        const int id = quad_bcast(idv[uu >> 2], uu & 3);
+        const bool live = f0 + uu < F;
+        const T* rsrc = live ? table + (int64_t)id * ld + c * 4 : reinterpret_cast<const T*>(zero16);
+        const T* wsrc = live ? wtab + (int64_t)id * wld : reinterpret_cast<const T*>(zero16);
+        if (FM) v[u] = load4(rsrc);
+        wv[u] = ld1(wsrc);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (h * U + u >= CH) break;
+        if (FM) {
+          s4.x += v[u].x; s4.y += v[u].y; s4.z += v[u].z; s4.w += v[u].w;
+          q4.x += v[u].x * v[u].x; q4.y += v[u].y * v[u].y;
+          q4.z += v[u].z * v[u].z; q4.w += v[u].w * v[u].w;
+        }
+        y1 += wv[u];
+      }
+    }
+  }
+  float y2 = 0.f;
+  if (FM) {  // encoder_k16_kernel's reduction, the same order
+    float d0 = s4.x * s4.x - q4.x, d1 = s4.y * s4.y - q4.y;
+    float d2 = s4.z * s4.z - q4.z, d3 = s4.w * s4.w - q4.w;
+    float acc = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int src = (lane & ~3) | cc;
+      acc += __shfl(d0, src);
+      acc += __shfl(d1, src);
+      acc += __shfl(d2, src);
+      acc += __shfl(d3, src);
+    }
+    y2 = 0.5f * (acc / 16.0f);
+  }
+  if (!valid || c != 0) return;
+  if (MODE == 0) y[b] = y1;
+  if (MODE == 1) y[b] = y1 + y2;
+  if (MODE == 2) prob[b] = 1.0f / (1.0f + expf(-(y1 + beta)));
+}
+
 // Generic-k fallback: one thread per sample, oracle order.
 template <int MODE, class T>
 __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32_t* __restrict__ ids,
@@ -145,6 +245,19 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
 template <class T>
 static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids, const T* table, const T* wtab, int F,
                              int k, float* y, float bt, float* prob, int ld, int wld, float* xo, float* so) {
+  // knob "enc_u" (round 5): rows per batch of the v2 kernel, 0 = the kernel above
+  const int eu = tuning_get("enc_u", 20);
+  if ((k == 16 || mode == 2) && ids && !xo && !so && mode != 3 && (eu == 13 || eu == 20)) {
+    dim3 grid((M + 63) / 64);
+#define RMX_ENC2(MD, UU) hipLaunchKernelGGL((encoder_k16v2_kernel<MD, T, UU>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld)
+    if (eu == 13) {
+      if (mode == 0) RMX_ENC2(0, 13); else if (mode == 1) RMX_ENC2(1, 13); else RMX_ENC2(2, 13);
+    } else {
+      if (mode == 0) RMX_ENC2(0, 20); else if (mode == 1) RMX_ENC2(1, 20); else RMX_ENC2(2, 20);
+    }
+#undef RMX_ENC2
+    return;
+  }
   if (k == 16 || mode == 2) {  // LR (mode 2) never reads the table: any k takes the 4-lane path
     dim3 grid((M + 63) / 64);
     switch (mode) {
