@@ -168,19 +168,20 @@ __device__ __forceinline__ f32x4 f_sbias(const float* b, int t, int g) {
 
 // layer-3 half HF (column tiles 13 HF .. + 12; half 1 computes 12, tile 25 is padding): 13 units, one per
 // K step, unrolled so that h2's tiles 2c, 2c + 1 are static registers (k_tail_s3.hip q_layer3)
-template <int HF>
+template <int HF, bool PREP>
 __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const float* prm, f32x4 (&h2)[kQNT],
                                          int& slot, int w, int lane, int lo, int fb, float& part) {
   const int g = lane >> 4;
   f32x4 acc[kQUT];
 #pragma unroll
   for (int t = 0; t < kQUT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ah, am, al;
+  if (PREP) split3(h2[0], h2[1], ah, am, al);
 #pragma unroll
   for (int c = 0; c < kFKS2; ++c) {
     q_enter<5>();
-    bf16x8 ah, am, al;
-    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-    split3(h2[2 * c], 2 * c + 1 < kQNT ? h2[2 * c + 1] : z, ah, am, al);
+    if (!PREP) split3(h2[2 * c], 2 * c + 1 < kQNT ? h2[2 * c + 1] : z, ah, am, al);
     const int dslot = slot == 0 ? 2 : slot - 1;  // (slot + 2) mod 3
     const char* ub = lds + slot * kQUnit;
     const bf16_t* src = f_src23(p, 2 * kFKS2 + HF * kFKS2 + c + 2);
@@ -189,6 +190,10 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
     else
       q_unit<kQUT - 1, 0, kQUT, RMX_FUSED_PF3>(ub, fb, ah, am, al, acc, src, lds, dslot, w, lo);
     slot = q_next(slot);
+    if (PREP && c + 1 < kFKS2) {  // the next step's split before the next barrier (layer 1's PREP)
+      __builtin_amdgcn_sched_barrier(0);
+      split3(h2[2 * c + 2], 2 * c + 3 < kQNT ? h2[2 * c + 3] : z, ah, am, al);
+    }
   }
   // the output dot over this half's columns: ReLU(acc + b3)[n] * wo[n], n = 16 (13 HF + t) + 4 g + q
   constexpr int NT = HF == 0 ? kQUT : kQNT - kQUT;
@@ -210,6 +215,7 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
   asm volatile("" : "+v"(part));  // (the dot is done here: sunk past half 1 it kept 13 accumulators alive)
 }
 
+template <bool PREP>
 __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Args p) {
   extern __shared__ __attribute__((aligned(16))) char fsmem[];
   char* lds = fsmem;
@@ -286,25 +292,31 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     for (int t = 0; t < kQNT; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 fs = f32x4{0.f, 0.f, 0.f, 0.f}, fq = fs;
     float y1 = 0.f;
+    bf16x8 ah, am, al;
+    // step ss's A operand from its rows in A slot ss & 1: FM sums + first order (field order) and the split
+    auto prep = [&](int ss) {
+      int o = r16 * 64 + swz_slot(r16, g) * 16;
+      asm volatile("" : "+v"(o));
+      const char* a = wl + (ss & 1) * 2048;
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(a + o);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(a + 1024 + o);
+      const float* wr = reinterpret_cast<const float*>(wl + kFA + kFId + (ss & 1) * 128);
+      {
+#pragma clang fp contract(off)
+        fm_accum(a0, a1, fs, fq);  // (SecondOrderEncoder sums, field order, k_gemm.hpp)
+        y1 += wr[r16];             // first order in field order (encoder_k16_kernel<0>)
+        y1 += wr[16 + r16];
+      }
+      split3(a0, a1, ah, am, al);
+    };
+    // PREP: step s + 1's A is formed at the end of step s's half-1 unit, before the barrier of step s + 1 --
+    // while the SIMD's partner wave still issues its MFMAs -- instead of after it, where both waves of the
+    // SIMD formed theirs with the matrix pipe idle.  The block's first step: its rows landed long ago.
+    if (PREP) prep(s);
 #pragma unroll 1
     for (int c = 0; c < KS; ++c, ++s) {
       q_enter<5>();  // previous unit: (c - 1, half 1) or the previous row block's last layer-3 unit, 5 DMAs
-      bf16x8 ah, am, al;
-      {
-        int o = r16 * 64 + swz_slot(r16, g) * 16;
-        asm volatile("" : "+v"(o));
-        const char* a = wl + (s & 1) * 2048;
-        const f32x4 a0 = *reinterpret_cast<const f32x4*>(a + o);
-        const f32x4 a1 = *reinterpret_cast<const f32x4*>(a + 1024 + o);
-        const float* wr = reinterpret_cast<const float*>(wl + kFA + kFId + (s & 1) * 128);
-        {
-#pragma clang fp contract(off)
-          fm_accum(a0, a1, fs, fq);  // (SecondOrderEncoder sums, field order, k_gemm.hpp)
-          y1 += wr[r16];             // first order in field order (encoder_k16_kernel<0>)
-          y1 += wr[16 + r16];
-        }
-        split3(a0, a1, ah, am, al);
-      }
+      if (!PREP) prep(s);
       id_dma(s + 3);
       f_row_dma(p, wl, s + 1, lane);
       __builtin_amdgcn_sched_barrier(0);  // these 4 DMAs ahead of the unit's 5 (the static vmcnt counts)
@@ -316,6 +328,13 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       dslot = slot == 0 ? 2 : slot - 1;
       q_unit<kQNT - kQUT, kQUT>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u + 1, 2), lds, dslot, w, lo);
       slot = q_next(slot);
+      if (PREP && c + 1 < KS) {
+        // rows + weights of step s + 1 were issued at the start of (c, half 0), ahead of its 5 plane DMAs and
+        // this unit's 5: they have landed once at most those 10 are in flight (wave-local slots: no barrier)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        prep(s + 1);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     // first order + FM of the row (k_head_s3.hip's epilogue: encoder_k16_kernel<1>'s arithmetic)
@@ -369,8 +388,8 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     }
     // ---- layer 3 + the output dot ----
     float part = 0.f;
-    f_layer3<0>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
-    f_layer3<1>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    f_layer3<0, PREP>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    f_layer3<1, PREP>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
     // ---- head: the four lane groups' columns, then bias, CAddTable, sigmoid (out_finish_kernel's order) ----
     part += __shfl_xor(part, 16);
     part += __shfl_xor(part, 32);
@@ -429,8 +448,10 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   int dev = 0, ncu = 0;
   RMX_HIP(hipGetDevice(&dev));
   RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  RMX_HIP(hipFuncSetAttribute((const void*)tower_fused_s3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kFLds));
+  // knob "fused_prep" (default 1): the next step's A formed before the step barrier (layers 1 and 3)
+  const bool prep = tuning_get("fused_prep", 1) != 0;
+  const void* kfn = prep ? (const void*)tower_fused_s3_kernel<true> : (const void*)tower_fused_s3_kernel<false>;
+  RMX_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFLds));
   FusedS3Args p{};
   p.M = M;
   int grid = 0;
@@ -450,7 +471,10 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   p.W3 = L3.W3;
   p.b3 = L3.b;
   p.oa = oa;
-  hipLaunchKernelGGL(tower_fused_s3_kernel, dim3(grid), dim3(kQThreads), kFLds, s, p);
+  if (prep)
+    hipLaunchKernelGGL(tower_fused_s3_kernel<true>, dim3(grid), dim3(kQThreads), kFLds, s, p);
+  else
+    hipLaunchKernelGGL(tower_fused_s3_kernel<false>, dim3(grid), dim3(kQThreads), kFLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

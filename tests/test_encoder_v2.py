@@ -47,8 +47,8 @@ def test_encoder_v2_bit_exact(ctx, F, B):
     table.upload(wt, et)
     ids_dev = rmx.DeviceArray.from_numpy(ctx, ids.astype(np.int32))
     deepfm = rmx.DeepFM(V, F, K, [32])
-    dnn_fo = rmx.PNN(V, F, K, [32])  # (a non-DeepFM model: the encoder computes the first order only)
-    for model, fm in ((deepfm, True), (dnn_fo, False)):
+    lr = rmx.LR(V, F)  # (a non-DeepFM model: the encoder computes the first order only)
+    for model, fm in ((deepfm, True), (lr, False)):
         res = {u: _encode(ctx, model, table, B, ids_dev, u) for u in (0, 13, 20)}
         assert np.array_equal(res[13], res[0]) and np.array_equal(res[20], res[0])
         n = min(B, 4096)

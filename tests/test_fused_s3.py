@@ -142,3 +142,19 @@ def test_fused_tower_is_the_default_at_the_bench_batch(ctx):
     ctx.sync()
     stages, _ = m.get_timing()
     assert list(stages) == ["tower_fused"], stages
+
+
+@pytest.mark.parametrize("B", [40000, 65536])
+def test_fused_tower_prep_knob_bitwise(ctx, B):
+    """fused_prep 1 (the next K step's A operand formed before the step barrier, layers 1 and 3) moves work,
+    not arithmetic: the same bits as fused_prep 0."""
+    V = 50000
+    m, mats, table, ids, out = _setup(ctx, B, V)
+    res = {}
+    try:
+        for pv in (0, 1):
+            rmx.set_tuning("fused_prep", pv)
+            res[pv] = _fwd(ctx, m, table, B, ids, out, True)
+    finally:
+        rmx.set_tuning("fused_prep", None)
+    assert np.array_equal(res[0], res[1])
