@@ -51,10 +51,8 @@ constexpr int kFPrm = 2 * kQN;                   // b3 | wo in LDS
 constexpr size_t kFLds = (size_t)kQSlots * kQUnit + (size_t)kQW * kFWave + sizeof(float) * kFPrm;
 static_assert(kFLds <= 160 * 1024, "LDS budget");
 
-// weight-fragment prefetch depth (column tiles) of the layer-2 units, where h1 and acc2 are both live
-#ifndef RMX_FUSED_PF2
-#define RMX_FUSED_PF2 1
-#endif
+// weight-fragment prefetch depth (column tiles) of the layer-3 units (2 spilled 7 registers); layer 2's is a
+// template parameter (knob fused_pf2: 1 or 2, both spill-free)
 #ifndef RMX_FUSED_PF3
 #define RMX_FUSED_PF3 1
 #endif
@@ -140,20 +138,26 @@ __device__ __forceinline__ void f_id_dma(const FusedS3Args& p, char* wl, int row
 
 // rows (2 DMAs) and first-order weights (lanes 0 .. 31) of the wave's step s, from the ids in id slot s & 3,
 // into A slot s & 1 / weight slot s & 1  (k_head_s3.hip h_row_dma)
-__device__ __forceinline__ void f_row_dma(const FusedS3Args& p, char* wl, int s, int lane) {
+// part 0 / 1: the row of field 2c / 2c + 1; part 2: the weights; -1: all three
+__device__ __forceinline__ void f_row_dma(const FusedS3Args& p, char* wl, int s, int lane, int part = -1) {
   const int* ids = reinterpret_cast<const int*>(wl + kFA + (s & 3) * 128);
   int r = lane >> 2, g = swz_slot(lane >> 2, lane & 3), lw = lane & 31;
   asm volatile("" : "+v"(r), "+v"(g), "+v"(lw));
-  const int id0 = ids[r], id1 = ids[16 + r], idw = ids[lw];
   const float* zero16 = g_rmx_zero16;
-  const float* s0 = id0 >= 0 ? p.table + ((int64_t)id0 << p.gsh) + 4 * g : zero16;
-  const float* s1 = id1 >= 0 ? p.table + ((int64_t)id1 << p.gsh) + 4 * g : zero16;
-  const float* sw = idw >= 0 ? p.wtab + ((int64_t)idw << p.wsh) : zero16;
   char* a = wl + (s & 1) * 2048;
-  lds_dma<16>(s0, a);
-  lds_dma<16>(s1, a + 1024);
-  if (lane < 32)
-    lds_dma<4>(sw, wl + kFA + kFId + (s & 1) * 128);
+  if (part < 0 || part == 0) {
+    const int id0 = ids[r];
+    lds_dma<16>(id0 >= 0 ? p.table + ((int64_t)id0 << p.gsh) + 4 * g : zero16, a);
+  }
+  if (part < 0 || part == 1) {
+    const int id1 = ids[16 + r];
+    lds_dma<16>(id1 >= 0 ? p.table + ((int64_t)id1 << p.gsh) + 4 * g : zero16, a + 1024);
+  }
+  if (part < 0 || part == 2) {
+    const int idw = ids[lw];
+    if (lane < 32)
+      lds_dma<4>(idw >= 0 ? p.wtab + ((int64_t)idw << p.wsh) : zero16, wl + kFA + kFId + (s & 1) * 128);
+  }
 }
 
 // b[16 t + 4 g .. + 3] through scalar loads (the address is wave-uniform; no LDS is left for b1 / b2):
@@ -215,7 +219,7 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
   asm volatile("" : "+v"(part));  // (the dot is done here: sunk past half 1 it kept 13 accumulators alive)
 }
 
-template <bool PREP>
+template <bool PREP, int PF2, bool SPREAD>
 __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Args p) {
   extern __shared__ __attribute__((aligned(16))) char fsmem[];
   char* lds = fsmem;
@@ -317,12 +321,27 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     for (int c = 0; c < KS; ++c, ++s) {
       q_enter<5>();  // previous unit: (c - 1, half 1) or the previous row block's last layer-3 unit, 5 DMAs
       if (!PREP) prep(s);
-      id_dma(s + 3);
-      f_row_dma(p, wl, s + 1, lane);
-      __builtin_amdgcn_sched_barrier(0);  // these 4 DMAs ahead of the unit's 5 (the static vmcnt counts)
       const int u = 2 * c;
       int dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQUT, 0>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo);
+      if (SPREAD) {
+        // SPREAD: the ids (3 steps ahead), rows and weights (1 step ahead) ride tiles 6, 8, 10, 11 of the
+        // unit's MFMA stream, after its 5 plane DMAs (an LDS-DMA issue can hold its wave ~100-200 cycles:
+        // four of them ahead of the unit's first MFMA delayed it)
+        const int sn = s;
+        auto extra = [&](int t) {
+          if (t == 6) id_dma(sn + 3);
+          if (t == 8) f_row_dma(p, wl, sn + 1, lane, 0);
+          if (t == 10) f_row_dma(p, wl, sn + 1, lane, 1);
+          if (t == 11) f_row_dma(p, wl, sn + 1, lane, 2);
+        };
+        q_unit<kQUT, 0, kQNT, 2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo,
+                                     true, extra);
+      } else {
+        id_dma(s + 3);
+        f_row_dma(p, wl, s + 1, lane);
+        __builtin_amdgcn_sched_barrier(0);  // these 4 DMAs ahead of the unit's 5 (the static vmcnt counts)
+        q_unit<kQUT, 0>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo);
+      }
       slot = q_next(slot);
       q_enter<9>();  // previous unit: 1 id + 2 row + 1 weight + 5 plane DMAs
       dslot = slot == 0 ? 2 : slot - 1;
@@ -331,8 +350,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       if (PREP && c + 1 < KS) {
         // rows + weights of step s + 1 were issued at the start of (c, half 0), ahead of its 5 plane DMAs and
         // this unit's 5: they have landed once at most those 10 are in flight (wave-local slots: no barrier)
+        // (SPREAD: they are the last 4 of (c, half 0)'s 9, so only this unit's 5 may still be in flight)
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        if (SPREAD)
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
         prep(s + 1);
       }
     }
@@ -370,12 +393,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
       split3(h1[2 * c], 2 * c + 1 < kQNT ? h1[2 * c + 1] : z, ah, am, al);
       int dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQUT, 0, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
+      q_unit<kQUT, 0, kQNT, PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
                                            dslot, w, lo);
       slot = q_next(slot);
       q_enter<5>();
       dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQNT - kQUT, kQUT, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
+      q_unit<kQNT - kQUT, kQUT, kQNT, PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
                                                      lds, dslot, w, lo);
       slot = q_next(slot);
     }
@@ -449,9 +472,18 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   RMX_HIP(hipGetDevice(&dev));
   RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   // knob "fused_prep" (default 1): the next step's A formed before the step barrier (layers 1 and 3)
+  // knob "fused_pf2" (1 or 2): layer 2's weight-fragment prefetch depth; "fused_spread" (default 1): layer 1's
+  // row / id DMAs spread over the MFMA stream (SPREAD)
   const bool prep = tuning_get("fused_prep", 1) != 0;
-  const void* kfn = prep ? (const void*)tower_fused_s3_kernel<true> : (const void*)tower_fused_s3_kernel<false>;
-  RMX_HIP(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFLds));
+  const int pf2 = tuning_get("fused_pf2", 1) == 2 ? 2 : 1;
+  const bool spread = tuning_get("fused_spread", 1) != 0;
+  typedef void (*KFn)(FusedS3Args);
+  static const KFn fns[8] = {tower_fused_s3_kernel<false, 1, false>, tower_fused_s3_kernel<false, 1, true>,
+                             tower_fused_s3_kernel<false, 2, false>, tower_fused_s3_kernel<false, 2, true>,
+                             tower_fused_s3_kernel<true, 1, false>,  tower_fused_s3_kernel<true, 1, true>,
+                             tower_fused_s3_kernel<true, 2, false>,  tower_fused_s3_kernel<true, 2, true>};
+  const KFn kfn = fns[(prep ? 4 : 0) + (pf2 == 2 ? 2 : 0) + (spread ? 1 : 0)];
+  RMX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFLds));
   FusedS3Args p{};
   p.M = M;
   int grid = 0;
@@ -471,10 +503,7 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   p.W3 = L3.W3;
   p.b3 = L3.b;
   p.oa = oa;
-  if (prep)
-    hipLaunchKernelGGL(tower_fused_s3_kernel<true>, dim3(grid), dim3(kQThreads), kFLds, s, p);
-  else
-    hipLaunchKernelGGL(tower_fused_s3_kernel<false>, dim3(grid), dim3(kQThreads), kFLds, s, p);
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(kQThreads), kFLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

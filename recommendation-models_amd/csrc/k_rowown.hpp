@@ -67,13 +67,20 @@ __device__ __forceinline__ int q_fbase(int lane) {
   return fb;
 }
 
+// no extra vector-memory instructions in a unit (q_unit's default)
+struct QNoExtra {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
 // One unit: NT column tiles (local tiles 0 .. NT - 1 of the unit's half) of one K step.  acc[T0 + t] +=
 // W_t h^T on the split planes (ah, am, al) of this wave's 16 rows; dma(q) issues the wave's q-th DMA of
-// unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.
-template <int NT, int T0, int NA, int PF = 2, int PS = kQN>
+// unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.  extra(t) may
+// issue more vector-memory instructions at tile t (after that tile's plane DMA): a caller's own DMAs spread
+// over the MFMA stream instead of issued ahead of it.
+template <int NT, int T0, int NA, int PF = 2, int PS = kQN, class X = QNoExtra>
 __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                        f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo,
-                                       bool mm = true) {
+                                       bool mm = true, const X& extra = X()) {
   f32x4 bq[PF + 1][3];
   int fbu = fb;
   asm volatile("" : "+v"(fbu));
@@ -91,6 +98,7 @@ __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah,
     static_assert(kD0 + (kQQ - 1) * kDS < kQUT - 1, "every unit (12 or 13 tiles) carries all its DMAs");
     if (t >= kD0 && (t - kD0) % kDS == 0 && (t - kD0) / kDS < kQQ && !(RMX_QTAIL_DIAG & 1))
       q_dma<PS>(dsrc, lds, dslot, w, (t - kD0) / kDS, lo);
+    extra(t);
     __builtin_amdgcn_sched_barrier(0);
     const f32x4* b = bq[t % (PF + 1)];
     const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);

@@ -145,16 +145,19 @@ def test_fused_tower_is_the_default_at_the_bench_batch(ctx):
 
 
 @pytest.mark.parametrize("B", [40000, 65536])
-def test_fused_tower_prep_knob_bitwise(ctx, B):
-    """fused_prep 1 (the next K step's A operand formed before the step barrier, layers 1 and 3) moves work,
-    not arithmetic: the same bits as fused_prep 0."""
+@pytest.mark.parametrize("knob", ["fused_prep", "fused_spread", "fused_pf2"])
+def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
+    """The schedule knobs move work, not arithmetic -- fused_prep (the next K step's A operand formed before
+    the step barrier, layers 1 and 3), fused_spread (layer 1's row / id DMAs spread over the MFMA stream),
+    fused_pf2 (layer 2's fragment prefetch depth): the same bits either way."""
     V = 50000
     m, mats, table, ids, out = _setup(ctx, B, V)
+    vals = (1, 2) if knob == "fused_pf2" else (0, 1)
     res = {}
     try:
-        for pv in (0, 1):
-            rmx.set_tuning("fused_prep", pv)
-            res[pv] = _fwd(ctx, m, table, B, ids, out, True)
+        for v in vals:
+            rmx.set_tuning(knob, v)
+            res[v] = _fwd(ctx, m, table, B, ids, out, True)
     finally:
-        rmx.set_tuning("fused_prep", None)
-    assert np.array_equal(res[0], res[1])
+        rmx.set_tuning(knob, None)
+    assert np.array_equal(res[vals[0]], res[vals[1]])
