@@ -51,8 +51,11 @@ constexpr int kFPrm = 2 * kQN;                   // b3 | wo in LDS
 constexpr size_t kFLds = (size_t)kQSlots * kQUnit + (size_t)kQW * kFWave + sizeof(float) * kFPrm;
 static_assert(kFLds <= 160 * 1024, "LDS budget");
 
-// weight-fragment prefetch depth (column tiles) of the layer-3 units (2 spilled 7 registers); layer 2's is a
-// template parameter (knob fused_pf2: 1 or 2, both spill-free)
+// weight-fragment prefetch depth (column tiles) of the layer-2 units (2 measured the same, 0.3101-0.3102 vs
+// 0.3093-0.3101 ms) and the layer-3 units (2 spilled 7 registers)
+#ifndef RMX_FUSED_PF2
+#define RMX_FUSED_PF2 1
+#endif
 #ifndef RMX_FUSED_PF3
 #define RMX_FUSED_PF3 1
 #endif
@@ -72,6 +75,7 @@ struct FusedS3Args {
   const bf16_t* W3;
   const float* b3;
   OutArgs oa;             // wo [416], bo, beta, out
+  int prio;
 };
 
 // unit u of a row block -> its weight planes (wave-uniform)
@@ -172,7 +176,7 @@ __device__ __forceinline__ f32x4 f_sbias(const float* b, int t, int g) {
 
 // layer-3 half HF (column tiles 13 HF .. + 12; half 1 computes 12, tile 25 is padding): 13 units, one per
 // K step, unrolled so that h2's tiles 2c, 2c + 1 are static registers (k_tail_s3.hip q_layer3)
-template <int HF, bool PREP>
+template <int HF>
 __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const float* prm, f32x4 (&h2)[kQNT],
                                          int& slot, int w, int lane, int lo, int fb, float& part) {
   const int g = lane >> 4;
@@ -180,12 +184,11 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
 #pragma unroll
   for (int t = 0; t < kQUT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ah, am, al;
-  if (PREP) split3(h2[0], h2[1], ah, am, al);
 #pragma unroll
   for (int c = 0; c < kFKS2; ++c) {
     q_enter<5>();
-    if (!PREP) split3(h2[2 * c], 2 * c + 1 < kQNT ? h2[2 * c + 1] : z, ah, am, al);
+    bf16x8 ah, am, al;
+    split3(h2[2 * c], 2 * c + 1 < kQNT ? h2[2 * c + 1] : z, ah, am, al);
     const int dslot = slot == 0 ? 2 : slot - 1;  // (slot + 2) mod 3
     const char* ub = lds + slot * kQUnit;
     const bf16_t* src = f_src23(p, 2 * kFKS2 + HF * kFKS2 + c + 2);
@@ -194,10 +197,6 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
     else
       q_unit<kQUT - 1, 0, kQUT, RMX_FUSED_PF3>(ub, fb, ah, am, al, acc, src, lds, dslot, w, lo);
     slot = q_next(slot);
-    if (PREP && c + 1 < kFKS2) {  // the next step's split before the next barrier (layer 1's PREP)
-      __builtin_amdgcn_sched_barrier(0);
-      split3(h2[2 * c + 2], 2 * c + 3 < kQNT ? h2[2 * c + 3] : z, ah, am, al);
-    }
   }
   // the output dot over this half's columns: ReLU(acc + b3)[n] * wo[n], n = 16 (13 HF + t) + 4 g + q
   constexpr int NT = HF == 0 ? kQUT : kQNT - kQUT;
@@ -219,7 +218,6 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
   asm volatile("" : "+v"(part));  // (the dot is done here: sunk past half 1 it kept 13 accumulators alive)
 }
 
-template <bool PREP, int PF2, bool SPREAD>
 __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Args p) {
   extern __shared__ __attribute__((aligned(16))) char fsmem[];
   char* lds = fsmem;
@@ -230,6 +228,9 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   const int nit = p.rows.nit(blockIdx.x);
   const int KS = p.KS;
   const OutArgs& oa = p.oa;
+  // knob "fused_prio" (timing A/B): the second-dispatched half of the waves at priority 1 (MI355X_MICROARCH.md,
+  // two waves per SIMD item 4)
+  if (p.prio && w >= kQW / 2) __builtin_amdgcn_s_setprio(1);
 
   for (int i = tid; i < kFPrm; i += kQThreads) {
     const int a = i / kQN, n = i - a * kQN;
@@ -313,51 +314,31 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       }
       split3(a0, a1, ah, am, al);
     };
-    // PREP: step s + 1's A is formed at the end of step s's half-1 unit, before the barrier of step s + 1 --
-    // while the SIMD's partner wave still issues its MFMAs -- instead of after it, where both waves of the
-    // SIMD formed theirs with the matrix pipe idle.  The block's first step: its rows landed long ago.
-    if (PREP) prep(s);
+    // (forming step s + 1's A at the end of step s's half-1 unit, before the barrier, measured the same:
+    // 0.3086-0.3097 vs 0.3094-0.3098 ms, profiles/r05/ab_fused.txt -- not kept)
 #pragma unroll 1
     for (int c = 0; c < KS; ++c, ++s) {
       q_enter<5>();  // previous unit: (c - 1, half 1) or the previous row block's last layer-3 unit, 5 DMAs
-      if (!PREP) prep(s);
+      prep(s);
       const int u = 2 * c;
       int dslot = slot == 0 ? 2 : slot - 1;
-      if (SPREAD) {
-        // SPREAD: the ids (3 steps ahead), rows and weights (1 step ahead) ride tiles 6, 8, 10, 11 of the
-        // unit's MFMA stream, after its 5 plane DMAs (an LDS-DMA issue can hold its wave ~100-200 cycles:
-        // four of them ahead of the unit's first MFMA delayed it)
-        const int sn = s;
-        auto extra = [&](int t) {
-          if (t == 6) id_dma(sn + 3);
-          if (t == 8) f_row_dma(p, wl, sn + 1, lane, 0);
-          if (t == 10) f_row_dma(p, wl, sn + 1, lane, 1);
-          if (t == 11) f_row_dma(p, wl, sn + 1, lane, 2);
-        };
-        q_unit<kQUT, 0, kQNT, 2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo,
-                                     true, extra);
-      } else {
-        id_dma(s + 3);
-        f_row_dma(p, wl, s + 1, lane);
-        __builtin_amdgcn_sched_barrier(0);  // these 4 DMAs ahead of the unit's 5 (the static vmcnt counts)
-        q_unit<kQUT, 0>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo);
-      }
+      // the ids (3 steps ahead), rows and weights (1 step ahead) ride tiles 6, 8, 10, 11 of the unit's MFMA
+      // stream, after its 5 plane DMAs: an LDS-DMA issue can hold its wave ~100-200 cycles, and four of them
+      // ahead of the unit's first MFMA (k_head_s3.hip's order) cost 2 % (0.3142-0.3162 vs 0.3088-0.3111 ms)
+      const int sn = s;
+      auto extra = [&](int t) {
+        if (t == 6) id_dma(sn + 3);
+        if (t == 8) f_row_dma(p, wl, sn + 1, lane, 0);
+        if (t == 10) f_row_dma(p, wl, sn + 1, lane, 1);
+        if (t == 11) f_row_dma(p, wl, sn + 1, lane, 2);
+      };
+      q_unit<kQUT, 0, kQNT, 2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo, true,
+                                   extra);
       slot = q_next(slot);
       q_enter<9>();  // previous unit: 1 id + 2 row + 1 weight + 5 plane DMAs
       dslot = slot == 0 ? 2 : slot - 1;
       q_unit<kQNT - kQUT, kQUT>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u + 1, 2), lds, dslot, w, lo);
       slot = q_next(slot);
-      if (PREP && c + 1 < KS) {
-        // rows + weights of step s + 1 were issued at the start of (c, half 0), ahead of its 5 plane DMAs and
-        // this unit's 5: they have landed once at most those 10 are in flight (wave-local slots: no barrier)
-        // (SPREAD: they are the last 4 of (c, half 0)'s 9, so only this unit's 5 may still be in flight)
-        __builtin_amdgcn_sched_barrier(0);
-        if (SPREAD)
-          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        prep(s + 1);
-      }
     }
     __builtin_amdgcn_sched_barrier(0);
     // first order + FM of the row (k_head_s3.hip's epilogue: encoder_k16_kernel<1>'s arithmetic)
@@ -393,12 +374,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
       split3(h1[2 * c], 2 * c + 1 < kQNT ? h1[2 * c + 1] : z, ah, am, al);
       int dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQUT, 0, kQNT, PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
+      q_unit<kQUT, 0, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
                                            dslot, w, lo);
       slot = q_next(slot);
       q_enter<5>();
       dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQNT - kQUT, kQUT, kQNT, PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
+      q_unit<kQNT - kQUT, kQUT, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
                                                      lds, dslot, w, lo);
       slot = q_next(slot);
     }
@@ -411,8 +392,8 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     }
     // ---- layer 3 + the output dot ----
     float part = 0.f;
-    f_layer3<0, PREP>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
-    f_layer3<1, PREP>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    f_layer3<0>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    f_layer3<1>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
     // ---- head: the four lane groups' columns, then bias, CAddTable, sigmoid (out_finish_kernel's order) ----
     part += __shfl_xor(part, 16);
     part += __shfl_xor(part, 32);
@@ -472,18 +453,8 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   RMX_HIP(hipGetDevice(&dev));
   RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   // knob "fused_prep" (default 1): the next step's A formed before the step barrier (layers 1 and 3)
-  // knob "fused_pf2" (1 or 2): layer 2's weight-fragment prefetch depth; "fused_spread" (default 1): layer 1's
-  // row / id DMAs spread over the MFMA stream (SPREAD)
-  const bool prep = tuning_get("fused_prep", 1) != 0;
-  const int pf2 = tuning_get("fused_pf2", 1) == 2 ? 2 : 1;
-  const bool spread = tuning_get("fused_spread", 1) != 0;
-  typedef void (*KFn)(FusedS3Args);
-  static const KFn fns[8] = {tower_fused_s3_kernel<false, 1, false>, tower_fused_s3_kernel<false, 1, true>,
-                             tower_fused_s3_kernel<false, 2, false>, tower_fused_s3_kernel<false, 2, true>,
-                             tower_fused_s3_kernel<true, 1, false>,  tower_fused_s3_kernel<true, 1, true>,
-                             tower_fused_s3_kernel<true, 2, false>,  tower_fused_s3_kernel<true, 2, true>};
-  const KFn kfn = fns[(prep ? 4 : 0) + (pf2 == 2 ? 2 : 0) + (spread ? 1 : 0)];
-  RMX_HIP(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFLds));
+  RMX_HIP(hipFuncSetAttribute((const void*)tower_fused_s3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kFLds));
   FusedS3Args p{};
   p.M = M;
   int grid = 0;
@@ -503,7 +474,8 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   p.W3 = L3.W3;
   p.b3 = L3.b;
   p.oa = oa;
-  hipLaunchKernelGGL(kfn, dim3(grid), dim3(kQThreads), kFLds, s, p);
+  p.prio = tuning_get("fused_prio", 0);
+  hipLaunchKernelGGL(tower_fused_s3_kernel, dim3(grid), dim3(kQThreads), kFLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

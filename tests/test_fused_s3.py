@@ -145,14 +145,13 @@ def test_fused_tower_is_the_default_at_the_bench_batch(ctx):
 
 
 @pytest.mark.parametrize("B", [40000, 65536])
-@pytest.mark.parametrize("knob", ["fused_prep", "fused_spread", "fused_pf2"])
+@pytest.mark.parametrize("knob", ["fused_prio"])
 def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
-    """The schedule knobs move work, not arithmetic -- fused_prep (the next K step's A operand formed before
-    the step barrier, layers 1 and 3), fused_spread (layer 1's row / id DMAs spread over the MFMA stream),
-    fused_pf2 (layer 2's fragment prefetch depth): the same bits either way."""
+    """The schedule knobs move work, not arithmetic -- fused_prio (the second half of the waves at priority 1):
+    the same bits either way."""
     V = 50000
     m, mats, table, ids, out = _setup(ctx, B, V)
-    vals = (1, 2) if knob == "fused_pf2" else (0, 1)
+    vals = (0, 1)
     res = {}
     try:
         for v in vals:
