@@ -300,10 +300,10 @@ extern "C" int rmx_table_create(rmx_ctx* c, int64_t V, int k, rmx_table** out) {
   return rmx_table_create_ex(c, V, k, RMX_DTYPE_F32, out);
 }
 
-// the [V][32] line copy of an fp32 k = 16 table (rmx_table::line), rebuilt from emb / w; knob
-// "table_lines" 0 drops it (the forward then reads emb / w)
+// the [V][32] line copy of a k = 16 table (rmx_table::line; fp32 or bf16 elements), rebuilt from emb / w;
+// knob "table_lines" 0 drops it (the forward then reads emb / w)
 int rmx::table_refresh_lines(rmx_table& t) {
-  const bool want = t.dtype == RMX_DTYPE_F32 && t.k == 16 && tuning_get("table_lines", 0) != 0;
+  const bool want = t.k == 16 && tuning_get("table_lines", 0) != 0;
   if (!want) {
     if (t.line) {
       RMX_HIP(hipStreamSynchronize(t.ctx->stream));
@@ -312,12 +312,13 @@ int rmx::table_refresh_lines(rmx_table& t) {
     }
     return RMX_OK;
   }
-  if (!t.line && hipMalloc(&t.line, sizeof(float) * 32 * t.V) != hipSuccess) {
+  const size_t es = t.dtype == RMX_DTYPE_BF16 ? sizeof(bf16_t) : sizeof(float);
+  if (!t.line && hipMalloc(&t.line, es * 32 * t.V) != hipSuccess) {
     t.line = nullptr;
     set_error("rmx_table: out of device memory for the line copy (set knob table_lines 0)");
     return RMX_E_NOMEM;
   }
-  const int st = launch_pack_lines(t.ctx->stream, t.V, (const float*)t.emb, (const float*)t.w, t.line);
+  const int st = launch_pack_lines(t.ctx->stream, t.V, t.emb, t.w, t.line, t.dtype);
   if (st) return st;
   RMX_HIP(hipStreamSynchronize(t.ctx->stream));
   return RMX_OK;

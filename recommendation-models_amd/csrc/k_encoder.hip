@@ -376,23 +376,36 @@ int launch_gen_ids(hipStream_t s, uint64_t seed, int64_t row0, int B, int F, int
   return RMX_OK;
 }
 
-// [V][32] line copy of an fp32 k = 16 table: row i = [emb[i][0..16) | w[i] | 15 zeros], one 128-B
-// memory line per id (rmx_table::line).  Eight lanes per row, one float4 each (coalesced 128-B rows).
-__global__ __launch_bounds__(256) void pack_lines_kernel(int64_t V, const float* __restrict__ emb,
-                                                        const float* __restrict__ w, float* __restrict__ line) {
+// [V][32] line copy of a k = 16 table: row i = [emb[i][0..16) | w[i] | 15 zeros] (rmx_table::line): one 128-B
+// memory line per id for fp32, one 64-B half line for bf16.  One lane per 16-B piece (8 fp32 / 4 bf16 lanes
+// per row, coalesced rows).
+template <class T>
+__global__ __launch_bounds__(256) void pack_lines_kernel(int64_t V, const T* __restrict__ emb, const T* __restrict__ w,
+                                                        T* __restrict__ line) {
+  constexpr int E = 16 / sizeof(T);  // elements per 16-B piece
+  constexpr int P = 32 / E;          // pieces per line row
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t i = t >> 3;
-  const int c = (int)(t & 7);
+  const int64_t i = t / P;
+  const int c = (int)(t - i * P);
   if (i >= V) return;
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c < 4) v = reinterpret_cast<const float4*>(emb)[i * 4 + c];
-  else if (c == 4) v.x = w[i];
-  reinterpret_cast<float4*>(line)[i * 8 + c] = v;
+  if (c < 16 / E) {
+    v = reinterpret_cast<const float4*>(emb + i * 16)[c];
+  } else if (c == 16 / E) {
+    T* e = reinterpret_cast<T*>(&v);
+    e[0] = w[i];
+  }
+  reinterpret_cast<float4*>(line + i * 32)[c] = v;
 }
 
-int launch_pack_lines(hipStream_t s, int64_t V, const float* emb, const float* w, float* line) {
+int launch_pack_lines(hipStream_t s, int64_t V, const void* emb, const void* w, void* line, int dt) {
   if (V <= 0) return RMX_OK;
-  hipLaunchKernelGGL(pack_lines_kernel, dim3((unsigned)((V * 8 + 255) / 256)), dim3(256), 0, s, V, emb, w, line);
+  if (dt == kBF16)
+    hipLaunchKernelGGL(pack_lines_kernel<bf16_t>, dim3((unsigned)((V * 4 + 255) / 256)), dim3(256), 0, s, V,
+                       (const bf16_t*)emb, (const bf16_t*)w, (bf16_t*)line);
+  else
+    hipLaunchKernelGGL(pack_lines_kernel<float>, dim3((unsigned)((V * 8 + 255) / 256)), dim3(256), 0, s, V,
+                       (const float*)emb, (const float*)w, (float*)line);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -671,16 +671,20 @@ int model_collect_timing(rmx_model& m) {
   return RMX_OK;
 }
 
+// the models whose every table access in the forward takes a row / weight stride: LR, DeepFM / DNN (encoder,
+// gathered layer 1), and DCN when its cross stack rides layer 1 (dcn_fused: the gathered layer 1 and the
+// first-order kernel read the table, never cross16_kernel)
 bool model_reads_lines(const rmx_model& m) {
   return m.type == RMX_MODEL_LR ||
-         ((m.type == RMX_MODEL_DEEPFM || m.type == RMX_MODEL_DNN) && m.k == 16 && !needs_gather_x(m));
+         ((m.type == RMX_MODEL_DEEPFM || m.type == RMX_MODEL_DNN || (m.type == RMX_MODEL_DCN && m.dcn_fused)) &&
+          m.k == 16 && !needs_gather_x(m));
 }
 
 void table_inputs(const rmx_table& t, const rmx_model& m, FwdInputs& in) {
   in.dtype = t.dtype;
   if (t.line && model_reads_lines(m)) {
     in.table = t.line;
-    in.wtab = t.line + 16;
+    in.wtab = t.dtype == kBF16 ? (const void*)(reinterpret_cast<const bf16_t*>(t.line) + 16) : (const void*)(t.line + 16);
     in.ld = in.wld = 32;
   } else {
     in.table = t.emb;
@@ -701,9 +705,8 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // strided ([emb | w | pad] line) tables reach only kernels that take a row stride: the encoder and
   // the gathered tower layer 1 (DeepFM / DNN / LR)
   const bool strided = (in.ld > 0 && in.ld != k) || in.wld > 1;
-  if (strided && !(m.type == RMX_MODEL_LR || ((m.type == RMX_MODEL_DEEPFM || m.type == RMX_MODEL_DNN) &&
-                                              !needs_gather_x(m) && k == 16))) {
-    set_error("forward: a strided (line-row) table needs a DeepFM / DNN model with k = 16 or LR");
+  if (strided && !model_reads_lines(m)) {
+    set_error("forward: a strided (line-row) table needs LR, or a DeepFM / DNN / DCN (cross fused) model with k = 16");
     return RMX_E_INVALID;
   }
   if (m.type == RMX_MODEL_LR) {

@@ -21,13 +21,14 @@ struct rmx_table {
   int dtype = 0;          // RMX_DTYPE_F32 / RMX_DTYPE_BF16 (elements of w and emb)
   void* w = nullptr;      // [V]     first-order weights (Angel "weights" row 0)
   void* emb = nullptr;    // [V][k]  embeddings, row-major (Angel "embedding" rows 0..k-1, transposed)
-  // fp32 k = 16 tables with knob "table_lines" 1 (default 0): a [V][32] line copy, row = [emb 16 | w |
-  // pad 15] -- one 128-B memory line per id instead of a 64-B row line plus a separate weight line.
+  // k = 16 tables with knob "table_lines" 1 (default 0): a [V][32] line copy (elements of dtype), row =
+  // [emb 16 | w | pad 15] -- one 128-B memory line per id instead of a 64-B row line plus a separate weight
+  // line (fp32), or one 64-B half line instead of a 32-B row line plus a weight line (bf16, round 5).
   // Rebuilt from emb / w by every upload / fill (rmx_table_refresh_lines after writes through
   // device_ptrs); read by the models whose every table access takes a row stride
   // (rmx::model_reads_lines).  Measured ~1 % SLOWER for DeepFM layer 1 at V = 1M (0.1851 vs 0.1829 ms,
   // two A/B pairs on one box): the weight lines it saves hit the Infinity Cache, so it is off.
-  float* line = nullptr;
+  float* line = nullptr;   // (bf16 tables: bf16 elements)
 };
 
 namespace rmx {
@@ -43,7 +44,7 @@ struct FwdInputs {
   int dtype = 0;                   // kF32 / kBF16
   // row stride of `table` and stride of `wtab` in elements (0: k and 1).  ld = wld = 32 with
   // wtab = table + 16: [emb 16 | w | pad] line rows (a sharded partition read in place at one rank,
-  // or a replicated table's line copy); DeepFM / DNN / LR only (model_forward checks)
+  // or a replicated table's line copy); only the models of rmx::model_reads_lines (model_forward checks)
   int ld = 0, wld = 0;
   const float* y1 = nullptr;       // precomputed first order (L-A irregular index) or nullptr
   float beta = 0.f;
@@ -171,7 +172,7 @@ bool model_reads_lines(const rmx_model& m);
 // the forward's table operands: the line copy when the table has one and the model reads lines
 void table_inputs(const rmx_table& t, const rmx_model& m, FwdInputs& in);
 int table_refresh_lines(rmx_table& t);
-int launch_pack_lines(hipStream_t s, int64_t V, const float* emb, const float* w, float* line);
+int launch_pack_lines(hipStream_t s, int64_t V, const void* emb, const void* w, void* line, int dt);
 int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
                        float bias, const float* weights, const float* embedding, const float* mats,
                        float* out);

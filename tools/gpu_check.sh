@@ -33,9 +33,9 @@ for s in $STEPS; do
     benchd) run bench_driver 400 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     sqx:*) wl=${s#sqx:}
          run pmc_${wl}_sq 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU --output-format csv -d "$OUT/pmc_$wl/sq" -o sq -- \
-            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --settle-ms 0 &&
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --no-encoder-record --settle-ms 0 &&
          run pmc_${wl}_grbm 400 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmc_$wl/grbm" -o grbm -- \
-            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --settle-ms 0 ;;
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --no-encoder-record --settle-ms 0 ;;
     benchx) run bench_xdeepfm 400 python bench.py --workload xdeepfm --no-cpu-baseline ;;
     benchs) run bench_sharded 400 python bench.py --workload deepfm_sharded --no-cpu-baseline ;;
     benchb) run bench_dcn_bf16 400 python bench.py --workload dcn_bf16 --no-cpu-baseline &&
@@ -54,12 +54,12 @@ for s in $STEPS; do
             python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --settle-ms 0 ;;
     pmc:*) wl=${s#pmc:}
          run pmc_${wl}_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$wl/fetch" -o fetch -- \
-            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --settle-ms 0 &&
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --no-encoder-record --settle-ms 0 &&
          run pmc_${wl}_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_$wl/write" -o write -- \
-            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --settle-ms 0 ;;
+            python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --no-encoder-record --settle-ms 0 ;;
     prof:*) wl=${s#prof:}
          run prof_$wl 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$wl" -o $wl -- \
-            python3 bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline --no-companion ;;
+            python3 bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline --no-companion --no-encoder-record ;;
     settle) for ms in 0 100 400 1000; do
               run settle_$ms 200 python bench.py --steps 20 --warmup 5 --no-companion --no-cpu-baseline --settle-ms $ms
             done ;;
