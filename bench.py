@@ -719,7 +719,8 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
             roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
             if "mfma_util" in ent:  # measured matrix-pipe occupancy of the same kernel (profiled run)
                 roof["mfma_util_pmc"] = ent["mfma_util"]
-                summ = next((q for q in ("profiles/r04/pmc_%s_summary.txt" % workload,
+                summ = next((q for q in ("profiles/r05/pmc_%s_summary.txt" % workload,
+                                         "profiles/r04/pmc_%s_summary.txt" % workload,
                                          "profiles/r03/pmc_%s_summary.txt" % workload)
                              if os.path.exists(os.path.join(ROOT, q))), None)
                 roof["mfma_util_source"] = ("rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), "
