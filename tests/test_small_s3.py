@@ -30,9 +30,11 @@ def ctx():
 
 @pytest.fixture(autouse=True)
 def _restore_knobs():
+    rmx.set_tuning("s3_grid", 0)  # (the grid tower, k_grid_s3.hip, takes B >= 1,024 by default)
     yield
     rmx.set_tuning("s3_small", None)
     rmx.set_tuning("s3_small_rt", None)
+    rmx.set_tuning("s3_grid", None)
 
 
 def _run(ctx, B, V, mats, rt=0):
@@ -93,7 +95,7 @@ def test_small_tower_first_order_and_fm_bitwise(ctx, B, rt):
 @pytest.mark.parametrize("B", [4096, 8192])
 def test_small_tower_auto_selection(ctx, B):
     """knob s3_small 1 (auto) takes the whole-tower kernel while one round of its 16- / 32-sample blocks
-    covers the batch: at B = 4,096 and 8,192 the forward is the one launch."""
+    covers the batch (with the grid tower off): at B = 4,096 and 8,192 the forward is the one launch."""
     rmx.set_tuning("s3_small", 1)
     V = 50000
     m = rmx.DeepFM(V, F, K, list(FC))

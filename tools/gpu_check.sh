@@ -95,6 +95,11 @@ for s in $STEPS; do
              run abw_${wl}_${knob}_${v}_${i} 300 python bench.py --workload $wl --no-companion --no-encoder-record --no-cpu-baseline --steps 100 --warmup 10 --set $knob=$v || exit $?
            done
          done ;;
+    gridab) for B in 1024 2048 4096 8192; do   # the grid tower (s3_grid 1) vs the whole-tower kernel (0) per batch
+              for v in 1 0; do
+                run gridab_b${B}_${v} 300 python bench.py --batch $B --no-companion --no-encoder-record --parity-only --steps 400 --warmup 20 --set s3_grid=$v || exit $?
+              done
+            done ;;
     testk:*) k=${s#testk:}
          run pytest_$k 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k $k ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
