@@ -46,21 +46,25 @@ constexpr int kGW = 8;                   // waves per block
 constexpr int kGThreads = kGW * 64;
 constexpr int kGRows = kGW * 16;         // rows per row group
 constexpr int kGMaxF = 40;
-constexpr int kGA = 3 * 2048;            // per wave: 3 A slots of 2 KiB (rows of 2 fields, or 16 rows x 32 K of h)
-constexpr int kGId = 4 * 128;            // per wave: 4 id slots of [2 fields][16]
-constexpr int kGWr = 3 * 128;            // per wave: 3 first-order weight slots
-constexpr int kGWave = kGA + kGId + kGWr;
 constexpr int kGKS2 = 13;                // K steps of layers 2 / 3
 
-template <int NT>
+// NT column tiles per block; L units of lead: the weight ring, the A slots (per wave: 2 KiB each -- two fields'
+// rows of 16 samples, or 16 rows x 32 K of h), the first-order weight slots and the id slots all hold L + 1
+// units.  A unit of a few tiles lasts well under the L2 / Infinity-Cache latency, so the ring has to run
+// several units ahead (Little's law: in-flight bytes / latency = the CU's fetch rate); L is as deep as LDS
+// allows for the NT (the A slots dominate: 16 KiB per unit per block).
+template <int NT, int L>
 struct GCfg {
+  static constexpr int S = L + 1;                   // slots of every ring
   static constexpr int NINS = 3 * NT;              // 1-KiB pieces per unit
   static constexpr int Q = (NINS + kGW - 1) / kGW;  // per wave (the last wave repeats a piece when short)
   static constexpr int UNIT = NINS * 1024;
+  static constexpr int A = S * 2048, ID = S * 128, WR = S * 128;
+  static constexpr int WAVE = A + ID + WR;          // per-wave LDS
   static constexpr int PRM = 4 * 16 * NT;          // b1 | b2 | b3 | wo of the block's columns
-  static constexpr size_t LDS = (size_t)3 * UNIT + (size_t)kGW * kGWave + sizeof(float) * PRM + 16;
+  static constexpr size_t LDS = (size_t)S * UNIT + (size_t)kGW * WAVE + sizeof(float) * PRM + 16;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
 };
-static_assert(GCfg<7>::LDS <= 160 * 1024, "LDS budget");
 
 struct GridArgs {
   int M, F, KS1, R, C;
@@ -81,21 +85,22 @@ struct GridArgs {
 
 __device__ __forceinline__ int g_clamp_tile(int T) { return T < kQNT ? T : kQNT; }  // tile 25: zero weights
 
-// piece q of this wave in unit (layer l, K step c) of column group cg into ring slot `slot`
-template <int NT>
+// piece q of this wave in unit (layer of W, K step c) of column group cg into ring slot `slot`
+template <int NT, int L>
 __device__ __forceinline__ void g_wdma(const bf16_t* W, int c, int cg, char* lds, int slot, int w, int q, int lo) {
+  using Cfg = GCfg<NT, L>;
   int ins = w + q * kGW;
-  ins = ins < GCfg<NT>::NINS ? ins : GCfg<NT>::NINS - 1;
+  ins = ins < Cfg::NINS ? ins : Cfg::NINS - 1;
   const int pl = ins / NT, tl = ins - pl * NT;
   const int T = g_clamp_tile(cg * NT + tl);
   int l = lo;
   asm volatile("" : "+v"(l));
   const bf16_t* s = W + ((int64_t)(c * 3 + pl) * kQN + 16 * T) * 32 + l;
-  lds_dma<16>(s, lds + slot * GCfg<NT>::UNIT + ins * 1024);
+  lds_dma<16>(s, lds + slot * Cfg::UNIT + ins * 1024);
 }
 
 // the weight source (layer, K step) of unit u of the launch's unit sequence (layer 1: KS1 units, then 13 +
-// 13); past the end: the last unit again (the trailing DMAs of a ring that runs 2 units ahead)
+// 13); past the end: the last unit again (the trailing DMAs of a ring that runs L units ahead)
 __device__ __forceinline__ void g_unit_of(const GridArgs& p, int u, const bf16_t*& W, int& c) {
   const int n = p.KS1 + 2 * kGKS2;
   u = u < n ? u : n - 1;
@@ -111,12 +116,13 @@ __device__ __forceinline__ void g_unit_of(const GridArgs& p, int u, const bf16_t
   }
 }
 
-// one unit's MFMAs over the block's NT tiles, unit U + 2's Q pieces riding tiles 0 .. Q - 1
-template <int NT>
+// one unit's MFMAs over the block's NT tiles, unit U + L's Q pieces riding tiles 0 .. Q - 1
+template <int NT, int L>
 __device__ __forceinline__ void g_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                        f32x4 (&acc)[NT], const bf16_t* dW, int dc, int cg, char* lds, int dslot, int w,
                                        int lo) {
   constexpr int PF = NT >= 2 ? 2 : 1;
+  static_assert(GCfg<NT, L>::Q <= NT, "the unit's DMAs ride its tiles");
   f32x4 bq[PF + 1][3];
   int fbu = fb;
   asm volatile("" : "+v"(fbu));
@@ -129,7 +135,7 @@ __device__ __forceinline__ void g_unit(const char* ub, int fb, const bf16x8& ah,
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (t + PF < NT) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
-    if (t < GCfg<NT>::Q) g_wdma<NT>(dW, dc, cg, lds, dslot, w, t, lo);
+    if (t < GCfg<NT, L>::Q) g_wdma<NT, L>(dW, dc, cg, lds, dslot, w, t, lo);
     __builtin_amdgcn_sched_barrier(0);
     const f32x4* b = bq[t % (PF + 1)];
     const bf16x8 bh = __builtin_bit_cast(bf16x8, b[0]);
@@ -144,39 +150,41 @@ __device__ __forceinline__ void g_unit(const char* ub, int fb, const bf16x8& ah,
     d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, d, 0, 0, 0);
     acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, d, 0, 0, 0);
   }
-  if constexpr (GCfg<NT>::Q > NT) {  // (never: Q <= NT for every NT used)
-#pragma unroll
-    for (int q = NT; q < GCfg<NT>::Q; ++q) g_wdma<NT>(dW, dc, cg, lds, dslot, w, q, lo);
-  }
 }
 
-// ids of K step c (lanes 0 .. 31: field 2c + (L >> 4) of the wave's row L & 15; -1 past M / F) into id slot c & 3
+// ids of K step c (lanes 0 .. 31: field 2c + (L >> 4) of the wave's row L & 15; -1 past M / F / the last step)
+// into id slot c % S
+template <int NT, int L>
 __device__ __forceinline__ void g_id_dma(const GridArgs& p, char* wl, int row0, int c, int w, int lane) {
+  using Cfg = GCfg<NT, L>;
   int f = lane >> 4, r = lane & 15;
   asm volatile("" : "+v"(f), "+v"(r));
   const int m = row0 + w * 16 + r, fld = 2 * c + f;
   const bool ok = m < p.M && fld < p.F && c < p.KS1;
   const int32_t* src = ok ? p.ids + (int64_t)m * p.F + fld : g_rmx_neg1;
-  if (lane < 32) lds_dma<4>(src, wl + kGA + (c & 3) * 128);
+  if (lane < 32) lds_dma<4>(src, wl + Cfg::A + (c % Cfg::S) * 128);
 }
 
-// rows (2 DMAs) and first-order weights of K step c from its ids (id slot c & 3) into A slot c % 3 / weight slot c % 3
+// rows (2 DMAs) and first-order weights of K step c from its ids (id slot c % S) into A slot c % S / weight slot
+template <int NT, int L>
 __device__ __forceinline__ void g_row_dma(const GridArgs& p, char* wl, int c, int lane) {
-  const int* ids = reinterpret_cast<const int*>(wl + kGA + (c & 3) * 128);
+  using Cfg = GCfg<NT, L>;
+  const int sl = c % Cfg::S;
+  const int* ids = reinterpret_cast<const int*>(wl + Cfg::A + sl * 128);
   int r = lane >> 2, g = swz_slot(lane >> 2, lane & 3), lw = lane & 31;
   asm volatile("" : "+v"(r), "+v"(g), "+v"(lw));
   const int id0 = ids[r], id1 = ids[16 + r], idw = ids[lw];
   const float* zero16 = g_rmx_zero16;
-  const int sl = c % 3;
   char* a = wl + sl * 2048;
   lds_dma<16>(id0 >= 0 ? p.table + ((int64_t)id0 << p.gsh) + 4 * g : zero16, a);
   lds_dma<16>(id1 >= 0 ? p.table + ((int64_t)id1 << p.gsh) + 4 * g : zero16, a + 1024);
-  if (lane < 32) lds_dma<4>(idw >= 0 ? p.wtab + ((int64_t)idw << p.wsh) : zero16, wl + kGA + kGId + sl * 128);
+  if (lane < 32) lds_dma<4>(idw >= 0 ? p.wtab + ((int64_t)idw << p.wsh) : zero16, wl + Cfg::A + Cfg::ID + sl * 128);
 }
 
-// 16 rows x 32 K of h (K step c, columns 32 c ..) into A slot c % 3 (k_tail_s3.hip q_h1_dma: lane L, instruction
+// 16 rows x 32 K of h (K step c, columns 32 c ..) into A slot c % S (k_tail_s3.hip q_h1_dma: lane L, instruction
 // i: row 8 i + (L >> 3), physical 16-B slot L & 7 = logical slot (L & 7) ^ (row & 7)); past M or past the last
 // step: the zero row
+template <int NT, int L>
 __device__ __forceinline__ void g_h_dma(const GridArgs& p, const float* H, char* wl, int row0, int c, int w, int lane) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -185,16 +193,17 @@ __device__ __forceinline__ void g_h_dma(const GridArgs& p, const float* H, char*
     const int m = row0 + w * 16 + r;
     const bool ok = m < p.M && c < kGKS2;
     const float* src = ok ? H + (int64_t)m * kQN + 32 * c + 4 * j : g_rmx_zero16;
-    lds_dma<16>(src, wl + (c % 3) * 2048 + i * 1024);
+    lds_dma<16>(src, wl + (c % GCfg<NT, L>::S) * 2048 + i * 1024);
   }
 }
 
 // the h fragment of step c from its slot (zero at step 12's upper half: columns 400 .. 415 are padding)
+template <int NT, int L>
 __device__ __forceinline__ void g_h_read(const char* wl, int c, int lane, f32x4& a0, f32x4& a1) {
   const int r = lane & 15, g = lane >> 4;
   int o0 = r * 128 + ((g ^ (r & 7)) << 4), o1 = r * 128 + (((g + 4) ^ (r & 7)) << 4);
   asm volatile("" : "+v"(o0), "+v"(o1));
-  const char* h = wl + (c % 3) * 2048;
+  const char* h = wl + (c % GCfg<NT, L>::S) * 2048;
   a0 = *reinterpret_cast<const f32x4*>(h + o0);
   a1 = *reinterpret_cast<const f32x4*>(h + o1);
   if (c == kGKS2 - 1) a1 = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -237,15 +246,16 @@ __device__ __forceinline__ bool g_acquire(uint32_t* cnt, uint32_t want, uint32_t
   return ok_s != 0;
 }
 
-template <int NT>
+template <int NT, int L>
 __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p) {
   extern __shared__ __attribute__((aligned(16))) char gsmem[];
-  using Cfg = GCfg<NT>;
+  using Cfg = GCfg<NT, L>;
+  constexpr int S = Cfg::S;
   char* lds = gsmem;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
-  char* wl = gsmem + 3 * Cfg::UNIT + w * kGWave;
-  float* prm = reinterpret_cast<float*>(gsmem + 3 * Cfg::UNIT + kGW * kGWave);  // [4][16 NT]
+  char* wl = gsmem + S * Cfg::UNIT + w * Cfg::WAVE;
+  float* prm = reinterpret_cast<float*>(gsmem + S * Cfg::UNIT + kGW * Cfg::WAVE);  // [4][16 NT]
   int& ok_s = *reinterpret_cast<int*>(prm + Cfg::PRM);
   const int r = blockIdx.x / p.C, cg = blockIdx.x - r * p.C;
   const int row0 = r * kGRows;
@@ -262,18 +272,19 @@ __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p)
   asm volatile("" : "+v"(lo));
   const int fb = q_fbase(lane);
 
-  // prologue: ids of steps 0 .. 3, rows of steps 0, 1, the weights of units 0 and 1
-  for (int c = 0; c < 4; ++c) g_id_dma(p, wl, row0, c, w, lane);
+  // prologue: ids of steps 0 .. L, rows of steps 0 .. L - 1 (reading those ids), then the ids of steps L + 1 ..
+  // 2L - 1 into the slots of steps 0 .. L - 2 (their ids already read), the weights of units 0 .. L - 1
+  for (int c = 0; c <= L; ++c) g_id_dma<NT, L>(p, wl, row0, c, w, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  g_row_dma(p, wl, 0, lane);
-  g_row_dma(p, wl, 1, lane);
+  for (int c = 0; c < L; ++c) g_row_dma<NT, L>(p, wl, c, lane);
+  for (int c = L + 1; c < 2 * L; ++c) g_id_dma<NT, L>(p, wl, row0, c, w, lane);
   {
     const bf16_t* W;
     int c;
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < L; ++u) {
       g_unit_of(p, u, W, c);
 #pragma unroll
-      for (int q = 0; q < Cfg::Q; ++q) g_wdma<NT>(W, c, cg, lds, u, w, q, lo);
+      for (int q = 0; q < Cfg::Q; ++q) g_wdma<NT, L>(W, c, cg, lds, u, w, q, lo);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -288,33 +299,36 @@ __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p)
   float y1 = 0.f;
 #pragma unroll 1
   for (int c = 0; c < KS1; ++c, ++u) {
-    q_enter<4 + Cfg::Q>();  // unit c - 2's weights and step c's rows (issued 2 units ago) have landed
+    // the DMAs of unit c - L (step c's rows, unit c's weights) have landed: only the L - 1 units since may
+    // still be in flight (4 + Q vector-memory instructions each)
+    q_enter<(L - 1) * (4 + Cfg::Q)>();
     bf16x8 ah, am, al;
     {
       int o = r16 * 64 + swz_slot(r16, g) * 16;
       asm volatile("" : "+v"(o));
-      const char* a = wl + (c % 3) * 2048;
+      const char* a = wl + (c % S) * 2048;
       const f32x4 a0 = *reinterpret_cast<const f32x4*>(a + o);
       const f32x4 a1 = *reinterpret_cast<const f32x4*>(a + 1024 + o);
       if (cg == 0) {
 #pragma clang fp contract(off)
-        const float* wr = reinterpret_cast<const float*>(wl + kGA + kGId + (c % 3) * 128);
+        const float* wr = reinterpret_cast<const float*>(wl + Cfg::A + Cfg::ID + (c % S) * 128);
         fm_accum(a0, a1, fs, fq);  // (SecondOrderEncoder sums, field order)
         y1 += wr[r16];             // first order in field order (encoder_k16_kernel<0>)
         y1 += wr[16 + r16];
       }
       split3(a0, a1, ah, am, al);
     }
-    // ids 4 steps ahead (their slot held step c's, read by step c - 2's row DMAs), rows + weights 2 ahead
-    g_id_dma(p, wl, row0, c + 4, w, lane);
-    g_row_dma(p, wl, c + 2, lane);
+    // ids 2L steps ahead (their slot held step c + L - 1's, read by this wave's row DMA one unit ago), rows +
+    // weights L steps ahead (their slots held step c - 1's, read one unit ago)
+    g_id_dma<NT, L>(p, wl, row0, c + 2 * L, w, lane);
+    g_row_dma<NT, L>(p, wl, c + L, lane);
     __builtin_amdgcn_sched_barrier(0);
     const bf16_t* dW;
     int dc;
-    g_unit_of(p, u + 2, dW, dc);
-    const int dslot = slot == 0 ? 2 : slot - 1;
-    g_unit<NT>(lds + slot * Cfg::UNIT, fb, ah, am, al, acc, dW, dc, cg, lds, dslot, w, lo);
-    slot = q_next(slot);
+    g_unit_of(p, u + L, dW, dc);
+    const int dslot = slot == 0 ? S - 1 : slot - 1;  // (slot + L) mod S: unit u - 1's, read before this barrier
+    g_unit<NT, L>(lds + slot * Cfg::UNIT, fb, ah, am, al, acc, dW, dc, cg, lds, dslot, w, lo);
+    slot = slot == S - 1 ? 0 : slot + 1;
   }
   __builtin_amdgcn_sched_barrier(0);
   float pre = 0.f;
@@ -330,7 +344,7 @@ __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p)
       for (int t = 0; t < 4; ++t) a += __shfl(d[t], gg * 16 + r16);
     pre = y1 + 0.5f * (a / 16.0f);
   }
-  // h1 = ReLU(acc + b1) -> global (sc1), then the hand-off
+  // h_l = ReLU(acc + b_l) -> global (sc1), then the hand-off
   auto store_h = [&](float* H, const float* bl) {
     if (m < p.M) {
 #pragma unroll
@@ -351,28 +365,27 @@ __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p)
 #pragma unroll 1
   for (int l = 1; l < 3; ++l) {
     const float* Hin = l == 1 ? p.h1 : p.h2;
-    g_h_dma(p, Hin, wl, row0, 0, w, lane);
-    g_h_dma(p, Hin, wl, row0, 1, w, lane);
+    for (int c = 0; c < L; ++c) g_h_dma<NT, L>(p, Hin, wl, row0, c, w, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
     for (int c = 0; c < kGKS2; ++c, ++u) {
-      q_enter<2 + Cfg::Q>();
+      q_enter<(L - 1) * (2 + Cfg::Q)>();
       bf16x8 ah, am, al;
       {
         f32x4 a0, a1;
-        g_h_read(wl, c, lane, a0, a1);
+        g_h_read<NT, L>(wl, c, lane, a0, a1);
         split3(a0, a1, ah, am, al);
       }
-      g_h_dma(p, Hin, wl, row0, c + 2, w, lane);
+      g_h_dma<NT, L>(p, Hin, wl, row0, c + L, w, lane);
       __builtin_amdgcn_sched_barrier(0);
       const bf16_t* dW;
       int dc;
-      g_unit_of(p, u + 2, dW, dc);
-      const int dslot = slot == 0 ? 2 : slot - 1;
-      g_unit<NT>(lds + slot * Cfg::UNIT, fb, ah, am, al, acc, dW, dc, cg, lds, dslot, w, lo);
-      slot = q_next(slot);
+      g_unit_of(p, u + L, dW, dc);
+      const int dslot = slot == 0 ? S - 1 : slot - 1;
+      g_unit<NT, L>(lds + slot * Cfg::UNIT, fb, ah, am, al, acc, dW, dc, cg, lds, dslot, w, lo);
+      slot = slot == S - 1 ? 0 : slot + 1;
     }
     __builtin_amdgcn_sched_barrier(0);
     if (l == 1) {
@@ -397,8 +410,7 @@ __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p)
   part += __shfl_xor(part, 16);
   part += __shfl_xor(part, 32);
   if (g == 0 && m < p.M) g_store1_sc1(p.part + (int64_t)cg * p.M + m, part);
-  g_publish(cnt, tid);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the ring's trailing DMAs land before the LDS is released)
+  g_publish(cnt, tid);  // (its vmcnt(0) also lands the ring's trailing DMAs before the LDS is released)
   if (cg != 0) return;
   ok = g_acquire(cnt, 3u * p.C, p.tmo, tid, ok_s) && ok;
   // ---- head (column group 0): the partial logits in column-group order, bias, CAddTable, sigmoid ----
@@ -411,6 +423,12 @@ __global__ __launch_bounds__(kGThreads, 1) void tower_grid_s3_kernel(GridArgs p)
     tt = tt + oa.beta;
     oa.out[m] = ok ? 1.0f / (1.0f + expf(-tt)) : __builtin_nanf("");
   }
+}
+
+// the lead per column-tile count (as deep as LDS allows: GCfg::LDS <= 160 KiB)
+template <int NT>
+constexpr int grid_lead() {
+  return NT == 1 ? 6 : (NT == 2 ? 5 : (NT == 4 ? 4 : 3));
 }
 
 // NT (column tiles per block) for M rows on ncu CUs: the smallest of 1, 2, 4, 7 whose grid (row groups x
@@ -489,12 +507,14 @@ int launch_tower_grid_s3(hipStream_t s, const rmx_model& m, int M, int F, const 
   void* args[] = {&p};
   const dim3 grid(p.R * p.C), block(kGThreads);
   switch (nt) {
-#define RMX_GRID_LAUNCH(N)                                                                                          \
-  case N:                                                                                                           \
-    RMX_HIP(hipFuncSetAttribute((const void*)tower_grid_s3_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                (int)GCfg<N>::LDS));                                                                \
-    RMX_HIP(hipLaunchCooperativeKernel((const void*)tower_grid_s3_kernel<N>, grid, block, args, GCfg<N>::LDS, s));  \
-    break;
+#define RMX_GRID_LAUNCH(N)                                                                                         \
+  case N: {                                                                                                        \
+    constexpr int LL = grid_lead<N>();                                                                             \
+    const void* fn = (const void*)tower_grid_s3_kernel<N, LL>;                                                     \
+    RMX_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GCfg<N, LL>::LDS));          \
+    RMX_HIP(hipLaunchCooperativeKernel(fn, grid, block, args, GCfg<N, LL>::LDS, s));                               \
+    break;                                                                                                         \
+  }
     RMX_GRID_LAUNCH(1)
     RMX_GRID_LAUNCH(2)
     RMX_GRID_LAUNCH(4)
