@@ -52,7 +52,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 PEAK_S3_TFLOPS = PEAK_BF16_TFLOPS / 6
 # stages whose GEMMs run on the split (f32_split on): priced against its peak.  The backward stages
 # (dW and dX on the split; the CIN backward's rocBLAS part is fp32) take the higher peak too.
-S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "tower_fused", "tower_grid", "cin", "tower_back")
+S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "tower_fused", "cin", "tower_back")
 
 
 def parse():
@@ -140,8 +140,8 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", 2.0 * B * FC[0] * FC[1]
     if stage == "tower_layer3":
         return "flop", 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]
-    if stage in ("tower_small", "tower_fused", "tower_grid"):  # the whole tower (+ the output dot) in one launch
-        # (csrc/k_small_s3.hip, k_fused_s3.hip, k_grid_s3.hip; the first order + FM sums ride along, not counted)
+    if stage in ("tower_small", "tower_fused"):  # the whole tower (+ the output dot) in one launch
+        # (csrc/k_small_s3.hip, k_fused_s3.hip; the first order + FM sums ride along, not counted)
         return "flop", 2.0 * B * (k1 * FC[0] + FC[0] * FC[1] + FC[1] * FC[2] + FC[2])
     if stage == "tower_tail":  # layers 2 and 3 + the output dot in one launch (csrc/k_tail.hip, k_tail_s3.hip)
         return "flop", 2.0 * B * FC[0] * FC[1] + 2.0 * B * FC[1] * FC[2] + 2.0 * B * FC[2]

@@ -466,9 +466,6 @@ void model_release(rmx_model& m) {
   dev_free(m.ubuf[1]);
   dev_free(m.rowdot);
   dev_free(m.opart);
-  dev_free(m.gpart);
-  if (m.gsync) (void)hipFree(m.gsync);
-  m.gsync = nullptr;
   dev_free(m.la_E);
   dev_free(m.la_w);
   dev_free(m.la_E16);
@@ -597,9 +594,6 @@ int ensure_ws(rmx_model& m, int B) {
   dev_free(m.ubuf[1]);
   dev_free(m.rowdot);
   dev_free(m.opart);
-  dev_free(m.gpart);
-  if (m.gsync) (void)hipFree(m.gsync);
-  m.gsync = nullptr;
   int st;
   int maxN = 16;
   for (auto& L : m.layers) maxN = std::max(maxN, L.Npad);
@@ -608,16 +602,6 @@ int ensure_ws(rmx_model& m, int B) {
     if ((st = dev_alloc(&m.h[1], (size_t)B * maxN))) return st;
     // partial logits of an output layer run in column slices (k_gemm_s3.hip)
     if ((st = dev_alloc(&m.opart, (size_t)B * (m.layers.back().Npad / 208 + 1)))) return st;
-  }
-  if (m.type == RMX_MODEL_DEEPFM && !m.layers.empty()) {  // the grid tower's partial logits and hand-off words
-    if ((st = dev_alloc(&m.gpart, (size_t)B * 25))) return st;
-    m.gsync_bytes = ((size_t)(B / 128 + 1) + 8) * sizeof(uint32_t);
-    m.gsync_bytes = (m.gsync_bytes + 15) / 16 * 16;
-    if (hipMalloc(&m.gsync, m.gsync_bytes) != hipSuccess) {
-      m.gsync = nullptr;
-      set_error("out of device memory");
-      return RMX_E_NOMEM;
-    }
   }
   if ((st = dev_alloc(&m.y12, B))) return st;
   if ((st = dev_alloc(&m.pre2, B))) return st;
@@ -731,20 +715,6 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out, in.ld, in.wld);
   }
 
-  // DeepFM fp32 at a small launch batch (B >= 1,024 while a grid fits the CUs): the whole tower as a grid of row
-  // groups x column groups with in-launch hand-offs (k_grid_s3.hip; knob "s3_grid")
-  if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) &&
-      tower_grid_s3_usable(m, B, F, k, true)) {
-    StageTimer t(m, s, "tower_grid");
-    OutArgs oa{};
-    oa.wo = m.wo;
-    oa.bo = m.bo;
-    oa.has_bo = m.has_bo ? 1 : 0;
-    oa.beta = in.beta;
-    oa.out = in.out;
-    return launch_tower_grid_s3(s, m, B, F, in.ids, (const float*)in.table, in.ld, (const float*)in.wtab, in.wld, oa,
-                                m.h[0], m.h[1], m.gpart, m.gsync, m.gsync_bytes);
-  }
   // DeepFM fp32 at a small launch batch: the whole tower + first order + FM + head in one launch, one block
   // per 16 samples (k_small_s3.hip; knob "s3_small")
   if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) &&

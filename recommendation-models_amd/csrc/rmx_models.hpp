@@ -123,9 +123,6 @@ struct rmx_model {
   float* ubuf[2] = {nullptr, nullptr};  // [B*k][Npad] CIN maps
   float* rowdot = nullptr;            // [B*k] CIN per-row output partials
   float* opart = nullptr;             // [slices][B] partial logits of a column-sliced output layer
-  float* gpart = nullptr;             // DeepFM: [25][B] partial logits of the grid tower (k_grid_s3.hip)
-  uint32_t* gsync = nullptr;          // DeepFM: the grid tower's hand-off words
-  size_t gsync_bytes = 0;
   // L-A staging
   int64_t la_nnz = 0;
   int la_B = 0;
@@ -256,12 +253,6 @@ int launch_product(hipStream_t s, int B, int F, int k, const int32_t* ids, const
 int launch_gather_x(hipStream_t s, int B, int F, int k, const int32_t* ids, const void* table, int dt, void* xbuf,
                     int xdt, int ldx);
 int tower_npad_for(int N);
-// DeepFM's whole fp32 tower for small batches as a row-group x column-group grid with in-launch hand-offs
-// (k_grid_s3.hip): h1 / h2 [M][416] and part [25][M] scratch, sync: hand-off words (zeroed per call)
-bool tower_grid_s3_usable(const rmx_model& m, int M, int F, int k, bool ids);
-int launch_tower_grid_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,
-                         int ld, const float* wtab, int wld, const OutArgs& oa, float* h1, float* h2, float* part,
-                         uint32_t* sync, size_t sync_bytes);
 // DeepFM's whole fp32 tower for small batches, one block per 16 samples (k_small_s3.hip)
 bool tower_small_s3_usable(const rmx_model& m, int M, int F, int k, bool ids);
 int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const int32_t* ids, const float* table,

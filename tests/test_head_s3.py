@@ -32,9 +32,8 @@ def ctx():
 def _restore_knobs():
     rmx.set_tuning("s3_small", 0)  # (small batches would run the whole-tower kernel, k_small_s3.hip)
     rmx.set_tuning("s3_fused", 0)  # (and batches that fill the GPU the fused tower, k_fused_s3.hip)
-    rmx.set_tuning("s3_grid", 0)  # (and B >= 1,024 while it fits the grid tower, k_grid_s3.hip)
     yield
-    for k in ("s3_head", "s3_tail", "table_lines", "s3_small", "half_blocks", "s3_fused", "s3_grid"):
+    for k in ("s3_head", "s3_tail", "table_lines", "s3_small", "half_blocks", "s3_fused"):
         rmx.set_tuning(k, None)
 
 

@@ -18,7 +18,7 @@ TOL = 1e-5
 F, K = 39, 16
 SEED_IDS, SEED_TAB, SEED_MATS = 0x4A77, 0x7AB1E, 0x3A75
 FC = (400, 400, 400)
-KNOBS = ("s3_small", "s3_head", "s3_tail", "s3_fused", "s3_grid", "s3_narrow")
+KNOBS = ("s3_small", "s3_head", "s3_tail", "s3_fused", "s3_narrow")
 
 
 @pytest.fixture(scope="module")

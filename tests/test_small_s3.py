@@ -30,11 +30,9 @@ def ctx():
 
 @pytest.fixture(autouse=True)
 def _restore_knobs():
-    rmx.set_tuning("s3_grid", 0)  # (the grid tower, k_grid_s3.hip, takes B >= 1,024 by default)
     yield
     rmx.set_tuning("s3_small", None)
     rmx.set_tuning("s3_small_rt", None)
-    rmx.set_tuning("s3_grid", None)
 
 
 def _run(ctx, B, V, mats, rt=0):
@@ -95,7 +93,7 @@ def test_small_tower_first_order_and_fm_bitwise(ctx, B, rt):
 @pytest.mark.parametrize("B", [4096, 8192])
 def test_small_tower_auto_selection(ctx, B):
     """knob s3_small 1 (auto) takes the whole-tower kernel while one round of its 16- / 32-sample blocks
-    covers the batch (with the grid tower off): at B = 4,096 and 8,192 the forward is the one launch."""
+    covers the batch: at B = 4,096 and 8,192 the forward is the one launch."""
     rmx.set_tuning("s3_small", 1)
     V = 50000
     m = rmx.DeepFM(V, F, K, list(FC))
@@ -139,3 +137,4 @@ def test_small_tower_ignores_lds_leftovers(ctx, rt, pattern):
         res.append(out.numpy().copy())
     assert np.isfinite(res[1]).all()
     assert np.array_equal(res[0], res[1])
+

@@ -39,9 +39,7 @@ def ctx():
 def _restore_knobs():
     rmx.set_tuning("s3_small", 0)  # (small batches would run the whole-tower kernel, k_small_s3.hip)
     rmx.set_tuning("s3_fused", 0)  # (and DeepFM batches that fill the GPU the fused tower, k_fused_s3.hip)
-    rmx.set_tuning("s3_grid", 0)  # (and DeepFM at B >= 1,024 while it fits the grid tower, k_grid_s3.hip)
     yield
-    rmx.set_tuning("s3_grid", None)
     rmx.set_tuning("s3_tail", None)
     rmx.set_tuning("s3_small", None)
     rmx.set_tuning("s3_fused", None)

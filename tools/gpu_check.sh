@@ -95,11 +95,20 @@ for s in $STEPS; do
              run abw_${wl}_${knob}_${v}_${i} 300 python bench.py --workload $wl --no-companion --no-encoder-record --no-cpu-baseline --steps 100 --warmup 10 --set $knob=$v || exit $?
            done
          done ;;
-    gridab) for B in 1024 2048 4096 8192; do   # the grid tower (s3_grid 1) vs the whole-tower kernel (0) per batch
-              for v in 1 0; do
-                run gridab_b${B}_${v} 300 python bench.py --batch $B --no-companion --no-encoder-record --parity-only --steps 400 --warmup 20 --set s3_grid=$v || exit $?
-              done
-            done ;;
+    abb:*) rest=${s#abb:}   # abb:<batch>:<knob>=<v1>/<v2>/...: DeepFM at that batch, each value twice, interleaved
+         B=${rest%%:*}; kv=${rest#*:}; knob=${kv%%=*}; vals=$(echo ${kv#*=} | tr '/' ' ')
+         for i in 1 2; do
+           for v in $vals; do
+             run abb_b${B}_${knob}_${v}_${i} 300 python bench.py --batch $B --no-companion --no-encoder-record --parity-only --steps 400 --warmup 20 --set $knob=$v || exit $?
+           done
+         done ;;
+    pmcb:*) B=${s#pmcb:}   # DeepFM at launch batch B: kernel trace, SQ / GRBM counters, HBM fetch / write
+         A="python3 bench.py --batch $B --steps 20 --warmup 5 --no-cpu-baseline --no-companion --no-encoder-record --settle-ms 0"
+         run prof_b$B 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmcb_$B/prof" -o k -- $A &&
+         run pmc_b${B}_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmcb_$B/sq" -o sq -- $A &&
+         run pmc_b${B}_grbm 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcb_$B/grbm" -o grbm -- $A &&
+         run pmc_b${B}_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb_$B/fetch" -o fetch -- $A &&
+         run pmc_b${B}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb_$B/tcc" -o tcc -- $A ;;
     testk:*) k=${s#testk:}
          run pytest_$k 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k $k ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;

@@ -72,8 +72,7 @@ def stage_of(kernel, workload=""):
                     ("owner_gather", "shard_exchange"), ("own_rows_kernel", "shard_exchange"),
                     ("own_gather", "shard_exchange"), ("tower_tail_bf16_kernel", "tower_tail"),
                     ("tower_tail_s3_kernel", "tower_tail"), ("tower_head_s3_kernel", "tower_layer1"),
-                    ("tower_small_s3_kernel", "tower_small"), ("tower_fused_s3_kernel", "tower_fused"),
-                    ("tower_grid_s3_kernel", "tower_grid")):
+                    ("tower_small_s3_kernel", "tower_small"), ("tower_fused_s3_kernel", "tower_fused"),):
         if kernel.startswith(pat):
             return st
     return None
