@@ -435,7 +435,7 @@ ENC_VOCABS = (1_000_000, 100_000_000)
 
 
 def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
-    """The encoder alone (rmx_encoder_ids: gather + first order + FM of DeepFM, encoder_k16_kernel<1>) at
+    """The encoder alone (rmx_encoder_ids: gather + first order + FM of DeepFM, encoder_k16v2_kernel) at
     vocabulary Vw, with the [V][k] row table + [V] weights and with the [V][32] line copy (one 128-B line per
     id: knob table_lines), timed with HIP events on its stream: examples/s, algorithmic GB/s (2,812 B per
     example) against the 8 TB/s HBM peak, and the 128-B line rate (a random 64-B row or 4-B
@@ -456,7 +456,8 @@ def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
     lib.rmx_event_create(ctypes.byref(ev0))
     lib.rmx_event_create(ctypes.byref(ev1))
     bpe = F * 4 + F * 4 + F * K * 4 + 4
-    rec = {"kernel": "encoder_k16_kernel<1, float>", "batch": B, "vocab": Vw,
+    rec = {"kernel": ("encoder_k16v2_kernel (enc_u %d)" % rmx.get_tuning("enc_u", 20)) if rmx.get_tuning("enc_u", 20)
+           else "encoder_k16_kernel<1, float>", "batch": B, "vocab": Vw,
            "algorithmic_bytes_per_example": bpe, "peak_gbs": PEAK_HBM_GBS}
     saved = rmx.get_tuning("table_lines", 0)
     try:
@@ -512,7 +513,7 @@ def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
 
 def encoder_record(args, rmx, ctx, steps, warmup):
     """models.encoder of the default line: the encoder alone at V = 1M (Infinity-Cache resident) and 100M."""
-    out = {"note": ("the DeepFM forward fuses this encoder into tower layer 1 (k_head_s3.hip); timed alone here "
+    out = {"note": ("the DeepFM forward fuses this encoder into tower layer 1 (k_fused_s3.hip); timed alone here "
                     "for its HBM roofline (north_star, SURVEY.md §8d)")}
     for Vw in ENC_VOCABS:
         try:

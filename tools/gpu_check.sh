@@ -109,6 +109,9 @@ for s in $STEPS; do
          run pmc_b${B}_grbm 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcb_$B/grbm" -o grbm -- $A &&
          run pmc_b${B}_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb_$B/fetch" -o fetch -- $A &&
          run pmc_b${B}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb_$B/tcc" -o tcc -- $A ;;
+    wgprobe) for dg in 0 1 2 4 6 0; do   # dW timing probes (wgrad_sq_kernel DG; results wrong by construction)
+               run wgprobe_$dg 300 python bench.py --workload deepfm_train --steps 20 --warmup 5 --no-companion --set wgrad_diag=$dg || exit $?
+             done ;;
     testk:*) k=${s#testk:}
          run pytest_$k 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k $k ;;
     bench2) run bench_gpus2 400 python bench.py --gpus 2 --steps 20 --warmup 5 ;;
