@@ -69,7 +69,7 @@ __device__ __forceinline__ void s_ldw(const bf16_t* __restrict__ W, int c, int w
 // the 26 tiles are computed) -- read as zeros, as the tails do: its weights are zero, but the LDS there
 // holds whatever an earlier workgroup left, and 0 x a leftover NaN / Inf is NaN, which ReLU turns into a
 // silently wrong 0 (seen as one wrong row in some blocks, depending on what ran before on the CU)
-template <int NTW, int RT, bool PAD>
+template <int NTW, int RT, bool PAD, int DG>
 __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const float* xin, int xs, int KS, int w, int lane,
                                         f32x4 (&acc)[RT][kSTW], f32x4 (&bp)[NTW][3], const bf16_t* __restrict__ Wn) {
   const int g = lane >> 4, r16 = lane & 15;
@@ -87,10 +87,19 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
   int xo = r16 * xs + 4 * g;
   asm volatile("" : "+v"(xo));
   auto step = [&](int c, f32x4 (&cur)[NTW][3], f32x4 (&nxt)[NTW][3]) {
-    if (c + 1 < KS)
-      s_ldw<NTW>(W, c + 1, w, wo, nxt);
-    else if (Wn)
-      s_ldw<NTW>(Wn, 0, w, wo, nxt);
+    if constexpr ((DG & 2) == 0) {
+      // unconditional: the next step of this layer, the next layer's step 0, or past the last layer its last
+      // step again (unused) -- a load skipped on some path makes the compiler's vmcnt waits count only the
+      // loads of the other path, which drained this step's requests before its own MFMAs
+      const bool more = c + 1 < KS;
+      s_ldw<NTW>(more ? W : (Wn ? Wn : W), more ? c + 1 : (Wn ? 0 : KS - 1), w, wo, nxt);
+      __builtin_amdgcn_sched_barrier(0);  // (issued before this step's work: the scheduler would sink them)
+    } else {
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) nxt[j][pl] = cur[j][pl] + f32x4{1e-30f, 0.f, 0.f, 0.f};
+    }
     bf16x8 ah[RT], am[RT], al[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -106,6 +115,10 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
       const bf16x8 bl = __builtin_bit_cast(bf16x8, cur[j][2]);
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
+        if constexpr ((DG & 1) != 0) {
+          acc[t][j] += cur[j][0] + __builtin_bit_cast(f32x4, ah[t]);
+          continue;
+        }
         f32x4 d = acc[t][j];
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am[t], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[t], d, 0, 0, 0);
@@ -150,7 +163,7 @@ __device__ __forceinline__ void s_store_h(const f32x4 (&acc)[RT][kSTW], const fl
 // the whole block (every wave runs it, NTW = the wave's tile count): layer 1's first weight fragments are
 // requested before the prologue (ids, the gathered rows, the first-order weights, FM), so their latency
 // overlaps it; each layer's last K step requests the next layer's first fragments.
-template <int NTW, int RT>
+template <int NTW, int RT, int DG>
 __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lane) {
   constexpr int kSR = 16 * RT;
   float* x = ssmem;                       // [kSR][kSXS] gathered rows; later layer 2's output
@@ -168,29 +181,63 @@ __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lan
     asm volatile("" : "+v"(wo));
     s_ldw<NTW>(p.W[0], 0, w, wo, bp);
   }
-  for (int i = tid; i < 3 * kSN; i += kSThreads) {
-    const int a = i / kSN, n = i - a * kSN;
-    const float* src = a == 0 ? p.b[0] : (a == 1 ? p.b[1] : p.b[2]);  // (no dynamic index into the kernel args)
-    prm[i] = src ? src[n] : 0.f;
-  }
-  for (int i = tid; i < kSR * F; i += kSThreads) {
-    const int r = i / F, m = m0 + r;
-    sid[i] = m < p.M ? p.ids[(int64_t)m * F + (i - r * F)] : -1;
+  // the prologue's loads are issued a whole phase at a time (fixed trip counts, unrolled, every load
+  // unconditional: a slot past the data reads the zero / -1 words), so each phase waits one memory latency,
+  // not one per loop iteration: the biases and the ids, then the gathered rows and the first-order weights
+  // (both from the ids)
+  const float* zero16 = g_rmx_zero16;
+  const int* neg1 = g_rmx_neg1;
+  {
+    constexpr int NP = (3 * kSN + kSThreads - 1) / kSThreads, NI = (kSR * kSMaxF + kSThreads - 1) / kSThreads;
+    float pv[NP];
+    int iv[NI];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      const int i = tid + u * kSThreads, a = i / kSN, n = i - a * kSN;
+      const float* src = a == 0 ? p.b[0] : (a == 1 ? p.b[1] : p.b[2]);  // (no dynamic index into the kernel args)
+      pv[u] = *((i < 3 * kSN && src) ? src + n : zero16);
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int i = tid + u * kSThreads, r = i / F, m = m0 + r;
+      iv[u] = *((i < kSR * F && m < p.M) ? p.ids + (int64_t)m * F + (i - r * F) : neg1);
+    }
+#pragma unroll
+    for (int u = 0; u < NP; ++u)
+      if (tid + u * kSThreads < 3 * kSN) prm[tid + u * kSThreads] = pv[u];
+#pragma unroll
+    for (int u = 0; u < NI; ++u)
+      if (tid + u * kSThreads < kSR * F) sid[tid + u * kSThreads] = iv[u];
   }
   __syncthreads();
   // the gathered rows: x[r][16 f + j] (fields past F and rows past M: zero); the first-order weights
-  for (int i = tid; i < kSR * kSMaxF * 4; i += kSThreads) {
-    const int r = i / (kSMaxF * 4), rest = i - r * (kSMaxF * 4), f = rest >> 2, q = rest & 3;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (f < F) {
-      const int id = sid[r * F + f];
-      if (id >= 0) v = *reinterpret_cast<const float4*>(p.table + ((int64_t)id << p.gsh) + 4 * q);
+  {
+    constexpr int NX = (kSR * kSMaxF * 4 + kSThreads - 1) / kSThreads, NW = (kSR * kSMaxF + kSThreads - 1) / kSThreads;
+    float4 xv[NX];
+    float wv[NW];
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = tid + u * kSThreads;
+      const int r = i / (kSMaxF * 4), rest = i - r * (kSMaxF * 4), f = rest >> 2, q = rest & 3;
+      const int id = i < kSR * kSMaxF * 4 && f < F ? sid[r * F + f] : -1;
+      xv[u] = *reinterpret_cast<const float4*>((DG & 4) == 0 && id >= 0 ? p.table + ((int64_t)id << p.gsh) + 4 * q
+                                                                        : zero16);
     }
-    *reinterpret_cast<float4*>(x + r * kSXS + 16 * f + 4 * q) = v;
-  }
-  for (int i = tid; i < kSR * F; i += kSThreads) {
-    const int id = sid[i];
-    swt[i] = id >= 0 ? p.wtab[(int64_t)id << p.wsh] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) {
+      const int i = tid + u * kSThreads;
+      const int id = i < kSR * F ? sid[i] : -1;
+      wv[u] = *((DG & 4) == 0 && id >= 0 ? p.wtab + ((int64_t)id << p.wsh) : zero16);
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int i = tid + u * kSThreads;
+      const int r = i / (kSMaxF * 4), rest = i - r * (kSMaxF * 4), f = rest >> 2, q = rest & 3;
+      if (i < kSR * kSMaxF * 4) *reinterpret_cast<float4*>(x + r * kSXS + 16 * f + 4 * q) = xv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NW; ++u)
+      if (tid + u * kSThreads < kSR * F) swt[tid + u * kSThreads] = wv[u];
   }
   __syncthreads();
   // first order + FM of sample r (16 lanes per sample, lane j of the group: column j; wave w takes samples
@@ -219,16 +266,16 @@ __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lan
 
   f32x4 acc[RT][kSTW];
   // layer 1: x tile (row stride kSXS) -> h
-  s_layer<NTW, RT, false>(p.W[0], x, kSXS, p.KS1, w, lane, acc, bp, p.W[1]);  // (x: every column written)
+  s_layer<NTW, RT, false, DG>(p.W[0], x, kSXS, p.KS1, w, lane, acc, bp, p.W[1]);  // (x: every column written)
   s_store_h<NTW, RT>(acc, prm, h, w, lane);
   __syncthreads();
   // layer 2: h -> the x region (stride kSHS)
-  s_layer<NTW, RT, true>(p.W[1], h, kSHS, 13, w, lane, acc, bp, p.W[2]);
+  s_layer<NTW, RT, true, DG>(p.W[1], h, kSHS, 13, w, lane, acc, bp, p.W[2]);
   __syncthreads();  // every wave has read h ... (the x region is free since layer 1)
   s_store_h<NTW, RT>(acc, prm + kSN, x, w, lane);
   __syncthreads();
   // layer 3 + the output dot over the wave's columns
-  s_layer<NTW, RT, true>(p.W[2], x, kSHS, 13, w, lane, acc, bp, nullptr);
+  s_layer<NTW, RT, true, DG>(p.W[2], x, kSHS, 13, w, lane, acc, bp, nullptr);
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     float part = 0.f;
@@ -264,14 +311,14 @@ __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lan
   }
 }
 
-template <int RT>
+template <int RT, int DG>
 __global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs p) {
   extern __shared__ __attribute__((aligned(16))) float ssmem[];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (w == 0)
-    s_wave<4, RT>(p, ssmem, tid, w, lane);
+    s_wave<4, RT, DG>(p, ssmem, tid, w, lane);
   else
-    s_wave<3, RT>(p, ssmem, tid, w, lane);
+    s_wave<3, RT, DG>(p, ssmem, tid, w, lane);
 }
 
 }  // namespace
@@ -335,15 +382,17 @@ int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const
   }
   p.KS1 = (F + 1) / 2;
   p.oa = oa;
-  if (rt == 2) {
-    RMX_HIP(hipFuncSetAttribute((const void*)tower_small_s3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)small_lds<2>()));
-    hipLaunchKernelGGL(tower_small_s3_kernel<2>, dim3((M + 31) / 32), dim3(kSThreads), small_lds<2>(), s, p);
-  } else {
-    RMX_HIP(hipFuncSetAttribute((const void*)tower_small_s3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)small_lds<1>()));
-    hipLaunchKernelGGL(tower_small_s3_kernel<1>, dim3((M + 15) / 16), dim3(kSThreads), small_lds<1>(), s, p);
-  }
+  const int dg = tuning_get("s3_small_diag", 0);  // (timing probes, wrong results: 1 no MFMA, 2 no weight loads, 4 no gather)
+  const void* fn = (const void*)tower_small_s3_kernel<1, 0>;
+  if (rt == 2) fn = (const void*)tower_small_s3_kernel<2, 0>;
+#define RMX_DG(V) else if (rt == 1 && dg == V) fn = (const void*)tower_small_s3_kernel<1, V>;
+  if (dg == 0) {}
+  RMX_DG(1) RMX_DG(2) RMX_DG(3) RMX_DG(4) RMX_DG(7)
+#undef RMX_DG
+  const size_t lds = rt == 2 ? small_lds<2>() : small_lds<1>();
+  RMX_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* args[] = {&p};
+  RMX_HIP(hipLaunchKernel(fn, dim3((M + 16 * rt - 1) / (16 * rt)), dim3(kSThreads), args, lds, s));
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

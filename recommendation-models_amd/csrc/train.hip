@@ -1046,7 +1046,9 @@ constexpr int kSqT = 208, kSqW = kSqT / 16, kSqThr = kSqW * 64;
 // bias gradient, sum_b dPre[b][n], fused: the A items pass through registers anyway) into
 // cpart[slice][N], rows in order per staging thread, the 4 row octets added in order at the end.
 // GZ: X is the CIN outer product z = x0 (x) up generated while staged (as wgrad_s3_kernel / wgrad_nk_kernel).
-template <bool GZ>
+// DG (timing probes, results wrong; knob "wgrad_diag"): 1 no MFMAs, 2 no staging (loads, split, LDS
+// stores), 4 no LDS fragment reads
+template <bool GZ, int DG = 0>
 __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, int K, const float* __restrict__ A,
                                                              int lda, const float* __restrict__ X, int ldx,
                                                              int rows_per_slice, int tiles, float* __restrict__ part,
@@ -1108,6 +1110,7 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
   // barrier), then chunk c + 2's loads; part 0 = the A item, 1 = the X item and the loads
   auto stage_part = [&](int c, int part_) {
     if (c + 1 >= nch) return;
+    if constexpr ((DG & 2) != 0) return;
     const int buf = (c + 1) & 1, o = col * 4 + wg_slot(col, h);
     wg_bf16x8 p0, p1, p2;
     if (part_ == 0) col_sum();
@@ -1122,12 +1125,26 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
     wg_bf16x8 fx[3], fa[3];
     const int cx = wid * 16 + r16;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) fx[pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
+    for (int pl = 0; pl < 3; ++pl) {
+      if constexpr ((DG & 4) != 0)
+        fx[pl] = __builtin_bit_cast(wg_bf16x8, f32x4{(float)(c + pl), 1.f, 2.f, 3.f});
+      else
+        fx[pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
+    }
 #pragma unroll
     for (int a = 0; a < kSqW; ++a) {
       const int ca = a * 16 + r16;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) fa[pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+      for (int pl = 0; pl < 3; ++pl) {
+        if constexpr ((DG & 4) != 0)
+          fa[pl] = __builtin_bit_cast(wg_bf16x8, f32x4{(float)(a + pl), 1.f, (float)c, 3.f});
+        else
+          fa[pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+      }
+      if constexpr ((DG & 1) != 0) {
+        acc[a] += __builtin_bit_cast(f32x4, fa[0]) + __builtin_bit_cast(f32x4, fx[1]);
+        continue;
+      }
       f32x4 d = acc[a];
       d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[1], d, 0, 0, 0);
       d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fx[0], d, 0, 0, 0);
@@ -1289,9 +1306,19 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     RMX_HIP(hipFuncSetAttribute(zg ? (const void*)wgrad_sq_kernel<true> : (const void*)wgrad_sq_kernel<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     float* cpart = fuse_bias ? T.part2 + (int64_t)S * N * K : nullptr;
+    const int dg = zg ? 0 : tuning_get("wgrad_diag", 0);
     if (zg)
       hipLaunchKernelGGL(wgrad_sq_kernel<true>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, cpart, z);
+#define RMX_WG_DG(V)                                                                                              \
+    else if (dg == V) {                                                                                           \
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<false, V>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)lds));                                                                     \
+      hipLaunchKernelGGL((wgrad_sq_kernel<false, V>), dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X,   \
+                         ldx, rps, tiles, T.part2, cpart, z);                                                     \
+    }
+    RMX_WG_DG(1) RMX_WG_DG(2) RMX_WG_DG(3) RMX_WG_DG(4) RMX_WG_DG(6)
+#undef RMX_WG_DG
     else
       hipLaunchKernelGGL(wgrad_sq_kernel<false>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, cpart, z);
