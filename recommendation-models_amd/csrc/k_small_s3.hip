@@ -69,7 +69,7 @@ __device__ __forceinline__ void s_ldw(const bf16_t* __restrict__ W, int c, int w
 // the 26 tiles are computed) -- read as zeros, as the tails do: its weights are zero, but the LDS there
 // holds whatever an earlier workgroup left, and 0 x a leftover NaN / Inf is NaN, which ReLU turns into a
 // silently wrong 0 (seen as one wrong row in some blocks, depending on what ran before on the CU)
-template <int NTW, int RT, bool PAD, int DG>
+template <int NTW, int RT, bool PAD, int DG, bool IL>
 __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const float* xin, int xs, int KS, int w, int lane,
                                         f32x4 (&acc)[RT][kSTW], f32x4 (&bp)[NTW][3], const bf16_t* __restrict__ Wn) {
   const int g = lane >> 4, r16 = lane & 15;
@@ -87,18 +87,23 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
   int xo = r16 * xs + 4 * g;
   asm volatile("" : "+v"(xo));
   auto step = [&](int c, f32x4 (&cur)[NTW][3], f32x4 (&nxt)[NTW][3]) {
-    if constexpr ((DG & 2) == 0) {
-      // unconditional: the next step of this layer, the next layer's step 0, or past the last layer its last
-      // step again (unused) -- a load skipped on some path makes the compiler's vmcnt waits count only the
-      // loads of the other path, which drained this step's requests before its own MFMAs
-      const bool more = c + 1 < KS;
-      s_ldw<NTW>(more ? W : (Wn ? Wn : W), more ? c + 1 : (Wn ? 0 : KS - 1), w, wo, nxt);
+    // the next step's fragments, unconditionally: the next step of this layer, the next layer's step 0, or
+    // past the last layer its last step again (unused) -- a load skipped on some path makes the compiler's
+    // vmcnt waits count only the loads of the other path, which drained the next step's requests too
+    const bool more = c + 1 < KS;
+    const bf16_t* __restrict__ Ws = more ? W : (Wn ? Wn : W);
+    const int cs = more ? c + 1 : (Wn ? 0 : KS - 1);
+    auto ld = [&](int q) {  // fragment q = 3 j + pl of the next step
+      if constexpr ((DG & 2) == 0)
+        nxt[q / 3][q % 3] =
+            *reinterpret_cast<const f32x4*>(Ws + ((int64_t)(cs * 3 + q % 3) * kSN + 16 * (w + 8 * (q / 3))) * 32 + wo);
+      else
+        nxt[q / 3][q % 3] = cur[q / 3][q % 3] + f32x4{1e-30f, 0.f, 0.f, 0.f};
+    };
+    if constexpr (!IL) {
+#pragma unroll
+      for (int q = 0; q < 3 * NTW; ++q) ld(q);
       __builtin_amdgcn_sched_barrier(0);  // (issued before this step's work: the scheduler would sink them)
-    } else {
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) nxt[j][pl] = cur[j][pl] + f32x4{1e-30f, 0.f, 0.f, 0.f};
     }
     bf16x8 ah[RT], am[RT], al[RT];
 #pragma unroll
@@ -108,24 +113,31 @@ __device__ __forceinline__ void s_layer(const bf16_t* __restrict__ W, const floa
       if (PAD && c == KS - 1) a1 = f32x4{0.f, 0.f, 0.f, 0.f};
       split3(a0, a1, ah[t], am[t], al[t]);
     }
+    // the six products in the engine's order, each over all the wave's (row tile, column tile) pairs;
+    // IL: two of the next step's fragment loads after each product group, so a wave's vector-memory issue
+    // is spread over its MFMA stream instead of stalling it in one burst at the step head
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const bf16x8 bh = __builtin_bit_cast(bf16x8, cur[j][0]);
-      const bf16x8 bm = __builtin_bit_cast(bf16x8, cur[j][1]);
-      const bf16x8 bl = __builtin_bit_cast(bf16x8, cur[j][2]);
+    for (int pr = 0; pr < 6; ++pr) {
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        if constexpr ((DG & 1) != 0) {
-          acc[t][j] += cur[j][0] + __builtin_bit_cast(f32x4, ah[t]);
-          continue;
+      for (int j = 0; j < NTW; ++j) {
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, cur[j][0]);
+        const bf16x8 bm = __builtin_bit_cast(bf16x8, cur[j][1]);
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, cur[j][2]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          if constexpr ((DG & 1) != 0) {
+            if (pr == 0) acc[t][j] += cur[j][0] + __builtin_bit_cast(f32x4, ah[t]);
+            continue;
+          }
+          const bf16x8 wa = pr == 0 || pr == 4 ? bm : (pr == 2 ? bl : bh);
+          const bf16x8 xa = pr == 1 ? al[t] : (pr == 0 || pr == 3 ? am[t] : ah[t]);
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xa, acc[t][j], 0, 0, 0);
         }
-        f32x4 d = acc[t][j];
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am[t], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[t], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[t], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am[t], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah[t], d, 0, 0, 0);
-        acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[t], d, 0, 0, 0);
+      }
+      if constexpr (IL) {
+        if (2 * pr < 3 * NTW) ld(2 * pr);
+        if (2 * pr + 1 < 3 * NTW) ld(2 * pr + 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   };
@@ -163,7 +175,7 @@ __device__ __forceinline__ void s_store_h(const f32x4 (&acc)[RT][kSTW], const fl
 // the whole block (every wave runs it, NTW = the wave's tile count): layer 1's first weight fragments are
 // requested before the prologue (ids, the gathered rows, the first-order weights, FM), so their latency
 // overlaps it; each layer's last K step requests the next layer's first fragments.
-template <int NTW, int RT, int DG>
+template <int NTW, int RT, int DG, bool IL>
 __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lane) {
   constexpr int kSR = 16 * RT;
   float* x = ssmem;                       // [kSR][kSXS] gathered rows; later layer 2's output
@@ -266,16 +278,16 @@ __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lan
 
   f32x4 acc[RT][kSTW];
   // layer 1: x tile (row stride kSXS) -> h
-  s_layer<NTW, RT, false, DG>(p.W[0], x, kSXS, p.KS1, w, lane, acc, bp, p.W[1]);  // (x: every column written)
+  s_layer<NTW, RT, false, DG, IL>(p.W[0], x, kSXS, p.KS1, w, lane, acc, bp, p.W[1]);  // (x: every column written)
   s_store_h<NTW, RT>(acc, prm, h, w, lane);
   __syncthreads();
   // layer 2: h -> the x region (stride kSHS)
-  s_layer<NTW, RT, true, DG>(p.W[1], h, kSHS, 13, w, lane, acc, bp, p.W[2]);
+  s_layer<NTW, RT, true, DG, IL>(p.W[1], h, kSHS, 13, w, lane, acc, bp, p.W[2]);
   __syncthreads();  // every wave has read h ... (the x region is free since layer 1)
   s_store_h<NTW, RT>(acc, prm + kSN, x, w, lane);
   __syncthreads();
   // layer 3 + the output dot over the wave's columns
-  s_layer<NTW, RT, true, DG>(p.W[2], x, kSHS, 13, w, lane, acc, bp, nullptr);
+  s_layer<NTW, RT, true, DG, IL>(p.W[2], x, kSHS, 13, w, lane, acc, bp, nullptr);
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     float part = 0.f;
@@ -311,14 +323,14 @@ __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lan
   }
 }
 
-template <int RT, int DG>
+template <int RT, int DG, bool IL>
 __global__ __launch_bounds__(kSThreads, 1) void tower_small_s3_kernel(SmallArgs p) {
   extern __shared__ __attribute__((aligned(16))) float ssmem[];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (w == 0)
-    s_wave<4, RT, DG>(p, ssmem, tid, w, lane);
+    s_wave<4, RT, DG, IL>(p, ssmem, tid, w, lane);
   else
-    s_wave<3, RT, DG>(p, ssmem, tid, w, lane);
+    s_wave<3, RT, DG, IL>(p, ssmem, tid, w, lane);
 }
 
 }  // namespace
@@ -383,9 +395,12 @@ int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const
   p.KS1 = (F + 1) / 2;
   p.oa = oa;
   const int dg = tuning_get("s3_small_diag", 0);  // (timing probes, wrong results: 1 no MFMA, 2 no weight loads, 4 no gather)
-  const void* fn = (const void*)tower_small_s3_kernel<1, 0>;
-  if (rt == 2) fn = (const void*)tower_small_s3_kernel<2, 0>;
-#define RMX_DG(V) else if (rt == 1 && dg == V) fn = (const void*)tower_small_s3_kernel<1, V>;
+  // knob "s3_small_il": 1 (default) the next step's weight loads ride the MFMA groups, 0 issued at the step head
+  const bool il = tuning_get("s3_small_il", 1) != 0;
+  const void* fn = il ? (const void*)tower_small_s3_kernel<1, 0, true> : (const void*)tower_small_s3_kernel<1, 0, false>;
+  if (rt == 2)
+    fn = il ? (const void*)tower_small_s3_kernel<2, 0, true> : (const void*)tower_small_s3_kernel<2, 0, false>;
+#define RMX_DG(V) else if (rt == 1 && dg == V) fn = (const void*)tower_small_s3_kernel<1, V, true>;
   if (dg == 0) {}
   RMX_DG(1) RMX_DG(2) RMX_DG(3) RMX_DG(4) RMX_DG(7)
 #undef RMX_DG

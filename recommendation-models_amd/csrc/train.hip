@@ -20,6 +20,7 @@
 //   encoders  emb_grad_kernel: dL/dE = dx (tower) + FM term dz (s_j - e_fj) / k; dL/dw[n] =
 //             dz[index[n]] (Scatter backward).
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "rmx_models.hpp"
@@ -1047,9 +1048,15 @@ constexpr int kSqT = 208, kSqW = kSqT / 16, kSqThr = kSqW * 64;
 // cpart[slice][N], rows in order per staging thread, the 4 row octets added in order at the end.
 // GZ: X is the CIN outer product z = x0 (x) up generated while staged (as wgrad_s3_kernel / wgrad_nk_kernel).
 // DG (timing probes, results wrong; knob "wgrad_diag"): 1 no MFMAs, 2 no staging (loads, split, LDS
-// stores), 4 no LDS fragment reads
-template <bool GZ, int DG = 0>
-__global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, int K, const float* __restrict__ A,
+// stores), 4 no LDS fragment reads.
+// W16 (knob "wgrad_sq16"): 16 waves instead of 13, so each SIMD carries 4 waves of nearly equal MFMA work: with
+// 13, SIMD 0 holds waves 0, 4, 8, 12 (4 x 13 tiles) against 3 x 13 on the others, and the block waits for it.
+// Waves 0 .. 12 keep their k tile and take n tiles 0 .. 9; waves 13, 14, 15 take n tile 10, 11, 12 across all
+// 13 k tiles (per SIMD 40 / 43 / 43 / 43 tiles).  Each output still sees the same chunks and products in the
+// same order: bitwise the 13-wave kernel.  Threads past the 832 staging items only compute.
+constexpr int kSq16Thr = 1024;
+template <bool GZ, int DG = 0, bool W16 = false>
+__global__ __launch_bounds__(W16 ? kSq16Thr : kSqThr, 1) void wgrad_sq_kernel(int rows, int N, int K, const float* __restrict__ A,
                                                              int lda, const float* __restrict__ X, int ldx,
                                                              int rows_per_slice, int tiles, float* __restrict__ part,
                                                              float* __restrict__ cpart, WgZ zg) {
@@ -1067,7 +1074,8 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
   const int nch = r_end > r_begin ? (r_end - r_begin + kWgR - 1) / kWgR : 0;
   // staging item of this thread: column col of A (n0 + col) and of X (k0 + col), row octet h
   const int col = tid % kSqT, h = tid / kSqT;
-  const bool a_ok = n0 + col < N, x_ok = k0 + col < K;
+  const bool stager = !W16 || tid < kSqThr;  // (W16: threads 832 .. 1023 stage nothing)
+  const bool a_ok = stager && n0 + col < N, x_ok = stager && k0 + col < K;
   const bool csum_on = cpart != nullptr && k0 == 0;
   const int zf = GZ ? (k0 + col) / zg.Hp : 0, zh = GZ ? k0 + col - zf * zg.Hp : 0;  // (f, h) of column k
   float va[8], vx[8], csum = 0.f;
@@ -1090,6 +1098,7 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
       for (int q = 0; q < 8; ++q) csum += va[q];
   };
   auto sstore = [&](int buf) {
+    if (!stager) return;
     const int o = col * 4 + wg_slot(col, h);
     wg_bf16x8 p0, p1, p2;
     col_sum();
@@ -1111,6 +1120,7 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
   auto stage_part = [&](int c, int part_) {
     if (c + 1 >= nch) return;
     if constexpr ((DG & 2) != 0) return;
+    if (!stager) return;
     const int buf = (c + 1) & 1, o = col * 4 + wg_slot(col, h);
     wg_bf16x8 p0, p1, p2;
     if (part_ == 0) col_sum();
@@ -1119,6 +1129,42 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
     L(buf, part_, 1)[o] = p1;
     L(buf, part_, 2)[o] = p2;
     if (part_ == 1 && c + 2 < nch) gload(c + 2);
+  };
+  auto compute16 = [&](int c, auto typeb) {  // W16: the wave's tiles as described above (DG ignored)
+    const int cur = c & 1;
+    wg_bf16x8 fx[3], fa[3];
+    auto mf = [&](f32x4& acc_) {
+      f32x4 d = acc_;
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[1], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fx[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[2], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fx[0], d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[1], d, 0, 0, 0);
+      acc_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fx[0], d, 0, 0, 0);
+    };
+    if constexpr (!decltype(typeb)::value) {  // k tile wid, n tiles 0 .. 9
+      const int cx = wid * 16 + r16;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fx[pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
+#pragma unroll
+      for (int a = 0; a < 10; ++a) {
+        const int ca = a * 16 + r16;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) fa[pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+        mf(acc[a]);
+      }
+    } else {  // n tile wid - 3 (10 .. 12), k tiles 0 .. 12
+      const int ca = (wid - 3) * 16 + r16;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) fa[pl] = L(cur, 0, pl)[ca * 4 + wg_slot(ca, g)];
+#pragma unroll
+      for (int a = 0; a < kSqW; ++a) {
+        const int cx = a * 16 + r16;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) fx[pl] = L(cur, 1, pl)[cx * 4 + wg_slot(cx, g)];
+        mf(acc[a]);
+      }
+    }
   };
   auto compute = [&](int c) {
     const int cur = c & 1;
@@ -1160,26 +1206,56 @@ __global__ __launch_bounds__(kSqThr, 1) void wgrad_sq_kernel(int rows, int N, in
   }
   if (nch > 1) gload(1);
   __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    compute(c);
-    // (issuing this staging between the last MFMA tiles instead measured the same: DeepFM training
-    // tower backward 0.2955 vs 0.2975 ms per layer)
-    stage_part(c, 0);
-    stage_part(c, 1);
-    __syncthreads();
+  if constexpr (W16) {
+    // one loop per wave kind (wave-uniform), so each is register-allocated alone; both meet the same barriers
+    if (wid < kSqW) {
+      for (int c = 0; c < nch; ++c) {
+        compute16(c, std::false_type());
+        stage_part(c, 0);
+        stage_part(c, 1);
+        __syncthreads();
+      }
+    } else {
+      for (int c = 0; c < nch; ++c) {
+        compute16(c, std::true_type());
+        stage_part(c, 0);
+        stage_part(c, 1);
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int c = 0; c < nch; ++c) {
+      compute(c);
+      // (issuing this staging between the last MFMA tiles instead measured the same: DeepFM training
+      // tower backward 0.2955 vs 0.2975 ms per layer)
+      stage_part(c, 0);
+      stage_part(c, 1);
+      __syncthreads();
+    }
   }
   float* out = part + (int64_t)slice * N * K;
-  const int k = k0 + wid * 16 + r16;
+  if (W16 && wid >= kSqW) {
+    const int n1 = n0 + (wid - 3) * 16;
 #pragma unroll
-  for (int a = 0; a < kSqW; ++a)
+    for (int a = 0; a < kSqW; ++a)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + a * 16 + 4 * g + r;
-      if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][r];
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int n = n1 + 4 * g + r, k = k0 + a * 16 + r16;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][r];
+      }
+  } else {
+    const int k = k0 + wid * 16 + r16;
+#pragma unroll
+    for (int a = 0; a < (W16 ? 10 : kSqW); ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + a * 16 + 4 * g + r;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[a][r];
+      }
+  }
   if (csum_on) {  // block-uniform; the LDS image is free after the loop's last barrier
     float* red = reinterpret_cast<float*>(wlds);
-    red[h * kSqT + col] = csum;
+    if (stager) red[h * kSqT + col] = csum;
     __syncthreads();
     if (h == 0 && a_ok)
       cpart[(int64_t)slice * N + n0 + col] = ((red[col] + red[kSqT + col]) + red[2 * kSqT + col]) + red[3 * kSqT + col];
@@ -1307,7 +1383,14 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     float* cpart = fuse_bias ? T.part2 + (int64_t)S * N * K : nullptr;
     const int dg = zg ? 0 : tuning_get("wgrad_diag", 0);
-    if (zg)
+    // knob "wgrad_sq16": 16 waves balanced over the SIMDs (read operands only)
+    const bool w16 = !zg && dg == 0 && tuning_get("wgrad_sq16", 1) != 0;
+    if (w16) {
+      RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<false, 0, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL((wgrad_sq_kernel<false, 0, true>), dim3(tiles * S), dim3(kSq16Thr), lds, s, rows, N, K, A, lda,
+                         X, ldx, rps, tiles, T.part2, cpart, z);
+    } else if (zg)
       hipLaunchKernelGGL(wgrad_sq_kernel<true>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, cpart, z);
 #define RMX_WG_DG(V)                                                                                              \

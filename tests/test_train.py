@@ -468,6 +468,51 @@ def test_backward_wgrad_sq_tile(kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "dcn", "pnn"])
+@pytest.mark.parametrize("B", [32775, 65536])
+def test_backward_wgrad_sq16_bitwise(kind, B):
+    """The 16-wave 208 x 208 dW (wgrad_sq16 1, the default: waves 0 .. 12 take n tiles 0 .. 9 of their k
+    tile, waves 13 .. 15 n tiles 10 .. 12 of every k tile) against the 13-wave kernel (0): every output sees
+    the same chunks, the same six products in the same order and the same row slices, so every gradient
+    is bit-identical, bias fused or not."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K, fc = 20_000, 39, 16, (400, 400, 400)
+    m = _gpu_model(rmx, kind, V, F, K, fc)
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 5, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(7).random(B) > 0.7).astype(np.float32))
+    ml = len(mats)
+
+    def grads():
+        out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, ml, 1)]
+        m.backward_ids(t, B, ids, targets, *out)
+        ctx.sync()
+        return [o.numpy().copy() for o in out]
+
+    res = {}
+    try:
+        for bias in (1, 0):
+            rmx.set_tuning("wgrad_bias", bias)
+            for v in (0, 1):
+                rmx.set_tuning("wgrad_sq16", v)
+                res[bias, v] = grads()
+    finally:
+        rmx.set_tuning("wgrad_sq16", None)
+        rmx.set_tuning("wgrad_bias", None)
+    for bias in (1, 0):
+        for a, b in zip(res[bias, 0], res[bias, 1]):
+            assert np.array_equal(a, b), bias
+    assert np.isfinite(res[1, 1][3]).all() and np.abs(res[1, 1][3]).max() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", GPU_KINDS)
 def test_backward_host_arrays_in_place(kind):
     """L-A RecModel.backward: the caller's arrays come back holding the gradients."""
