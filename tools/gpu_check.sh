@@ -72,6 +72,13 @@ for s in $STEPS; do
              run line_$wl 400 python bench.py --workload $wl --steps 100 --warmup 10 || exit $?
              grep '^{' "$OUT/line_$wl.log" | tail -n 1 > "$OUT/line_$wl.json"
            done ;;
+    lines5) for wl in xdeepfm_cin1 encoder deepfm_sharded dcn_bf16 pnn_bf16 lr_plumbing deepfm_train xdeepfm_train; do
+             run line_$wl 400 python bench.py --workload $wl --steps 100 --warmup 10 --no-companion || exit $?
+             grep '^{' "$OUT/line_$wl.log" | tail -n 1 > "$OUT/line_$wl.json"
+           done ;;
+    grid5) for B in 1024 4096 8192 16384 32768 49152 65536 98304 131072; do
+             run grid_b$B 300 python bench.py --batch $B --no-companion --no-encoder-record --parity-only --steps 200 --warmup 10 || exit $?
+           done ;;
     blas) run probe_blas 300 python tools/probe_blas.py ;;
     profx20) run profx20 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profx20" -o xdeepfm -- \
             python3 bench.py --workload xdeepfm --gpus 1 --steps 20 --warmup 5 ;;
