@@ -423,7 +423,10 @@ bool tower_fused_s3_usable(const DenseLayer& L1, const DenseLayer& L2, const Den
         L3.bias_mode == 1))
     return false;
   if (!L1.b || !L2.b) return false;
-  // knob "s3_fused": 0 off (head + tail), 2 always, 1 (default) when the (half) row blocks fill every CU once
+  // knob "s3_fused": 0 off (head + tail), 2 always, 1 (default) when at least one round of full 128-row blocks
+  // fills every CU (B >= 32,768 on 256 CUs): at B = 16,384 (one round of 64-row half blocks) head + tail ran
+  // 154.4 M against the fused tower's 147.7 M; at 32,768 / 49,152 the fused tower wins, 201.1 / 189.0 M against
+  // 190.3 / 184.0 M (profiles/r05/ab_fused_batch.txt)
   const int knob = tuning_get("s3_fused", 1);
   if (knob == 0) return false;
   if (knob == 2) return true;
@@ -431,7 +434,9 @@ bool tower_fused_s3_usable(const DenseLayer& L1, const DenseLayer& L2, const Den
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     ncu = 256;
-  return q_fills(M, ncu) || (tuning_get("half_blocks", 1) != 0 && M > 16 * ncu);
+  int grid = 0;
+  const QRows r = q_rows(M, ncu, grid);
+  return grid >= ncu && r.nfull >= ncu;
 }
 
 int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer& L2, const DenseLayer& L3, int M, int F,

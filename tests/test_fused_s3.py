@@ -144,6 +144,22 @@ def test_fused_tower_is_the_default_at_the_bench_batch(ctx):
     assert list(stages) == ["tower_fused"], stages
 
 
+@pytest.mark.parametrize("B,want", [(16384, ["tower_layer1", "tower_tail"]), (32768, ["tower_fused"]),
+                                    (49152, ["tower_fused"])])
+def test_fused_tower_default_batch_rule(ctx, B, want):
+    """knob s3_fused 1 (default) takes the fused tower once a round of full 128-row blocks fills the CUs
+    (B >= 32,768 on 256 CUs); below, head + tail with their half blocks (measured faster at B = 16,384)."""
+    V = 50000
+    m, mats, table, ids, out = _setup(ctx, B, V)
+    for k in ("s3_fused", "s3_head", "s3_tail", "s3_small"):
+        rmx.set_tuning(k, None)
+    m.set_timing(True)
+    m.forward_ids(table, B, ids, out)
+    ctx.sync()
+    stages, _ = m.get_timing()
+    assert list(stages) == want, stages
+
+
 @pytest.mark.parametrize("B", [40000, 65536])
 @pytest.mark.parametrize("knob", ["fused_prio"])
 def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
