@@ -18,6 +18,10 @@
 // swapped as in k_rowown.hpp), the FM / first order in encoder_k16_kernel<1>'s order (bit-identical).
 #include "k_gemm.hpp"
 
+#ifndef RMX_SMALL_DIAG
+#define RMX_SMALL_DIAG 0
+#endif
+
 namespace rmx {
 namespace {
 
@@ -394,16 +398,16 @@ int launch_tower_small_s3(hipStream_t s, const rmx_model& m, int M, int F, const
   }
   p.KS1 = (F + 1) / 2;
   p.oa = oa;
-  const int dg = tuning_get("s3_small_diag", 0);  // (timing probes, wrong results: 1 no MFMA, 2 no weight loads, 4 no gather)
-  // knob "s3_small_il": 1 (default) the next step's weight loads ride the MFMA groups, 0 issued at the step head
-  const bool il = tuning_get("s3_small_il", 1) != 0;
-  const void* fn = il ? (const void*)tower_small_s3_kernel<1, 0, true> : (const void*)tower_small_s3_kernel<1, 0, false>;
-  if (rt == 2)
-    fn = il ? (const void*)tower_small_s3_kernel<2, 0, true> : (const void*)tower_small_s3_kernel<2, 0, false>;
-#define RMX_DG(V) else if (rt == 1 && dg == V) fn = (const void*)tower_small_s3_kernel<1, V, true>;
-  if (dg == 0) {}
+  // (IL = false: the next step's loads at the step head, measured 0.0704 vs 0.069 ms at B = 8,192 --
+  // profiles/r05/ab_small_il_wgrad16.txt; DG: timing probes, built only with RMX_SMALL_DIAG, results wrong)
+  const void* fn = rt == 2 ? (const void*)tower_small_s3_kernel<2, 0, true> : (const void*)tower_small_s3_kernel<1, 0, true>;
+#if RMX_SMALL_DIAG
+  const int dg = tuning_get("s3_small_diag", 0);  // 1 no MFMA, 2 no weight loads, 4 no gather (tools/probe_small.py)
+#define RMX_DG(V) \
+  if (rt == 1 && dg == V) fn = (const void*)tower_small_s3_kernel<1, V, true>;
   RMX_DG(1) RMX_DG(2) RMX_DG(3) RMX_DG(4) RMX_DG(7)
 #undef RMX_DG
+#endif
   const size_t lds = rt == 2 ? small_lds<2>() : small_lds<1>();
   RMX_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* args[] = {&p};

@@ -21,6 +21,9 @@
 //             dz[index[n]] (Scatter backward).
 #include <algorithm>
 #include <type_traits>
+#ifndef RMX_WGRAD_SQ_DIAG
+#define RMX_WGRAD_SQ_DIAG 0  // 1: the wgrad_sq timing probes (knob wgrad_diag) are built
+#endif
 #include <vector>
 
 #include "rmx_models.hpp"
@@ -1382,7 +1385,11 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     RMX_HIP(hipFuncSetAttribute(zg ? (const void*)wgrad_sq_kernel<true> : (const void*)wgrad_sq_kernel<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     float* cpart = fuse_bias ? T.part2 + (int64_t)S * N * K : nullptr;
-    const int dg = zg ? 0 : tuning_get("wgrad_diag", 0);
+#if RMX_WGRAD_SQ_DIAG
+    const int dg = zg ? 0 : tuning_get("wgrad_diag", 0);  // timing probes (results wrong): DESIGN.md §10
+#else
+    const int dg = 0;
+#endif
     // knob "wgrad_sq16": 16 waves balanced over the SIMDs (read operands only)
     const bool w16 = !zg && dg == 0 && tuning_get("wgrad_sq16", 1) != 0;
     if (w16) {
@@ -1393,6 +1400,7 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     } else if (zg)
       hipLaunchKernelGGL(wgrad_sq_kernel<true>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, cpart, z);
+#if RMX_WGRAD_SQ_DIAG
 #define RMX_WG_DG(V)                                                                                              \
     else if (dg == V) {                                                                                           \
       RMX_HIP(hipFuncSetAttribute((const void*)wgrad_sq_kernel<false, V>, hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -1402,6 +1410,7 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     }
     RMX_WG_DG(1) RMX_WG_DG(2) RMX_WG_DG(3) RMX_WG_DG(4) RMX_WG_DG(6)
 #undef RMX_WG_DG
+#endif
     else
       hipLaunchKernelGGL(wgrad_sq_kernel<false>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, cpart, z);
