@@ -1,6 +1,6 @@
 """Timing probes of the small-batch whole-tower kernel (k_small_s3.hip, knob s3_small_diag: 1 no MFMAs, 2 no
 weight loads, 4 no row gather; the results of a probe are wrong by construction).  The probe kernels exist only
-in a build with -DRMX_SMALL_DIAG=1 (make CXXFLAGS+=-DRMX_SMALL_DIAG=1 in csrc/); otherwise every line is the
+in a build with -DRMX_SMALL_DIAG=1 (make EXTRA=-DRMX_SMALL_DIAG=1 in csrc/, after a make clean); otherwise every line is the
 default kernel.  Prints the stage time per batch and probe.  Usage: python tools/probe_small.py [B ...]"""
 import os
 import sys
