@@ -176,3 +176,31 @@ def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
     finally:
         rmx.set_tuning(knob, None)
     assert np.array_equal(res[vals[0]], res[vals[1]])
+
+
+@pytest.mark.parametrize("Fn", [1, 2, 7, 40])
+def test_fused_tower_field_counts(ctx, Fn):
+    """Field counts other than the bench's 39 (F = 1 / 2: one K step; 7: odd, a half-empty last step; 40: the
+    maximum, 20 full steps): the fused tower gives head + tail's bits and meets the fp64 oracle."""
+    B, V = 40000, 50000
+    m = rmx.DeepFM(V, Fn, K, list(FC))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * Fn, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, Fn, V, ids)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    got = _fwd(ctx, m, table, B, ids, out, True)
+    ref = _fwd(ctx, m, table, B, ids, out, False)
+    assert np.isfinite(got).all()
+    assert np.array_equal(got, ref)
+    rows = np.union1d(np.arange(0, B, 997), [B - 1])
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    om = oc.make_model(oc.DEEPFM, Fn, K, fc=FC)
+    h = oc.gen_ids(SEED_IDS, 0, B, Fn, V).reshape(B, Fn)[rows].astype(np.int64).ravel()
+    w, e = oc.gather(wt, et, 1, h)
+    n = rows.size
+    r64 = oc.forward(om, n, np.repeat(np.arange(n, dtype=np.int64), Fn), np.array([0.01], np.float32), w, e, mats, 1)
+    assert float(np.abs(got[rows] - r64).max()) <= TOL

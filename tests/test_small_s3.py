@@ -138,3 +138,39 @@ def test_small_tower_ignores_lds_leftovers(ctx, rt, pattern):
     assert np.isfinite(res[1]).all()
     assert np.array_equal(res[0], res[1])
 
+
+
+@pytest.mark.parametrize("rt", [1, 2])
+@pytest.mark.parametrize("Fn", [1, 2, 7, 40])
+def test_small_tower_field_counts(ctx, Fn, rt):
+    """Field counts other than 39 through the whole-tower kernel (F = 1 / 2: one K step of layer 1; 7: odd;
+    40: the maximum): within 5e-6 of the engine path and 1e-5 of the fp64 oracle."""
+    V, B = 50000, 1000
+    m = rmx.DeepFM(V, Fn, K, list(FC))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * Fn, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, Fn, V, ids)
+    out = rmx.DeviceArray(ctx, B, np.float32)
+    rmx.set_tuning("s3_small_rt", rt)
+    res = {}
+    for knob in (0, 2):
+        rmx.set_tuning("s3_small", knob)
+        m.set_timing(True)
+        m.forward_ids(table, B, ids, out)
+        ctx.sync()
+        stages, _ = m.get_timing()
+        m.set_timing(False)
+        assert ("tower_small" in stages) == (knob == 2), stages
+        res[knob] = out.numpy().copy()
+    assert float(np.abs(res[2] - res[0]).max()) <= SMALL_VS_ENGINE
+    om = oc.make_model(oc.DEEPFM, Fn, K, fc=FC)
+    wt, et = oc.gen_table(SEED_TAB, V, K)
+    n = 256
+    h = oc.gen_ids(SEED_IDS, 0, n, Fn, V).astype(np.int64)
+    w, e = oc.gather(wt, et, 1, h)
+    ref = oc.forward(om, n, np.repeat(np.arange(n, dtype=np.int64), Fn), np.array([0.01], np.float32), w, e, mats, 1)
+    assert float(np.abs(res[2][:n] - ref).max()) <= TOL
