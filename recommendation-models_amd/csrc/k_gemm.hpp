@@ -1464,7 +1464,9 @@ int launch_epi(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
 // the tower_variant launch_tower_nt uses at M >= 65536 (knob, else the default below)
 inline int tower_variant_for(int NT, Epi epi, bool bf16, int K) {
   const bool even = NT % 2 == 0 && NT >= 8;
-  const int def = NT == 26 ? ((epi == Epi::kOutput && !bf16) ? 5 : (bf16 && K >= 1024 ? 3 : 4)) : (even ? 3 : 0);
+  // (bf16 K >= 1024, PNN layer 1: variant 6, 0.089-0.091 vs 0.093-0.094 ms for variant 3 at B = 65,536,
+  // profiles/r05/ab_bf16_variant.txt)
+  const int def = NT == 26 ? ((epi == Epi::kOutput && !bf16) ? 5 : (bf16 && K >= 1024 ? 6 : 4)) : (even ? 3 : 0);
   return tuning_get("tower_variant", def);
 }
 
@@ -1491,8 +1493,8 @@ int launch_tower_nt(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // LDS-DMA ring fit 2 blocks per CU (one block's epilogue overlaps the other's MFMAs): fp32
   // 0.280 / 0.183 ms for layers 1 / 2 vs 0.288 / 0.189 (variant 3), bf16 DCN 457 vs 431 M ex/s; the
   // fp32 output layer prefers 32 rows per wave (variant 5: 0.171 vs 0.177 ms)
-  // bf16 layers with a long K (PNN layer 1: K = 624 + 741) prefer the 16-wave 3-deep ring
-  // (0.098 vs 0.119 ms at B = 65,536)
+  // bf16 layers with a long K (PNN layer 1: K = 624 + 741) prefer the 3-deep rings: the 16-wave one
+  // (variant 3: 0.098 vs 0.119 ms at B = 65,536) and, since round 5, the fast ring tile (variant 6)
   int var = tower_variant_for(NT, epi, PREC == kPrecBF16, p.K);
   if (p.M >= 65536) {
     if constexpr (kEven) {

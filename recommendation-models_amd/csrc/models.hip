@@ -763,7 +763,9 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // PNN bf16: its first order (a kernel of its own otherwise: nothing else gathers the weights) summed by
   // the tower tail's head (knob "tail_fo", default on)
   const size_t nl = m.layers.size();
-  const bool tail_fo = m.type == RMX_MODEL_PNN && m.precision == kBF16 && in.dtype == kBF16 && in.ids && !in.y1 &&
+  // DCN bf16 too when layer 1 does not sum it from its weight ring (tower_wring: the 2-deep ring variants)
+  const bool tail_fo = (m.type == RMX_MODEL_PNN || (m.type == RMX_MODEL_DCN && !fm_fused)) && m.precision == kBF16 &&
+                       in.dtype == kBF16 && in.ids && !in.y1 &&
                        F <= 40 && nl >= 3 && tuning_get("tail_fo", 1) != 0 &&
                        tower_tail_usable(m.layers[nl - 2], m.layers[nl - 1], B, m.layers[nl - 3].Npad);
   // DeepFM fp32 at a batch that fills the GPU: layer 1 + first order + FM as one row-owner kernel

@@ -161,10 +161,10 @@ def test_bf16_bench_batch_matches_bf16_oracle(kind):
 @pytest.mark.parametrize("kind", ["dcn", "pnn", "dnn32"])
 def test_bf16_fast_ring_variant_bitwise(kind):
     """tower_variant 6 (the branch-free 3-deep ring tile with two 208-column slices, k_gemm.hpp
-    launch_tower_nt) accumulates each output in the same K-step order as the default 2-deep ring:
-    bitwise-equal predictions at B = 65,536.  dnn32 has a 400-wide layer with K = 32, one K step:
-    fewer steps than the ring's two stages of lead, which the prologue must still fill (the loop's
-    counted wait assumes them)."""
+    launch_tower_nt; PNN layer 1's default) accumulates each output in the same K-step order as the
+    2-deep ring (variant 4, DCN's default) and the 16-wave 3-deep ring (variant 3): bitwise-equal
+    predictions at B = 65,536.  dnn32 has a 400-wide layer with K = 32, one K step: fewer steps than the
+    ring's two stages of lead, which the prologue must still fill (the loop's counted wait assumes them)."""
     import rmx
     ctx = rmx.default_context()
     V, B = 50_003, 65536
@@ -181,7 +181,7 @@ def test_bf16_fast_ring_variant_bitwise(kind):
     got = {}
     try:
         rmx.set_tuning("bf16_tail", 0)  # the engine's layers 2 / 3 (the tail kernel has its own test)
-        for var in (None, 6):
+        for var in (None, 3, 4, 6):
             rmx.set_tuning("tower_variant", var)
             m.forward_ids(t, B, ids_d, out)
             ctx.sync()
@@ -189,7 +189,8 @@ def test_bf16_fast_ring_variant_bitwise(kind):
     finally:
         rmx.set_tuning("tower_variant", None)
         rmx.set_tuning("bf16_tail", None)
-    assert np.array_equal(got[6], got[None])
+    for var in (None, 3, 4):
+        assert np.array_equal(got[6], got[var]), var
     wt, et = _rounded_table(V)
     n = 256
     ids = oc.gen_ids(SEED_IDS, B - n, n, F, V).astype(np.int64)
@@ -249,14 +250,15 @@ def test_bf16_tower_tail_matches_unfused(kind, B):
         assert np.abs(got[1][r0:r0 + n] - ref).max() <= TOL_BF16
 
 
-@pytest.mark.parametrize("B", [1000, 65536])
-def test_bf16_tail_first_order_bitwise(B):
-    """PNN bf16: the tower tail's head sums the first order itself (tail_fo, default on: field order from
-    0, encoder_k16_kernel<0>'s arithmetic) -- bitwise the predictions of the first-order kernel path."""
+@pytest.mark.parametrize("kind,B", [("pnn", 1000), ("pnn", 65536), ("dcn", 1000), ("dcn", 65536)])
+def test_bf16_tail_first_order_bitwise(kind, B):
+    """PNN bf16, and DCN bf16 when layer 1 does not sum the first order from its weight ring (tower variant 3
+    here): the tower tail's head sums the first order itself (tail_fo, default on: field order from 0,
+    encoder_k16_kernel<0>'s arithmetic) -- bitwise the predictions of the first-order kernel path."""
     import rmx
     ctx = rmx.default_context()
     V = 50_003
-    m, _ = _model("pnn", V)
+    m, _ = _model(kind, V)
     t = rmx.EmbeddingTable(ctx, V, K, rmx.DTYPE_BF16)
     t.fill_synthetic(SEED_TAB)
     m.setPrecision(rmx.DTYPE_BF16)
@@ -267,6 +269,8 @@ def test_bf16_tail_first_order_bitwise(B):
     out = rmx.DeviceArray(ctx, B, np.float32)
     got = {}
     try:
+        if kind == "dcn":
+            rmx.set_tuning("tower_variant", 3)
         for fo in (0, 1):
             rmx.set_tuning("tail_fo", fo)
             m.set_timing(True)
@@ -278,4 +282,5 @@ def test_bf16_tail_first_order_bitwise(B):
             assert ("first_order" in stages) == (fo == 0), stages
     finally:
         rmx.set_tuning("tail_fo", None)
+        rmx.set_tuning("tower_variant", None)
     assert np.array_equal(got[0], got[1])
