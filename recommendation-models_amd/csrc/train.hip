@@ -1267,11 +1267,24 @@ __global__ __launch_bounds__(W16 ? kSq16Thr : kSqThr, 1) void wgrad_sq_kernel(in
 
 // out[i] (=, or += when accum) sum_s part[s][i]: a block covers 64 outputs with 4 wave-groups, group
 // q summing slices q, q + 4, ...; the 4 group sums are added in fixed order (deterministic).
+// Blocks past ceil(n / 64) reduce a second array the same way (n2 outputs of part2 into out2, "=" only):
+// the dW's fused bias partials ride its launch instead of a launch of their own.
 __global__ __launch_bounds__(256) void slice_reduce_kernel(int S, int64_t n, const float* __restrict__ part,
-                                                           float* __restrict__ out, int accum) {
+                                                           float* __restrict__ out, int accum, int64_t n2 = 0,
+                                                           const float* __restrict__ part2 = nullptr,
+                                                           float* __restrict__ out2 = nullptr) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + c;
+  const int64_t nb1 = (n + 63) / 64;
+  int64_t blk = blockIdx.x;
+  if (blk >= nb1) {  // block-uniform
+    blk -= nb1;
+    n = n2;
+    part = part2;
+    out = out2;
+    accum = 0;
+  }
+  const int64_t i = blk * 64 + c;
   float v = 0.f;
   if (i < n)
     for (int sl = q; sl < S; sl += 4) v += part[(int64_t)sl * n + i];
@@ -1364,10 +1377,17 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
     RMX_HIP(hipGetDevice(&dev));
     RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     ncu = std::max(ncu, 1);
-    int64_t best = -1;
+    // knob "wgrad_smodel": 1 (default) also prices the S partial planes the kernel writes and slice_reduce reads
+    // back (~8 B per output per slice at ~4 TB/s, against ~3.8 us per round of 32-row chunks): DeepFM training's
+    // layer-1 dW (624 x 400) took S = 128 (3 rounds x 16 chunks) and paid 33 us of slice reduction for it;
+    // 0: rounds x chunks alone
+    const bool smodel = tuning_get("wgrad_smodel", 1) != 0;
+    double best = -1.0;
     for (int s8 = 8; s8 <= 512; s8 += 8) {
       const int64_t chunks = round_up((rows + s8 - 1) / s8, kWgR) / kWgR;
-      const int64_t cost = ((int64_t)tiles * s8 + ncu - 1) / ncu * chunks;
+      const int64_t rounds = ((int64_t)tiles * s8 + ncu - 1) / ncu;
+      const double cost = smodel ? 3.8 * (double)(rounds * chunks) + (double)s8 * N * K * 8.0 / 4.0e6
+                                 : (double)(rounds * chunks);
       if (best < 0 || cost < best) {
         best = cost;
         S = s8;
@@ -1415,15 +1435,12 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
       hipLaunchKernelGGL(wgrad_sq_kernel<false>, dim3(tiles * S), dim3(kSqThr), lds, s, rows, N, K, A, lda, X, ldx, rps,
                          tiles, T.part2, cpart, z);
     RMX_HIP(hipGetLastError());
-    hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)N * K + 63) / 64)), dim3(256), 0, s, S,
-                       (int64_t)N * K, T.part2, out, accum ? 1 : 0);
+    // the bias partials (fuse_bias) in the same launch: its blocks past the dW's
+    const int64_t nb1 = ((int64_t)N * K + 63) / 64, nb2 = fuse_bias ? (N + 63) / 64 : 0;
+    hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(nb1 + nb2)), dim3(256), 0, s, S, (int64_t)N * K, T.part2,
+                       out, accum ? 1 : 0, fuse_bias ? (int64_t)N : 0, cpart, bias);
     RMX_HIP(hipGetLastError());
-    if (fuse_bias) {
-      hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, s, S, (int64_t)N, cpart,
-                         bias, 0);
-      RMX_HIP(hipGetLastError());
-      *bias_done = true;
-    }
+    if (fuse_bias) *bias_done = true;
     return RMX_OK;
   }
   // knob "wgrad_sb": 1 (default) the single-buffered kernel on the 128 x 128 tiles (two blocks per CU),
