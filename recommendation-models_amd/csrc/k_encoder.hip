@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void encoder_k16_kernel(int M, const int32_t* 
 // them; V = 100M row table: 0.106 ms, 0.78 of the 128-B line rate of HBM).  Here the 4 lanes of a sample
 // load the sample's ids of a 40-field chunk once, coalesced (lane c: fields 4i + c), share them with a quad
 // DPP broadcast, and request the rows (+ first-order weights) in batches of U: 1 + ceil(F / U) round trips.
-// Forward modes only (0, 1, 2: ids given, no x / FM-sum outputs); the kernel above keeps the rest.
+// Modes 0, 1, 2 with ids given; XO: also the training forward's outputs (x, and the FM sums in mode 1) from the
+// same loads, as encoder_k16_kernel writes them (mode 3 and the implicit-id L-A path keep the kernel above).
 __device__ __attribute__((aligned(16))) float g_enc_zero16[16];  // the zero row of fields past F
 
 template <int J>
@@ -127,21 +128,25 @@ __device__ __forceinline__ int quad_bcast(int v, int j) {  // (j is a constant a
   }
 }
 
-template <int MODE, class T, int U>
+template <int MODE, class T, int U, bool XO = false>
 __global__ __launch_bounds__(256) void encoder_k16v2_kernel(int M, const int32_t* __restrict__ ids,
                                                             const T* __restrict__ table,
                                                             const T* __restrict__ wtab, int F,
                                                             float* __restrict__ y, float beta,
-                                                            float* __restrict__ prob, int ld, int wld) {
+                                                            float* __restrict__ prob, int ld, int wld,
+                                                            float* __restrict__ xo = nullptr,
+                                                            float* __restrict__ so = nullptr) {
 #pragma clang fp contract(off)
   constexpr int NI = 10, CH = 4 * NI;  // ids per lane / fields per chunk
   constexpr int NB = (CH + U - 1) / U;
   constexpr bool FM = MODE == 1;
+  constexpr bool ROWS = FM || (XO && MODE == 0);
   const int lane = threadIdx.x & 63;
   const int s = lane >> 2, c = lane & 3;
   const int b = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + s;
   const bool valid = b < M;
   const int32_t* irow = ids + (int64_t)(valid ? b : 0) * F;
+  float4* xr = XO && xo && valid ? reinterpret_cast<float4*>(xo + (int64_t)b * F * 16) + c : nullptr;  // (xo nullable)
   float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = s4;
   float y1 = 0.f;
   // branch-free inside a batch (a per-lane or per-field branch around a load made the compiler wait for each
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(256) void encoder_k16v2_kernel(int M, const int32_t
         const bool live = f0 + uu < F;
         const T* rsrc = live ? table + (int64_t)id * ld + c * 4 : reinterpret_cast<const T*>(zero16);
         const T* wsrc = live ? wtab + (int64_t)id * wld : reinterpret_cast<const T*>(zero16);
-        if (FM) v[u] = load4(rsrc);
+        if (ROWS) v[u] = load4(rsrc);
         wv[u] = ld1(wsrc);
       }
 #pragma unroll
@@ -182,8 +187,17 @@ __global__ __launch_bounds__(256) void encoder_k16v2_kernel(int M, const int32_t
         }
         y1 += wv[u];
       }
+      if constexpr (XO) {  // after the batch's sums: the stores wait for nothing the sums did not
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int uu = h * U + u;
+          if (uu >= CH) break;
+          if (xr && f0 + uu < F) xr[(f0 + uu) * 4] = v[u];
+        }
+      }
     }
   }
+  if (XO && FM && so && valid) reinterpret_cast<float4*>(so + (int64_t)b * 16)[c] = s4;
   float y2 = 0.f;
   if (FM) {  // encoder_k16_kernel's reduction, the same order
     float d0 = s4.x * s4.x - q4.x, d1 = s4.y * s4.y - q4.y;
@@ -247,8 +261,20 @@ static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids,
                              int k, float* y, float bt, float* prob, int ld, int wld, float* xo, float* so) {
   // knob "enc_u" (round 5): rows per batch of the v2 kernel, 0 = the kernel above
   const int eu = tuning_get("enc_u", 20);
-  if ((k == 16 || mode == 2) && ids && !xo && !so && mode != 3 && (eu == 13 || eu == 20)) {
+  // (x / FM sums for the training forward: knob "enc_v2_x", default 1)
+  const bool xs = xo || so;
+  if ((k == 16 || mode == 2) && ids && mode != 3 && (eu == 13 || eu == 20) &&
+      (!xs || (mode != 2 && eu == 20 && tuning_get("enc_v2_x", 1) != 0))) {
     dim3 grid((M + 63) / 64);
+    if (xs) {
+      if (mode == 0)
+        hipLaunchKernelGGL((encoder_k16v2_kernel<0, T, 20, true>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt,
+                           prob, ld, wld, xo, so);
+      else
+        hipLaunchKernelGGL((encoder_k16v2_kernel<1, T, 20, true>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt,
+                           prob, ld, wld, xo, so);
+      return;
+    }
 #define RMX_ENC2(MD, UU) hipLaunchKernelGGL((encoder_k16v2_kernel<MD, T, UU>), grid, dim3(256), 0, s, M, ids, table, wtab, F, y, bt, prob, ld, wld)
     if (eu == 13) {
       if (mode == 0) RMX_ENC2(0, 13); else if (mode == 1) RMX_ENC2(1, 13); else RMX_ENC2(2, 13);

@@ -336,6 +336,43 @@ def test_backward_fused_x_bitwise(kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,fx,B", [("deepfm", 1, 777), ("deepfm", 1, 65536), ("xdeepfm", 2, 777), ("dcn", 2, 4099)])
+def test_backward_encoder_v2_x_bitwise(kind, fx, B):
+    """enc_v2_x: the training forward's encoder (x, the FM sums, y1 + y2 / y1) on the batched-request kernel
+    (encoder_k16v2_kernel with XO) against the round-4 kernel (0): every gradient and the loss bit for bit --
+    x and the FM sums are copies / sums in the same field order either way.  B = 777 / 4,099: a ragged last
+    wave; 65,536: the bench batch."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K = 20_000, 39, 16
+    m = _gpu_model(rmx, kind, V, F, K, (32, 16))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 5, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(3).random(B) > 0.7).astype(np.float32))
+    res = {}
+    try:
+        rmx.set_tuning("train_fuse_x", fx)
+        for v in (0, 1):
+            rmx.set_tuning("enc_v2_x", v)
+            out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, len(mats), 1)]
+            m.backward_ids(t, B, ids, targets, *out)
+            ctx.sync()
+            res[v] = [o.numpy().copy() for o in out]
+    finally:
+        rmx.set_tuning("train_fuse_x", None)
+        rmx.set_tuning("enc_v2_x", None)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+    assert np.abs(res[1][2]).max() > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("fc,B", [((32, 16), 777), ((400, 400, 400), 4099)])
 def test_backward_fused_head_and_emb_grad(fc, B):
     """train_emb_fused: DeepFM's layer-1 dX epilogue writes the embedding gradient itself (dX + the FM
