@@ -52,7 +52,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense
 PEAK_S3_TFLOPS = PEAK_BF16_TFLOPS / 6
 # stages whose GEMMs run on the split (f32_split on): priced against its peak.  The backward stages
 # (dW and dX on the split; the CIN backward's rocBLAS part is fp32) take the higher peak too.
-S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "tower_fused", "cin", "tower_back")
+S3_STAGES = ("tower_layer", "tower_tail", "tower_small", "tower_fused", "cin", "tower_back", "head_x")
 
 
 def parse():
@@ -134,7 +134,7 @@ def stage_work(workload, stage, B, direct=False):
         return "flop", sum(4.0 * B * K * F * hp * h for hp, h in zip(hps, cin))
     if stage == "gather_x":
         return "byte", B * (F * 4 + F * K * es + D * 4)
-    if stage == "tower_layer1":
+    if stage in ("tower_layer1", "head_x"):  # head_x: training's encoder + layer 1 (k_head_s3.hip XS), the GEMM
         return "flop", 2.0 * B * k1 * FC[0]
     if stage == "tower_layer2":
         return "flop", 2.0 * B * FC[0] * FC[1]

@@ -49,7 +49,14 @@ struct HeadS3Args {
   float* H;               // [M][416] out: ReLU(x W^T + b), columns 400 .. 415 zero
   float* fm_y;            // [M] y1 + y2 (fm_sums) or y1
   int fm_sums;
+  float* X;               // XS (training forward): [M][ldx] the gathered rows x, as the encoder stores them
+  int ldx;
+  float* S;               // XS: [M][16] the FM sums s_j (field order), or null
 };
+
+// XS: the x stores of rows past M / fields past F go here instead (every store is issued: the units'
+// vector-memory counts stay static)
+__device__ __attribute__((aligned(16))) float g_head_sink[64 * 4];
 
 // K step c, half h of unit u (wave-uniform)
 __device__ __forceinline__ const bf16_t* h_unit_src(const HeadS3Args& p, int u) {
@@ -89,6 +96,10 @@ __device__ __forceinline__ void h_row_dma(const HeadS3Args& p, char* wl, int s, 
     lds_dma<4>(sw, wl + kHA + kHId + (s & 1) * 128);
 }
 
+// XS (training forward, k_head_s3 as DeepFM's layer 1 + encoder): also x and the FM sums, from the rows the
+// head loads anyway -- two 16-B stores per half-0 unit (x of fields 2c, 2c + 1: a lane holds sample r16's
+// j = 4g .. 4g + 3 of each) and one per row in the epilogue
+template <bool XS>
 __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args p) {
   extern __shared__ __attribute__((aligned(16))) char hsmem[];
   char* lds = hsmem;
@@ -159,6 +170,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
     for (int c = 0; c < KS; ++c, ++s) {
       q_enter<5>();  // previous unit: (c - 1, half 1) or the previous row block's last, 5 DMAs
       bf16x8 ah, am, al;
+      f32x4 xa0, xa1;  // (XS)
       {
         // rows of step s: a0 = field 2c, a1 = field 2c + 1 (zero past F), j = 4 g .. 4 g + 3
         int o = r16 * 64 + swz_slot(r16, g) * 16;
@@ -174,18 +186,30 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
           y1 += wr[16 + r16];
         }
         split3(a0, a1, ah, am, al);
+        xa0 = a0;
+        xa1 = a1;
       }
       // ids three steps ahead (their slot held step s - 1's, read at step s - 2); rows + weights of the
       // next step into the A / weight slots step s - 1 used (its ids landed: issued at step s - 2)
       id_dma(s + 3);
       h_row_dma(p, wl, s + 1, lane);
-      __builtin_amdgcn_sched_barrier(0);  // these 4 DMAs ahead of the unit's 5 (the static vmcnt counts)
+      if constexpr (XS) {
+        const int mx = row0 + w * 16 + r16, f0 = 2 * c;
+        const bool okm = mx < p.M;
+        float* sink = g_head_sink + lane * 4;
+        float* xrow = p.X + (int64_t)mx * p.ldx + 4 * g;
+        float* d0 = okm && f0 < p.F ? xrow + 16 * f0 : sink;
+        float* d1 = okm && f0 + 1 < p.F ? xrow + 16 * (f0 + 1) : sink;
+        *reinterpret_cast<f32x4*>(d0) = xa0;
+        *reinterpret_cast<f32x4*>(d1) = xa1;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // these 4 (XS: 6) ahead of the unit's 5 (the static vmcnt counts)
       const int u = 2 * c;
       int dslot = slot == 0 ? 2 : slot - 1;
       q_unit<kQUT, 0>(lds + slot * kQUnit, fb, ah, am, al, acc, h_unit_src(p, u + 2 < NU ? u + 2 : u + 2 - NU), lds,
                       dslot, w, lo);
       slot = q_next(slot);
-      q_enter<9>();  // previous unit: 1 id + 2 row + 1 weight + 5 plane DMAs
+      q_enter<XS ? 11 : 9>();  // previous unit: 1 id + 2 row + 1 weight (+ 2 x stores) + 5 plane DMAs
       dslot = slot == 0 ? 2 : slot - 1;
       q_unit<kQNT - kQUT, kQUT>(lds + slot * kQUnit, fb, ah, am, al, acc,
                                 h_unit_src(p, u + 3 < NU ? u + 3 : u + 3 - NU), lds, dslot, w, lo);
@@ -217,6 +241,8 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
         for (int t = 0; t < 4; ++t) a += __shfl(d[t], gg * 16 + r16);
       if (g == 0 && m < p.M && p.fm_y) p.fm_y[m] = p.fm_sums ? y1 + 0.5f * (a / 16.0f) : y1;
     }
+    if constexpr (XS)
+      if (p.S && m < p.M) *reinterpret_cast<f32x4*>(p.S + (int64_t)m * 16 + g4) = fs;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing DMAs land before the LDS is released
 }
@@ -242,7 +268,8 @@ bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids) {
 }
 
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
-                         int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums) {
+                         int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums, float* X,
+                         int ldx, float* S) {
   if (!tower_head_s3_usable(L1, M, F, 16, ids != nullptr) && tuning_get("s3_head", 1) != 2) {
     set_error("fp32 tower head: needs a k = 16 gather (F <= 40, ids) into a 400-wide split-GEMM layer");
     return RMX_E_INVALID;
@@ -256,8 +283,12 @@ int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, cons
   int dev = 0, ncu = 0;
   RMX_HIP(hipGetDevice(&dev));
   RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  RMX_HIP(hipFuncSetAttribute((const void*)tower_head_s3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kHLds));
+  if (X && ldx < 16 * F) {
+    set_error("fp32 tower head: x needs ldx >= 16 F");
+    return RMX_E_INVALID;
+  }
+  const void* fn = X ? (const void*)tower_head_s3_kernel<true> : (const void*)tower_head_s3_kernel<false>;
+  RMX_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHLds));
   HeadS3Args p{};
   p.M = M;
   int grid = 0;
@@ -274,7 +305,13 @@ int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, cons
   p.H = H;
   p.fm_y = fm_y;
   p.fm_sums = fm_sums;
-  hipLaunchKernelGGL(tower_head_s3_kernel, dim3(grid), dim3(kQThreads), kHLds, s, p);
+  p.X = X;
+  p.ldx = ldx;
+  p.S = S;
+  if (X)
+    hipLaunchKernelGGL(tower_head_s3_kernel<true>, dim3(grid), dim3(kQThreads), kHLds, s, p);
+  else
+    hipLaunchKernelGGL(tower_head_s3_kernel<false>, dim3(grid), dim3(kQThreads), kHLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;
 }

@@ -138,8 +138,10 @@ int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer
 // fp32 tower layer 1 of DeepFM as a row-owner kernel (k_head_s3.hip): gather (k = 16, ids [M][F], table row
 // of id at table + id * ld) + ReLU(x W1^T + b1) -> H [M][416] + first order (+ FM: fm_sums) -> fm_y [M]
 bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids);
+// X / S (nullable; X non-null selects the training variant): also x [M][ldx] and the FM sums [M][16]
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
-                         int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums);
+                         int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums,
+                         float* X = nullptr, int ldx = 0, float* S = nullptr);
 // DeepFM's whole fp32 tower in one persistent row-owner kernel (k_fused_s3.hip): gather (k = 16, ids [M][F])
 // + first order + FM + three 400-wide split-GEMM layers + the head, h1 and h2 in registers -> oa.out [M]
 bool tower_fused_s3_usable(const DenseLayer& L1, const DenseLayer& L2, const DenseLayer& L3, int M, int F, int k,

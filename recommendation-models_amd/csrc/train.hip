@@ -1697,7 +1697,19 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
                         (t == RMX_MODEL_DEEPFM ||
                          (fxk == 2 && !in.y1 && t != RMX_MODEL_PNN && t != RMX_MODEL_DNN));
     float* xo = fuse_x ? T.x : nullptr;
-    if (t == RMX_MODEL_DEEPFM) {
+    // DeepFM at a batch that fills the GPU: encoder + layer 1 as the row-owner head storing x and the FM sums
+    // too (k_head_s3.hip XS; knob "train_head_s3", default 1)
+    const bool head_x = t == RMX_MODEL_DEEPFM && fuse_x && !in.y1 && in.ids && in.dtype == kF32 && T.fms &&
+                        tuning_get("train_emb_fused", 1) != 0 && tuning_get("train_head_s3", 1) != 0 &&
+                        m.layers.size() > 1 && tower_head_s3_usable(m.layers[0], B, F, k, true);
+    if (head_x) {
+      StageTimer tm(m, s, "head_x");
+      T.fms_valid = true;
+      if ((st = launch_tower_head_s3(s, m.layers[0], B, F, in.ids, (const float*)in.table, 0, (const float*)in.wtab, 0,
+                                     T.h[0], m.layers[0].Npad, m.y12, 1, T.x, T.ldx, T.fms)))
+        return st;
+      pre = m.y12;
+    } else if (t == RMX_MODEL_DEEPFM) {
       StageTimer tm(m, s, fuse_x ? "encoder_fm_x" : "encoder_fm");
       // the FM sums for the fused embedding gradient (knob "train_emb_fused", default on)
       T.fms_valid = T.fms && k == 16 && tuning_get("train_emb_fused", 1) != 0;
@@ -1736,8 +1748,12 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     const float* A = T.x;
     int lda = T.ldx;
     static const char* names[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
-    for (size_t i = 0; i < m.layers.size(); ++i) {
+    for (size_t i = head_x ? 1 : 0; i < m.layers.size(); ++i) {
       const DenseLayer& L = m.layers[i];
+      if (i == 1 && head_x) {
+        A = T.h[0];
+        lda = m.layers[0].Npad;
+      }
       StageTimer tm(m, s, names[std::min<size_t>(i, 3)]);
       XColArgs xc{T.xcol, L.N1, Lc + 1};
       const bool fused = i == 0 && m.dcn_fused;

@@ -232,6 +232,39 @@ def _backward_ids_check(kind, B, fc, F=39, V=20_000):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B", [512, 4099])
+def test_backward_head_x_matches_oracle(B):
+    """train_head_s3: DeepFM's encoder + tower layer 1 as the row-owner head that also stores x and the FM
+    sums (k_head_s3.hip, XS) -- every gradient and the loss against the oracle at the usual bar.  B = 512 runs
+    it as half row blocks on part of the chip (s3_head 2 forces it), 4,099 one row past the default rule's
+    threshold (16 rows per CU); the stage list shows the head ran."""
+    import rmx
+    rmx.set_tuning("s3_head", 2)
+    try:
+        _backward_ids_check("deepfm", B, (400, 400, 400))
+        ctx = rmx.default_context()
+        V, F, K = 20_000, 39, 16
+        m = _gpu_model(rmx, "deepfm", V, F, K, (400, 400, 400))
+        m.setMats(m.initMats(SEED_MATS))
+        m.setBias(0.01)
+        t = rmx.EmbeddingTable(ctx, V, K)
+        t.fill_synthetic(SEED_TAB)
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        ids.upload(oc.gen_ids(SEED_IDS, 9, B, F, V).astype(np.int32))
+        targets = rmx.DeviceArray(ctx, B, np.float32)
+        targets.upload(np.zeros(B, np.float32))
+        out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, m.matsLength(), 1)]
+        m.set_timing(True)
+        m.backward_ids(t, B, ids, targets, *out)
+        ctx.sync()
+        stages, _ = m.get_timing()
+        m.set_timing(False)
+        assert "head_x" in stages and "encoder_fm_x" not in stages and "tower_layer1" not in stages, stages
+    finally:
+        rmx.set_tuning("s3_head", None)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("variant,gz", [(0, 128), (1, 128), (1, 64), (2, 128)])
 @pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn"])
 def test_backward_weight_grad_variants(kind, variant, gz):
