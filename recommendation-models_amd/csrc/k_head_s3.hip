@@ -51,7 +51,8 @@ struct HeadS3Args {
   int fm_sums;
   float* X;               // XS (training forward): [M][ldx] the gathered rows x, as the encoder stores them
   int ldx;
-  float* S;               // XS: [M][16] the FM sums s_j (field order), or null
+  float* S;               // XS: [2][M][16] the FM sums s_j (field order), then the ReLU mask bits of h1 as
+                          // uint32 (k_rowown.hpp bits_set; one pointer: a separate one spilled 179 SGPRs)
 };
 
 // XS: the x stores of rows past M / fields past F go here instead (every store is issued: the units'
@@ -222,12 +223,23 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_head_s3_kernel(HeadS3Args 
     asm volatile("" : "+v"(g4));
     if (m < p.M) {
       float* hrow = p.H + (int64_t)m * kQN;
+      uint32_t mb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
       for (int t = 0; t < kQNT; ++t) {
         const f32x4 bb = *reinterpret_cast<const f32x4*>(bl + 16 * t + g4);
-        *reinterpret_cast<f32x4*>(hrow + 16 * t + g4) = relu4(acc[t] + bb);
+        const f32x4 v = relu4(acc[t] + bb);
+        *reinterpret_cast<f32x4*>(hrow + 16 * t + g4) = v;
+        if constexpr (XS) {
+          bits_set(mb, t, v);
+          __builtin_amdgcn_sched_barrier(0);  // tile by tile (scheduled together, the bits spilled 177 SGPRs)
+        }
       }
       *reinterpret_cast<f32x4*>(hrow + 16 * kQNT + g4) = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (XS)
+        if (p.S) {
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<u32x4*>(p.S + ((int64_t)p.M + m) * 16 + g4) = u32x4{mb[0], mb[1], mb[2], mb[3]};
+        }
     }
     {
 #pragma clang fp contract(off)

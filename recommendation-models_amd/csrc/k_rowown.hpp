@@ -188,6 +188,18 @@ __device__ __forceinline__ void q_enter() {
   asm volatile("" ::: "memory");
 }
 
+// the ReLU mask bits of a lane's outputs (training, k_layer_s3.hip): tile t's four outputs (n = 16 t + 4 g + q)
+// at bits 4 t + q of the lane's 4-word group (100 of 128 bits for 25 tiles).  v is a ReLU output (> 0 or +0),
+// so its bit is min(bits(v), 1): integer ops only (compares would hold 100 lane masks in SGPR pairs: the
+// head spilled 179 SGPRs with them)
+__device__ __forceinline__ void bits_set(uint32_t (&mb)[4], int t, const f32x4& v) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = 4 * t + q;
+    mb[i >> 5] |= min(__float_as_uint(v[q]), 1u) << (i & 31);
+  }
+}
+
 __device__ __forceinline__ f32x4 relu4(f32x4 v) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;

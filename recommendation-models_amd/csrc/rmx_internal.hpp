@@ -138,7 +138,14 @@ int launch_tower_tail_bf16(hipStream_t s, const DenseLayer& L2, const DenseLayer
 // fp32 tower layer 1 of DeepFM as a row-owner kernel (k_head_s3.hip): gather (k = 16, ids [M][F], table row
 // of id at table + id * ld) + ReLU(x W1^T + b1) -> H [M][416] + first order (+ FM: fm_sums) -> fm_y [M]
 bool tower_head_s3_usable(const DenseLayer& L1, int M, int F, int k, bool ids);
-// X / S (nullable; X non-null selects the training variant): also x [M][ldx] and the FM sums [M][16]
+// one 400 x 400 fp32 layer as a row-owner kernel (k_layer_s3.hip), for the training step: forward
+// (dx = false: C = ReLU(A W^T + b), and its ReLU mask bits hm_out [M][16]) or dX (dx = true: C = (A W) masked
+// by the bits hm_in of the layer below, W^T's planes); A [M][lda], C [M][ldc]
+bool layer_s3_usable(const DenseLayer& L, bool dx, int M, int lda, int ldc);
+int launch_layer_s3(hipStream_t s, const DenseLayer& L, bool dx, int M, const float* A, int lda, float* C, int ldc,
+                    uint32_t* hm_out, const uint32_t* hm_in);
+// X / S (nullable; X non-null selects the training variant): also x [M][ldx], and into S [2][M][16] the FM
+// sums, then h1's ReLU mask bits (k_rowown.hpp bits_set)
 int launch_tower_head_s3(hipStream_t s, const DenseLayer& L1, int M, int F, const int32_t* ids, const float* table,
                          int ld, const float* wtab, int wld, float* H, int ldc, float* fm_y, int fm_sums,
                          float* X = nullptr, int ldx = 0, float* S = nullptr);

@@ -35,6 +35,8 @@ struct TrainState {
   int ldx = 0;                  // row stride of x / dx
   float* x = nullptr;           // [B][ldx] tower input (Reshape(B, F*k) of the gathered rows)
   std::vector<float*> h;        // per tower layer [B][Npad]
+  std::vector<float*> hm;       // per tower layer [B][16] ReLU mask bits (uint32), written by the row-owner
+  std::vector<char> hm_ok;      //   forward kernels this step (k_layer_s3.hip / k_head_s3.hip XS); hm_ok: valid
   float* g[2] = {nullptr, nullptr};  // [B][maxld] dPre / dx ping-pong
   float* p = nullptr;           // [B] probabilities
   float* dz = nullptr;          // [B] dL/dlogit
@@ -1540,6 +1542,9 @@ int ensure_train(rmx_model& m, int B) {
   tfree(T.x);
   for (auto& p : T.h) tfree(p);
   T.h.clear();
+  for (size_t i = 1; i < T.hm.size(); ++i) tfree(T.hm[i]);  // (hm[0] is borrowed from fms, never owned)
+  T.hm.clear();
+  T.hm_ok.clear();
   tfree(T.g[0]);
   tfree(T.g[1]);
   tfree(T.fms);
@@ -1573,6 +1578,10 @@ int ensure_train(rmx_model& m, int B) {
   for (auto& L : m.layers) {
     T.h.push_back(nullptr);
     if ((st = talloc(&T.h.back(), (size_t)B * L.Npad))) return st;
+    T.hm.push_back(nullptr);
+    T.hm_ok.push_back(0);
+    // (layer 1's bits, from the training head, live in T.fms's second half)
+    if (T.h.size() > 1 && L.N == 400 && L.Npad == 416 && (st = talloc(&T.hm.back(), (size_t)B * 16))) return st;
     maxld = std::max(maxld, L.Npad);
   }
   if (!m.layers.empty()) {
@@ -1580,7 +1589,8 @@ int ensure_train(rmx_model& m, int B) {
     if ((st = talloc(&T.g[1], (size_t)B * maxld))) return st;
   }
   if ((st = talloc(&T.p, B)) || (st = talloc(&T.dz, B)) || (st = talloc(&T.ones, B))) return st;
-  if (m.type == RMX_MODEL_DEEPFM && m.k == 16 && (st = talloc(&T.fms, (size_t)B * 16))) return st;
+  // [2][B][16]: the FM sums, then (training head, k_head_s3.hip XS) h1's ReLU mask bits
+  if (m.type == RMX_MODEL_DEEPFM && m.k == 16 && (st = talloc(&T.fms, (size_t)B * 32))) return st;
   if ((st = talloc(&T.tmp, std::max(maxld, 2 * m.cross_depth + 1)))) return st;
   if (m.type == RMX_MODEL_XDEEPFM) {
     const int64_t R = (int64_t)B * m.k;
@@ -1628,6 +1638,7 @@ void train_release(rmx_model& m) {
   (void)hipDeviceSynchronize();
   tfree(T.x);
   for (auto& p : T.h) tfree(p);
+  for (size_t i = 1; i < T.hm.size(); ++i) tfree(T.hm[i]);  // (hm[0] is borrowed from fms, never owned)
   tfree(T.g[0]);
   tfree(T.g[1]);
   tfree(T.fms);
@@ -1702,12 +1713,15 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
     const bool head_x = t == RMX_MODEL_DEEPFM && fuse_x && !in.y1 && in.ids && in.dtype == kF32 && T.fms &&
                         tuning_get("train_emb_fused", 1) != 0 && tuning_get("train_head_s3", 1) != 0 &&
                         m.layers.size() > 1 && tower_head_s3_usable(m.layers[0], B, F, k, true);
+    for (auto& ok : T.hm_ok) ok = 0;
     if (head_x) {
       StageTimer tm(m, s, "head_x");
       T.fms_valid = true;
       if ((st = launch_tower_head_s3(s, m.layers[0], B, F, in.ids, (const float*)in.table, 0, (const float*)in.wtab, 0,
                                      T.h[0], m.layers[0].Npad, m.y12, 1, T.x, T.ldx, T.fms)))
         return st;
+      T.hm[0] = T.fms + (int64_t)B * 16;  // (not owned: see ensure_train)
+      T.hm_ok[0] = 1;
       pre = m.y12;
     } else if (t == RMX_MODEL_DEEPFM) {
       StageTimer tm(m, s, fuse_x ? "encoder_fm_x" : "encoder_fm");
@@ -1757,9 +1771,15 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       StageTimer tm(m, s, names[std::min<size_t>(i, 3)]);
       XColArgs xc{T.xcol, L.N1, Lc + 1};
       const bool fused = i == 0 && m.dcn_fused;
-      if ((st = launch_tower_layer(s, L, B, A, lda, nullptr, T.h[i], L.Npad, Epi::kReluStore, nullptr,
-                                   fused ? &xc : nullptr)))
+      if (i > 0 && layer_s3_usable(L, false, B, lda, L.Npad)) {
+        // 400 x 400 hidden layers: the row-owner kernel (k_layer_s3.hip; knob "train_layer_s3")
+        uint32_t* hmi = reinterpret_cast<uint32_t*>(T.hm[i]);
+        if ((st = launch_layer_s3(s, L, false, B, A, lda, T.h[i], L.Npad, hmi, nullptr))) return st;
+        T.hm_ok[i] = hmi ? 1 : 0;
+      } else if ((st = launch_tower_layer(s, L, B, A, lda, nullptr, T.h[i], L.Npad, Epi::kReluStore, nullptr,
+                                          fused ? &xc : nullptr))) {
         return st;
+      }
       A = T.h[i];
       lda = L.Npad;
     }
@@ -1900,6 +1920,11 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
         if (emb_fused) {
           const EmbGradArgs eg{T.x, T.fms, T.dz, T.ldx};
           if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, o.g_emb, D, nullptr, 0, &eg))) return st;
+        } else if (mask && T.hm_ok[l - 1] && bk.c0 == 0 && layer_s3_usable(L, true, B, L.Npad, ldin)) {
+          // 400 x 400 layers whose lower layer left its mask bits: the row-owner kernel (k_layer_s3.hip)
+          if ((st = launch_layer_s3(s, L, true, B, dpre, L.Npad, dxin, ldin, nullptr,
+                                    reinterpret_cast<const uint32_t*>(T.hm[l - 1]))))
+            return st;
         } else if ((st = launch_dx_s3(s, L, B, dpre, L.Npad, dxin + bk.c0, ldin, mask, ldmask))) {
           return st;
         }

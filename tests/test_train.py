@@ -265,6 +265,42 @@ def test_backward_head_x_matches_oracle(B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["deepfm", "dnn"])
+def test_backward_row_owner_layers_match_oracle(kind):
+    """train_layer_s3: the 400 x 400 hidden layers' forward (ReLU(h W^T + b), stored) and their dX (dPre W
+    masked by the ReLU of the layer below) on the row-owner kernel (k_layer_s3.hip), which needs a full round of
+    row blocks: B = 20,000 (half blocks, a ragged last block).  Every gradient and the loss against the oracle
+    at the usual bar, and against the engine's kernels (knob 0) within fp32 summation-order noise."""
+    import rmx
+    _backward_ids_check(kind, 20_000, (400, 400, 400))
+    ctx = rmx.default_context()
+    V, F, K, B = 20_000, 39, 16, 20_000
+    m = _gpu_model(rmx, kind, V, F, K, (400, 400, 400))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    ids.upload(oc.gen_ids(SEED_IDS, 13, B, F, V).astype(np.int32))
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(7).random(B) > 0.7).astype(np.float32))
+    res = {}
+    try:
+        for v in (0, 1):
+            rmx.set_tuning("train_layer_s3", v)
+            out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, len(mats), 1)]
+            m.backward_ids(t, B, ids, targets, *out)
+            ctx.sync()
+            res[v] = [o.numpy().copy() for o in out]
+    finally:
+        rmx.set_tuning("train_layer_s3", None)
+    for a, b in zip(res[0], res[1]):
+        scale = max(float(np.abs(a).max()), 1e-30)
+        assert float(np.abs(a - b).max()) <= 1e-4 * scale
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("variant,gz", [(0, 128), (1, 128), (1, 64), (2, 128)])
 @pytest.mark.parametrize("kind", ["deepfm", "xdeepfm", "dcn"])
 def test_backward_weight_grad_variants(kind, variant, gz):
