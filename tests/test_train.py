@@ -232,6 +232,38 @@ def _backward_ids_check(kind, B, fc, F=39, V=20_000):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind,B", [("deepfm", 65536), ("dnn", 40000)])
+def test_backward_slice_reduce4_bitwise(kind, B):
+    """slice_reduce4: the dW's slice reduction on float4s sums every output's slices in the scalar kernel's
+    order -- bitwise the same gradients (the 208 x 208 dW path, rows >= 32,768)."""
+    import rmx
+    ctx = rmx.default_context()
+    V, F, K = 20_000, 39, 16
+    m = _gpu_model(rmx, kind, V, F, K, (400, 400, 400))
+    mats = m.initMats(SEED_MATS)
+    m.setMats(mats)
+    m.setBias(0.01)
+    t = rmx.EmbeddingTable(ctx, V, K)
+    t.fill_synthetic(SEED_TAB)
+    ids = rmx.DeviceArray(ctx, B * F, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids)
+    targets = rmx.DeviceArray(ctx, B, np.float32)
+    targets.upload((np.random.default_rng(11).random(B) > 0.7).astype(np.float32))
+    res = {}
+    try:
+        for v in (0, 1):
+            rmx.set_tuning("slice_reduce4", v)
+            out = [rmx.DeviceArray(ctx, n, np.float32) for n in (1, B * F, B * F * K, len(mats), 1)]
+            m.backward_ids(t, B, ids, targets, *out)
+            ctx.sync()
+            res[v] = [o.numpy().copy() for o in out]
+    finally:
+        rmx.set_tuning("slice_reduce4", None)
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B", [512, 4099])
 def test_backward_head_x_matches_oracle(B):
     """train_head_s3: DeepFM's encoder + tower layer 1 as the row-owner head that also stores x and the FM
