@@ -1871,11 +1871,22 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
       RMX_HIP(hipGetLastError());
       if (cp && G > 1) {
         float* cp2 = cp + (int64_t)np * Nh;
-        hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)G * Nh + 63) / 64)), dim3(256), 0, s, np / G,
-                           (int64_t)G * Nh, cp, cp2, 0);
+        // (the float4 form when the arrays allow it: the same sums in the same order)
+        const bool v4 = Nh % 4 == 0 && ((uintptr_t)cp2 & 15) == 0 && ((uintptr_t)(o.g_mats + m.wo_off) & 15) == 0 &&
+                        tuning_get("slice_reduce4", 1) != 0;
+        if (v4)
+          hipLaunchKernelGGL(slice_reduce4_kernel, dim3((unsigned)(((int64_t)G * Nh / 4 + 63) / 64)), dim3(256), 0, s,
+                             np / G, (int64_t)G * Nh, cp, cp2, 0, (int64_t)0, nullptr, nullptr);
+        else
+          hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)(((int64_t)G * Nh + 63) / 64)), dim3(256), 0, s, np / G,
+                             (int64_t)G * Nh, cp, cp2, 0);
         RMX_HIP(hipGetLastError());
-        hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((Nh + 63) / 64)), dim3(256), 0, s, G, (int64_t)Nh, cp2,
-                           o.g_mats + m.wo_off, 0);
+        if (v4)
+          hipLaunchKernelGGL(slice_reduce4_kernel, dim3((unsigned)((Nh / 4 + 63) / 64)), dim3(256), 0, s, G, (int64_t)Nh,
+                             cp2, o.g_mats + m.wo_off, 0, (int64_t)0, nullptr, nullptr);
+        else
+          hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((Nh + 63) / 64)), dim3(256), 0, s, G, (int64_t)Nh, cp2,
+                             o.g_mats + m.wo_off, 0);
         RMX_HIP(hipGetLastError());
       } else if (cp) {
         hipLaunchKernelGGL(slice_reduce_kernel, dim3((unsigned)((Nh + 63) / 64)), dim3(256), 0, s, np, (int64_t)Nh, cp,
