@@ -297,7 +297,7 @@ def test_backward_head_x_matches_oracle(B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["deepfm", "dnn"])
+@pytest.mark.parametrize("kind", ["deepfm", "dnn", "dcn", "pnn"])
 def test_backward_row_owner_layers_match_oracle(kind):
     """train_layer_s3: the 400 x 400 hidden layers' forward (ReLU(h W^T + b), stored) and their dX (dPre W
     masked by the ReLU of the layer below) on the row-owner kernel (k_layer_s3.hip), which needs a full round of
