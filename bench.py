@@ -65,6 +65,11 @@ def parse():
                     default="deepfm")
     ap.add_argument("--no-encoder-record", action="store_true",
                     help="deepfm: skip the encoder sub-record (gather + first order + FM alone at V = 1M and 100M)")
+    ap.add_argument("--enc-table", choices=["row", "line", "both"], default="both",
+                    help="encoder workload: time the [V][k] row table, the [V][32] line table or both (a PMC pass "
+                         "profiles one layout per run: the kernel instantiation is the same)")
+    ap.add_argument("--no-la-record", action="store_true",
+                    help="deepfm: skip the L-A record (rmx_forward with host arrays at B = 100 / 4,096 / 65,536)")
     ap.add_argument("--no-companion", action="store_true",
                     help="deepfm: skip the xDeepFM sub-record (BASELINE.json's metric names both models)")
     ap.add_argument("--no-sharded-companion", action="store_true",
@@ -264,6 +269,9 @@ def parity_check(workload, got, row0, n=512, vocab=V, ids_host=None):
 # launch_ranks see it, not only a string inside the line
 STATUS_PARITY_MISS = 5
 STATUS_COMPANION_FAILED = 6
+STATUS_RECORD_ERROR = 7
+STATUS_REASON = {STATUS_PARITY_MISS: "parity miss", STATUS_COMPANION_FAILED: "sharded sub-record failed",
+                 STATUS_RECORD_ERROR: "encoder / L-A sub-record raised"}
 
 
 def _pc_ok(p):
@@ -289,6 +297,22 @@ def job_status(parity_ranks=None, sub=None, cpu=None, cpu2=None):
         if not sub.get("parity_ok", True):
             return STATUS_PARITY_MISS
     return 0
+
+
+def record_status(*recs):
+    """Status of rank 0's encoder / L-A sub-records ({"V1M": {...}, ...} or {"B100": {...}, ...}): an entry
+    that raised is STATUS_RECORD_ERROR (not a parity miss), a failed check STATUS_PARITY_MISS."""
+    st = 0
+    for rec in recs:
+        for k_, e in (rec or {}).items():
+            if not isinstance(e, dict):
+                continue
+            if "error" in e:
+                return STATUS_RECORD_ERROR
+            pc = e.get("parity_check", {})
+            if not (pc.get("bitwise_equal", False) if k_.startswith("V") else pc.get("ok", False)):
+                st = STATUS_PARITY_MISS
+    return st
 
 
 def cpu_model():
@@ -458,10 +482,13 @@ def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
     bpe = F * 4 + F * 4 + F * K * 4 + 4
     rec = {"kernel": ("encoder_k16v2_kernel (enc_u %d)" % rmx.get_tuning("enc_u", 20)) if rmx.get_tuning("enc_u", 20)
            else "encoder_k16_kernel<1, float>", "batch": B, "vocab": Vw,
+           **({"kernel_line_table": "encoder_line8_kernel (enc_line8 %d: one whole-line load per id)"
+               % rmx.get_tuning("enc_line8", 1)} if rmx.get_tuning("enc_line8", 1) else {}),
            "algorithmic_bytes_per_example": bpe, "peak_gbs": PEAK_HBM_GBS}
     saved = rmx.get_tuning("table_lines", 0)
+    layouts = {"row": (0,), "line": (1,)}.get(getattr(args, "enc_table", "both"), (0, 1))
     try:
-        for lines in (0, 1):
+        for lines in layouts:
             rmx.set_tuning("table_lines", lines)
             table.refresh_lines()
             ctx.sync()
@@ -489,12 +516,24 @@ def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
                    "lines_per_example": lines_per_ex,
                    "line_gbs": round(B * (lines_per_ex * 128 + F * 4 + 4) / avg_s / 1e9, 1),
                    "line_frac": round(B * (lines_per_ex * 128 + F * 4 + 4) / avg_s / 1e9 / PEAK_HBM_GBS, 4)}
+            # HBM bytes per launch from the committed rocprofv3 PMC passes of this exact record
+            # (tools/gpu_check.sh pmcenc, tools/pmc_summary.py --stages: FETCH_SIZE x 2 + WRITE_SIZE)
+            tkey = "encoder_V%dM_%s" % (Vw // 1_000_000, "line" if lines else "row")
+            tent = _traffic(tkey, "encoder", B)
+            ent["traffic"] = tent["hbm_bytes"] if tent else None
+            if tent:
+                ent["traffic_per_example"] = round(tent["hbm_bytes"] / B, 1)
+                ent["traffic_over_algorithmic"] = round(tent["hbm_bytes"] / (B * bpe), 3)
+                ent["traffic_source"] = "profiles/traffic.json %s (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)" % tkey
+                if "avg_ns" in tent:  # the same launches' kernel-trace duration under the profiler
+                    ent["pmc_pass_avg_ms"] = round(tent["avg_ns"] / 1e6, 4)
             rec["line_table" if lines else "row_table"] = ent
+        # parity (bit-exact) on the layout timed last: rows [0, n) of the first batch, y = y1 + y2 from the
+        # oracle's own gather + sums
+        m.encoder_ids(table, B, ids.view(0, B * F), y.view(0, B), stream)
+        ctx.sync()
     finally:
         rmx.set_tuning("table_lines", saved)
-    # parity (bit-exact): rows [0, n) of the first batch, y = y1 + y2 from the oracle's own gather + sums
-    m.encoder_ids(table, B, ids.view(0, B * F), y.view(0, B), stream)
-    ctx.sync()
     got = y.numpy()[:256]
     oc = _oracle()
     n = 256
@@ -511,6 +550,15 @@ def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
     return rec
 
 
+def _traffic(workload, stage, B):
+    """profiles/traffic.json entry of (workload, stage) when it was profiled at batch B, else None."""
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(tpath):
+        return None
+    ent = json.load(open(tpath)).get(workload, {}).get(stage)
+    return ent if ent and ent.get("batch") == B else None
+
+
 def encoder_record(args, rmx, ctx, steps, warmup):
     """models.encoder of the default line: the encoder alone at V = 1M (Infinity-Cache resident) and 100M."""
     out = {"note": ("the DeepFM forward fuses this encoder into tower layer 1 (k_fused_s3.hip); timed alone here "
@@ -520,6 +568,87 @@ def encoder_record(args, rmx, ctx, steps, warmup):
             out["V%dM" % (Vw // 1_000_000)] = run_encoder(args, rmx, ctx, steps, warmup, Vw)
         except Exception as e:
             out["V%dM" % (Vw // 1_000_000)] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
+    return out
+
+
+LA_BATCHES = (100, 4096, 65536)  # 100 = the reference's batchSize (example/DeepFMLocalExample.scala:16)
+
+
+def run_la(args, rmx, ctx, B, calls):
+    """L-A: rmx_forward, the exact RecModel.forward host-array contract (RecModel.scala:37-48,
+    ParRecModel.scala:555-567) -- COO index / feats, the gathered first-order weights [nnz] and embeddings
+    [nnz][k], and the whole mats array with EVERY call, as the Scala side would hand them over through JNI
+    (pageable host memory) -- timed end to end on the host clock (arrays in, probabilities out), plus its
+    stages from HIP events: la_mats (mats H2D + pack), la_h2d (rows / weights H2D), the forward's kernels
+    and la_d2h.  The host arrays are the device table's own rows (rmx_gather), so the forward sees the same
+    inputs as the L-B line; parity against the fp64 oracle, and bitwise against L-B on the same rows."""
+    m = rmx.DeepFM(V, F, K, FC, ctx=ctx)
+    mats = m.initMats(SEED_MATS)
+    sizes = np.asarray(m.getMatsSize(), np.int32)
+    table = rmx.EmbeddingTable(ctx, V, K)
+    table.fill_synthetic(SEED_TAB)
+    nnz = B * F
+    ids = rmx.DeviceArray(ctx, nnz, np.int32)
+    rmx.gen_ids(ctx, SEED_IDS, 0, B, F, V, ids)
+    w_d = rmx.DeviceArray(ctx, nnz, np.float32)
+    e_d = rmx.DeviceArray(ctx, nnz * K, np.float32)
+    table.gather(ids, nnz, w_d, e_d)
+    ctx.sync()
+    feats = ids.numpy().astype(np.int64)
+    index = np.repeat(np.arange(B, dtype=np.int64), F)
+    w, e = w_d.numpy(), e_d.numpy()
+    bias = np.array([0.01], np.float32)
+    batch = rmx.CooLongFloatMatrix(index, feats)
+
+    def call():
+        return m.forward(B, batch, bias, w, e, K, mats, sizes)
+
+    for _ in range(max(3, calls // 10)):
+        out = call()
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        out = call()
+    wall = (time.perf_counter() - t0) / calls
+    m.set_timing(True)
+    nt = max(3, min(calls, 20))
+    for _ in range(nt):
+        call()
+    stages, ncalls = m.get_timing()
+    m.set_timing(False)
+    st = {n: round(t / max(ncalls, 1), 4) for n, t in stages.items()}
+    kern = sum(v for n, v in st.items() if not n.startswith("la_"))
+    # L-B on the same rows and table (forward_ids), for the bitwise comparison
+    m.setMats(mats)
+    m.setBias(0.01)
+    o_d = rmx.DeviceArray(ctx, B, np.float32)
+    m.forward_ids(table, B, ids, o_d)
+    ctx.sync()
+    lb = o_d.numpy()
+    mats_b = 4 * len(mats)
+    rows_b = 4 * nnz * (K + 1)
+    pc = parity_check("deepfm", out, 0, n=min(B, 512))
+    rec = {"batch": B, "calls": calls, "wall_ms_per_call": round(wall * 1e3, 4),
+           "examples_per_s": round(B / wall, 1), "stages_ms": st, "kernels_ms": round(kern, 4),
+           "h2d_bytes_per_call": {"mats": mats_b, "rows_and_weights": rows_b},
+           "h2d_gbs": round((mats_b + rows_b) / ((st.get("la_mats", 0) + st.get("la_h2d", 0)) / 1e3) / 1e9, 1)
+           if st.get("la_h2d") else None,
+           "pcie_cap_examples_per_s": round(63e9 / (4 * F * (K + 1)), 1),
+           "parity_check": pc, "bitwise_vs_lb": bool(np.array_equal(out, lb))}
+    table.close()
+    m.close()
+    return rec
+
+
+def la_record(args, rmx, ctx):
+    """models.deepfm_la of the default line: the L-A drop-in (host arrays) at B = 100 / 4,096 / 65,536."""
+    out = {"note": ("rmx_forward: the RecModel.forward host-array contract through librmx (what the JNI shim "
+                    "calls); SURVEY.md §8b prices its cap at PCIe: (16 + 1) x 4 B x 39 per example at 63 GB/s "
+                    "= 23.8 M examples/s, before the per-call mats")}
+    for B in LA_BATCHES:
+        try:
+            out["B%d" % B] = run_la(args, rmx, ctx, B, {100: 200, 4096: 50}.get(B, 10))
+        except Exception as e:
+            out["B%d" % B] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
     return out
 
 
@@ -553,6 +682,7 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
             table = rmx.ShardedTable(ctx, Vw, K, world, rank, uid)
             LIVE_SHARDS.append(table)
         table.set_dedupe(False if args.no_dedupe else (True if args.dedupe_on else "auto"))
+        table.set_batch_hint(B * F)  # every rank the same B: the first exchange skips the overflow round
     else:
         table = rmx.EmbeddingTable(ctx, Vw, K, rmx.DTYPE_BF16 if bf16 else rmx.DTYPE_F32)
     table.fill_synthetic(SEED_TAB)
@@ -911,15 +1041,16 @@ def main():
         Vw = args.vocab or 100_000_000
         rec = run_encoder(args, rmx, ctx, args.steps, args.warmup, Vw, B=args.batch or 65536)
         if rank == 0:
-            ent = rec["row_table"]
+            lay = "row_table" if "row_table" in rec else "line_table"
+            ent = rec[lay]
             print(json.dumps({
                 "metric": "encoder (gather + first order + FM) examples/sec", "value": ent["examples_per_s"],
                 "unit": "examples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": ent["avg_ms"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": "f32", "data": "synthetic", "config": {"workload": "encoder_fp32_F39_V%s_k16_B%d" % (
-                    ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else Vw, rec["batch"])},
+                "dtype": "f32", "data": "synthetic", "config": {"workload": "encoder_fp32_F39_V%s_k16_B%d_%s" % (
+                    ("%dM" % (Vw // 1_000_000)) if Vw % 1_000_000 == 0 else Vw, rec["batch"], lay)},
                 "roofline": {"bound": "hbm", "achieved": ent["achieved_gbs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": ent["frac"], "traffic": None, "kernel": rec["kernel"]},
+                             "frac": ent["frac"], "traffic": ent.get("traffic"), "kernel": rec["kernel"]},
                 "encoder": rec}), flush=True)
         if dist:
             dist.destroy_process_group()
@@ -930,11 +1061,6 @@ def main():
     companion = None
     if args.workload == "deepfm" and not args.no_companion:
         companion = run(args, "xdeepfm", rmx, ctx, rank, world, dist, args.steps, args.warmup, B=16384)
-    # the encoder alone (gather + first order + FM) at V = 1M and 100M: its HBM roofline
-    enc = None
-    if args.workload == "deepfm" and not args.no_encoder_record and not args.zipf and rank == 0:
-        enc = encoder_record(args, rmx, ctx, max(20, min(args.steps, 100)), max(5, args.warmup))
-
     cpu = cpu2 = None
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not train and not args.parity_only
     if rank == 0 and world == 1 and args.parity_only and not train and args.workload != "lr_plumbing":
@@ -1011,8 +1137,6 @@ def main():
                 "roofline": companion["roofline"], "stages": companion["stages"],
                 "stage_sum_ms": companion["stage_sum_ms"], "cpu_baseline": cpu2,
                 **({"predict_auc": companion["predict_auc"]} if companion.get("predict_auc") else {})}}
-        if enc is not None:
-            line.setdefault("models", {})["encoder"] = enc
         if not train and args.workload != "lr_plumbing":
             # BASELINE.json asks for the HBM-roofline fraction too: the whole forward's algorithmic
             # bytes per example (ids + first-order weights + embedding rows + output)
@@ -1032,20 +1156,26 @@ def main():
         sub = sharded_companion(args, rmx, ctx, rank, world, dist, line if rank == 0 else None)
         if rank == 0:
             line.setdefault("models", {})["deepfm_sharded"] = sub
-    status = job_status(parity_ranks, sub, cpu, cpu2)
-    if enc is not None and any(not e.get("parity_check", {}).get("bitwise_equal", False)
-                               for k_, e in enc.items() if k_.startswith("V")):
-        status = status or STATUS_PARITY_MISS
+    # rank 0's own sub-records, after the sharded one (whose watchdog budget they would otherwise eat at
+    # N > 1): the encoder alone (gather + first order + FM) at V = 1M and 100M, its HBM
+    # roofline, and the L-A drop-in (host arrays) at the reference's batch sizes
+    enc = la = None
+    if args.workload == "deepfm" and not args.zipf and rank == 0:
+        if not args.no_encoder_record:
+            enc = encoder_record(args, rmx, ctx, max(20, min(args.steps, 100)), max(5, args.warmup))
+            line.setdefault("models", {})["encoder"] = enc
+        if not args.no_la_record:
+            la = la_record(args, rmx, ctx)
+            line.setdefault("models", {})["deepfm_la"] = la
+    status = job_status(parity_ranks, sub, cpu, cpu2) or record_status(enc, la)
     if rank == 0:
         if status:
-            line["status"] = {"exit": status, "reason": "parity miss" if status == STATUS_PARITY_MISS
-                              else "sharded sub-record failed"}
+            line["status"] = {"exit": status, "reason": STATUS_REASON[status]}
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
     if status:
-        sys.stderr.write("bench.py: rank %d exits %d (%s)\n" % (rank, status, "parity miss" if status == STATUS_PARITY_MISS
-                                                                 else "sharded sub-record failed"))
+        sys.stderr.write("bench.py: rank %d exits %d (%s)\n" % (rank, status, STATUS_REASON[status]))
         raise SystemExit(status)
 
 

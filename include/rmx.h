@@ -218,6 +218,12 @@ int rmx_gen_ids_zipf(rmx_ctx* ctx, uint64_t seed, int64_t row0, int32_t batch, i
  * kernel launched next that reads LDS it never wrote reads that pattern (tests/test_small_s3.py). */
 int rmx_debug_fill_lds(rmx_ctx* ctx, uint32_t pattern, void* stream);
 
+/* Test hook (host only, no GPU): the slice count S the training dW on the 208 x 208 tile uses for a
+ * rows x N x K weight gradient on a device with ncu CUs.  S fixes the dW's fp32 summation order over the
+ * slices, so gradients are bitwise reproducible across devices with the same CU count (every 256-CU
+ * MI355X), not across CU counts.  Returns S (> 0) or RMX_E_INVALID. */
+int rmx_debug_wgrad_slices(int64_t rows, int N, int K, int ncu);
+
 /* Debug gather: d_w[n] = weights[ids[n]], d_emb[n*k+j] = emb[ids[n]][j] (makeWeights /
  * makeEmbeddings, ParRecModel.scala:279-306).  Bit-exact copies (as fp32 for a bf16 table). */
 int rmx_gather(const rmx_table* t, int64_t n, const int32_t* d_ids, float* d_w, float* d_emb,
@@ -256,7 +262,8 @@ int rmx_encoder_ids(rmx_model* m, const rmx_table* t, int32_t batch, const int32
  * once.  Abort the shard on every rank (rmx_shard_abort, then rmx_shard_destroy) and create a new one;
  * peers already waiting in the failed exchange are released by their own abort (e.g. a watchdog).
  * The first exchange of a shard has no agreed bucket capacity yet, so all of its ids take the counted
- * overflow round (one extra round, once; timed under the "shard_exchange" stage).
+ * overflow round (one extra round, once; timed under the "shard_exchange" stage) -- unless every rank
+ * called rmx_shard_set_batch_hint with the same ids-per-batch figure first, which seeds that capacity.
  * CONTRACT CHANGE (round 3): the default owner function is the keyed permutation below, no longer
  * id mod nranks.  A caller that pre-partitions ids or rows must use rmx_owner_hash (or
  * rmx_shard_set_owner_hash(sh, 0) for id mod nranks). 
@@ -294,6 +301,12 @@ int64_t rmx_owner_hash(uint64_t key, int64_t num_rows, int nranks, int64_t id, i
  * on: 0 off, 1 on, 2 auto (default: off at one rank; else on for a batch, then off for the next 63
  * batches when it removed fewer than 10 % of the ids, re-probed after them). */
 int rmx_shard_set_dedupe(rmx_shard* sh, int on);
+/* Seeds the first fixed-capacity exchange's bucket capacity from nnz, the ids one rank sends per batch
+ * (B * nFields; the reference's batchSize * fields, ParRecModel.scala:165-199): ~1.1 nnz / nranks per
+ * peer.  Collective by value: every rank must pass the same nnz before its first exchange.  Later
+ * exchanges size their buckets from the previous one as before.  Without it the first exchange runs its
+ * ids through the counted overflow round. */
+int rmx_shard_set_batch_hint(rmx_shard* sh, int64_t nnz);
 /* Ids this rank sent to owners in its last exchange (the distinct ids when deduplicating). */
 int64_t rmx_shard_last_sent(const rmx_shard* sh);
 /* Overflow rounds this shard has run (fixed-capacity exchange at nranks > 1: an id past its bucket's

@@ -60,6 +60,31 @@ static_assert(kFLds <= 160 * 1024, "LDS budget");
 #define RMX_FUSED_PF3 1
 #endif
 
+// Diagnostic builds only (tools/diag_fused.py; never set in librmx.so): s_memtime stamps of block 0's waves
+// at the layer boundaries of its first row blocks, s_memrealtime at the kernel's start and end (the clock)
+#ifndef RMX_FUSED_DIAG
+#define RMX_FUSED_DIAG 0
+#endif
+#if RMX_FUSED_DIAG
+constexpr int kFDiagIt = 4, kFDiagPh = 6;
+__device__ unsigned long long g_fused_t[kQW][kFDiagIt][kFDiagPh];  // [wave][row block][phase]
+__device__ unsigned long long g_fused_clk[kQW][4];                   // memtime / memrealtime at start, end
+// one lane's vector store (the value and the address depend on the lane: never a scalar-cache store)
+__device__ __forceinline__ void f_stamp(unsigned long long* dst, int lane, unsigned long long v) {
+  int l = lane;
+  asm volatile("" : "+v"(l), "+v"(v));
+  if (l == 0) dst[l] = v;
+}
+#define F_STAMP(it, ph)                                                                                  \
+  do {                                                                                                   \
+    if (blockIdx.x == 0 && (it) < kFDiagIt) f_stamp(&g_fused_t[w][it][ph], lane, __builtin_amdgcn_s_memtime()); \
+  } while (0)
+#else
+#define F_STAMP(it, ph) \
+  do {                  \
+  } while (0)
+#endif
+
 struct FusedS3Args {
   int M, F, KS, NU;       // KS = ceil(F / 2) layer-1 K steps; NU = 2 KS + 52 units per row block
   QRows rows;             // full / half row blocks (k_rowown.hpp)
@@ -231,6 +256,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   // knob "fused_prio" (timing A/B): the second-dispatched half of the waves at priority 1 (MI355X_MICROARCH.md,
   // two waves per SIMD item 4)
   if (p.prio && w >= kQW / 2) __builtin_amdgcn_s_setprio(1);
+#if RMX_FUSED_DIAG
+  if (blockIdx.x == 0) {
+    f_stamp(&g_fused_clk[w][0], lane, __builtin_amdgcn_s_memtime());
+    f_stamp(&g_fused_clk[w][1], lane, __builtin_amdgcn_s_memrealtime());
+  }
+#endif
 
   for (int i = tid; i < kFPrm; i += kQThreads) {
     const int a = i / kQN, n = i - a * kQN;
@@ -292,6 +323,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       continue;
     }
     // ---- layer 1 (+ first order + FM): units (c, half 0), (c, half 1) ----
+    F_STAMP(it, 0);
     f32x4 h1[kQNT];
 #pragma unroll
     for (int t = 0; t < kQNT; ++t) h1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -341,6 +373,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       slot = q_next(slot);
     }
     __builtin_amdgcn_sched_barrier(0);
+    F_STAMP(it, 1);
     // first order + FM of the row (k_head_s3.hip's epilogue: encoder_k16_kernel<1>'s arithmetic)
     float pre;
     {
@@ -364,6 +397,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       for (int t = 0; t < kQNT; ++t) h1[t] = relu4(h1[t] + f_sbias(b1, t, g));
     }
     // ---- layer 2: units (c, half 0), (c, half 1); h1 tiles 2c, 2c + 1 die after step c ----
+    F_STAMP(it, 2);
     f32x4 h2[kQNT];
 #pragma unroll
     for (int t = 0; t < kQNT; ++t) h2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -391,9 +425,12 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       for (int t = 0; t < kQNT; ++t) h2[t] = relu4(h2[t] + f_sbias(b2, t, g));
     }
     // ---- layer 3 + the output dot ----
+    F_STAMP(it, 3);
     float part = 0.f;
     f_layer3<0>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    F_STAMP(it, 4);
     f_layer3<1>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    F_STAMP(it, 5);
     // ---- head: the four lane groups' columns, then bias, CAddTable, sigmoid (out_finish_kernel's order) ----
     part += __shfl_xor(part, 16);
     part += __shfl_xor(part, 32);
@@ -409,9 +446,25 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   // the ring's trailing DMAs (units 0 / 1 of a row block that does not exist, the next block's ids / rows)
   // land before the block's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if RMX_FUSED_DIAG
+  if (blockIdx.x == 0) {
+    f_stamp(&g_fused_clk[w][2], lane, __builtin_amdgcn_s_memtime());
+    f_stamp(&g_fused_clk[w][3], lane, __builtin_amdgcn_s_memrealtime());
+  }
+#endif
 }
 
 }  // namespace
+
+#if RMX_FUSED_DIAG
+// out: [8 waves][4 row blocks][6 stamps] then [8 waves][4] (memtime, memrealtime at start and end)
+extern "C" int rmx_diag_fused(unsigned long long* out) {
+  RMX_HIP(hipDeviceSynchronize());
+  RMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(g_fused_t)));
+  RMX_HIP(hipMemcpyFromSymbol(out + sizeof(g_fused_t) / 8, HIP_SYMBOL(g_fused_clk), sizeof(g_fused_clk)));
+  return RMX_OK;
+}
+#endif
 
 bool tower_fused_s3_usable(const DenseLayer& L1, const DenseLayer& L2, const DenseLayer& L3, int M, int F, int k,
                            bool ids) {
@@ -457,7 +510,6 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   int dev = 0, ncu = 0;
   RMX_HIP(hipGetDevice(&dev));
   RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  // knob "fused_prep" (default 1): the next step's A formed before the step barrier (layers 1 and 3)
   RMX_HIP(hipFuncSetAttribute((const void*)tower_fused_s3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kFLds));
   FusedS3Args p{};

@@ -915,7 +915,15 @@ int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, boo
     m.la_B = B;
   }
   if ((st = ensure_ws(m, B))) return st;
-  if (m.mats_len > 0 && (st = model_load_mats(m, mats, false))) return st;
+  {
+    // the L-A contract hands over the whole mats array with every call (RecModel.scala:37-48; the reference
+    // copies it into fresh BigDL modules per forward, LayerUtil.scala:13-19): H2D + pack, timed as la_mats
+    StageTimer t(m, s, "la_mats");
+    if (m.mats_len > 0 && (st = model_load_mats(m, mats, false))) return st;
+  }
+  // la_h2d: the gathered rows / weights (+ row pointers) to HBM; for bf16 models and irregular batches also
+  // their rounding / the CSR first order that follows the copies
+  StageTimer t_h2d(m, s, "la_h2d");
   if (m.type != RMX_MODEL_LR && nnz > 0)
     RMX_HIP(hipMemcpyAsync(m.la_E, embedding, sizeof(float) * nnz * m.k, hipMemcpyHostToDevice, s));
 
@@ -989,7 +997,10 @@ int model_forward_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, b
   int st = model_stage_host(m, B, nnz, index, regular, sorted, bias, weights, embedding, mats, &in);
   if (st) return st;
   if ((st = model_forward(m, s, in))) return st;
-  RMX_HIP(hipMemcpyAsync(out, m.la_out, sizeof(float) * B, hipMemcpyDeviceToHost, s));
+  {
+    StageTimer t(m, s, "la_d2h");
+    RMX_HIP(hipMemcpyAsync(out, m.la_out, sizeof(float) * B, hipMemcpyDeviceToHost, s));
+  }
   RMX_HIP(hipStreamSynchronize(s));
   // host buffers (h_rowptr / h_wperm) stay alive until the sync above
   return RMX_OK;

@@ -154,8 +154,8 @@ struct rmx_shard {
   int64_t cap_fix = 0;                  // N * cap held by recv_fix / srow_*
   // The capacity must be the same on every rank (the message sizes pair up) without a host round trip,
   // so it comes from the PREVIOUS exchange: ~1.1 x the largest routed total of any rank there / N (every
-  // rank reads the same maximum from its summary).  The first exchange has cap 0: every id goes through
-  // the counted overflow round.
+  // rank reads the same maximum from its summary).  The first exchange has cap 0 (every id goes through
+  // the counted overflow round) unless rmx_shard_set_batch_hint seeded it with the same value on every rank.
   int64_t cap_next = 0;
   int32_t* send_ovf = nullptr;          // [cap_send] overflow ids in bucket order
   int32_t* recv_fix = nullptr;          // [N][cap] ids requested by the peers
@@ -763,6 +763,7 @@ struct RcclTransport : Transport {
   const std::atomic<int>* state;
   std::timed_mutex* mu;
   bool held = false;
+  bool group_open = false;  // ncclGroupStart succeeded and its ncclGroupEnd has not run yet
   RcclTransport(ncclComm_t c, const std::atomic<int>* st, std::timed_mutex* m) : comm(c), state(st), mu(m) {}
   ~RcclTransport() override {
     if (held) mu->unlock();
@@ -779,6 +780,7 @@ struct RcclTransport : Transport {
     }
     if (int e = live()) return e;
     RMX_NCCL(ncclGroupStart());
+    group_open = true;
     return RMX_OK;
   }
   int send(const void* p, size_t bytes, int peer, hipStream_t s) override {
@@ -801,13 +803,24 @@ struct RcclTransport : Transport {
         }
       }
     } rel{this};
-    // (with the lock held no abort can have run since start()'s check unless start() already failed; a
-    // group that start() opened is always closed)
-    if (state->load() != 0) {
+    // A group that start() opened is closed here whatever happened in between: with the lock
+    // held an abort normally waits, but rmx_shard_abort gives up waiting after 5 s and aborts the
+    // communicator anyway, and this thread must not stay inside an open RCCL group -- a later shard's
+    // ncclCommInitRank on it would run inside the leaked group.  On an aborted communicator the group's
+    // own ncclGroupEnd result is ignored; the exchange reports RMX_E_COMM.
+    const bool aborted = state->load() != 0;
+    if (group_open) {
+      group_open = false;
+      const ncclResult_t r = ncclGroupEnd();
+      if (!aborted && r != ncclSuccess) {
+        set_error(std::string("RCCL ncclGroupEnd: ") + ncclGetErrorString(r));
+        return RMX_E_COMM;
+      }
+    }
+    if (aborted) {
       set_error("shard exchange: the communicator was aborted (rmx_shard_abort)");
       return RMX_E_COMM;
     }
-    RMX_NCCL(ncclGroupEnd());
     return RMX_OK;
   }
 };
@@ -1065,6 +1078,12 @@ int shard_route(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_ids,
   const int N = sh.N;
   int st;
   *dd_out = false;
+  // test hook (knob "shard_debug_fail_rank" = rank + 1): this rank's route fails as a local error would
+  // (out of device memory, ...), so the tests can drive the failed-exchange contract of include/rmx.h
+  if (!sh.loopback && tuning_get("shard_debug_fail_rank", 0) == sh.rank + 1) {
+    set_error("shard exchange: injected route failure (knob shard_debug_fail_rank)");
+    return RMX_E_INVALID;
+  }
   const int64_t nfix = cap > 0 ? N * cap : 0;
   if ((st = ensure_batch(sh, nnz, slot, nfix))) return st;
   sh.perm = sh.perm_s[slot];
@@ -1424,6 +1443,9 @@ int shard_exchange(rmx_shard& sh, hipStream_t s, int64_t nnz, const int32_t* d_i
       keep(tr.recv(sh.recv_w + so, sizeof(float) * hc[o], (int)o, s));
   }
   keep(tr.end(s));
+  //  as on the fixed path: a failed exchange leaves this rank out of step with its peers, so
+  // every later exchange on the shard fails at once (include/rmx.h)
+  if (err != RMX_OK) sh.failed = true;
   return err;
 }
 
@@ -1596,6 +1618,18 @@ extern "C" int64_t rmx_owner_hash(uint64_t key, int64_t num_rows, int nranks, in
 }
 
 extern "C" int64_t rmx_shard_overflow_rounds(const rmx_shard* sh) { return sh ? sh->rounds2 : -1; }
+
+extern "C" int rmx_shard_set_batch_hint(rmx_shard* sh, int64_t nnz) {
+  if (!sh || nnz < 0) {
+    set_error("rmx_shard_set_batch_hint: NULL shard or negative nnz");
+    return RMX_E_INVALID;
+  }
+  std::lock_guard<std::mutex> lk(sh->mu);
+  // the first fixed exchange's bucket capacity (later ones take it from the previous exchange's summary);
+  // every rank passes the same value, so the message sizes pair up
+  sh->cap_next = cap_of(*sh, nnz);
+  return RMX_OK;
+}
 
 extern "C" int rmx_shard_set_dedupe(rmx_shard* sh, int on) {
   if (!sh) {

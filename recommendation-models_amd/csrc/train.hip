@@ -1369,6 +1369,34 @@ bool wgrad_z_ok() { return f32_split_enabled() && tuning_get("wgrad_s3", 2) != 0
 
 // bias (nullable): also bias[n] = sum_b A[b][n] when the kernel can fuse it (the 208 x 208 tile); *bias_done
 // says whether it did (else the caller runs colsum)
+
+// The 208 x 208 dW's slice count S (one block per CU): the multiple of 8 with the fewest rounds x chunks per
+// block.  With smodel (knob "wgrad_smodel", default 1) the S partial planes the kernel writes and
+// slice_reduce reads back are priced too (~8 B per output per slice at ~4 TB/s, against ~3.8 us per round of
+// 32-row chunks): DeepFM training's layer-1 dW (624 x 400) took S = 128 (3 rounds x 16 chunks) and paid 33 us
+// of slice reduction for it; without smodel rounds x chunks alone.  The two constants were measured on one
+// MI355X and are fixed in the source, so S -- and with it the dW's fp32 summation order over the slices -- is
+// a pure function of (rows, N, K, CU count): the same on every 256-CU MI355X, different on a part with
+// another CU count (pinned for the bench shapes by tests/test_abi.py through
+// rmx_debug_wgrad_slices).
+int wgrad_sq_slices(int64_t rows, int N, int K, int tiles, int ncu, bool smodel) {
+  ncu = std::max(ncu, 1);
+  int S = 8;
+  double best = -1.0;
+  for (int s8 = 8; s8 <= 512; s8 += 8) {
+    const int64_t chunks = round_up((rows + s8 - 1) / s8, kWgR) / kWgR;
+    const int64_t rounds = ((int64_t)tiles * s8 + ncu - 1) / ncu;
+    const double cost = smodel ? 3.8 * (double)(rounds * chunks) + (double)s8 * N * K * 8.0 / 4.0e6
+                               : (double)(rounds * chunks);
+    if (best < 0 || cost < best) {
+      best = cost;
+      S = s8;
+    }
+    if (chunks <= 1) break;
+  }
+  return S;
+}
+
 int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, int lda, const float* X, int ldx,
           float* out, bool accum, const WgZ* zg = nullptr, float* bias = nullptr, bool* bias_done = nullptr) {
   if (bias_done) *bias_done = false;
@@ -1407,28 +1435,10 @@ int wgrad(TrainState& T, hipStream_t s, int rows, int N, int K, const float* A, 
   int S = std::max((rows + 1023) / 1024, std::min((1024 + tiles - 1) / tiles, std::max(1, rows / 64)));
   S = round_up(std::min(S, 512), 8);
   if (sq) {
-    // one block per CU: the S (a multiple of 8) with the fewest rounds x chunks per block
     int ncu = 0, dev = 0;
     RMX_HIP(hipGetDevice(&dev));
     RMX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    ncu = std::max(ncu, 1);
-    // knob "wgrad_smodel": 1 (default) also prices the S partial planes the kernel writes and slice_reduce reads
-    // back (~8 B per output per slice at ~4 TB/s, against ~3.8 us per round of 32-row chunks): DeepFM training's
-    // layer-1 dW (624 x 400) took S = 128 (3 rounds x 16 chunks) and paid 33 us of slice reduction for it;
-    // 0: rounds x chunks alone
-    const bool smodel = tuning_get("wgrad_smodel", 1) != 0;
-    double best = -1.0;
-    for (int s8 = 8; s8 <= 512; s8 += 8) {
-      const int64_t chunks = round_up((rows + s8 - 1) / s8, kWgR) / kWgR;
-      const int64_t rounds = ((int64_t)tiles * s8 + ncu - 1) / ncu;
-      const double cost = smodel ? 3.8 * (double)(rounds * chunks) + (double)s8 * N * K * 8.0 / 4.0e6
-                                 : (double)(rounds * chunks);
-      if (best < 0 || cost < best) {
-        best = cost;
-        S = s8;
-      }
-      if (chunks <= 1) break;
-    }
+    S = wgrad_sq_slices(rows, N, K, tiles, ncu, tuning_get("wgrad_smodel", 1) != 0);
   }
   const int rps = round_up((rows + S - 1) / S, var ? kWgR : 16);
   const bool fuse_bias = sq && bias && tuning_get("wgrad_bias", 1) != 0;
@@ -2118,3 +2128,12 @@ int model_train(rmx_model& m, hipStream_t s, const FwdInputs& in, const TrainOut
 }
 
 }  // namespace rmx
+
+extern "C" int rmx_debug_wgrad_slices(int64_t rows, int N, int K, int ncu) {
+  if (rows <= 0 || N <= 0 || K <= 0 || ncu <= 0) {
+    rmx::set_error("rmx_debug_wgrad_slices: rows, N, K and ncu must be positive");
+    return RMX_E_INVALID;
+  }
+  const int tiles = ((N + rmx::kSqT - 1) / rmx::kSqT) * ((K + rmx::kSqT - 1) / rmx::kSqT);
+  return rmx::wgrad_sq_slices(rows, N, K, tiles, ncu, rmx::tuning_get("wgrad_smodel", 1) != 0);
+}

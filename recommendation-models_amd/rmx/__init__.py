@@ -18,12 +18,14 @@ from . import _lib
 from ._lib import (IllegalArgumentError, MatsError, RmxError, ShapeError, LAYOUT_K_MAJOR,  # noqa: F401
                    LAYOUT_ROW_MAJOR, DTYPE_F32, DTYPE_BF16, FORMAT_LIBSVM, FORMAT_LIBFFM, check, ptr)
 
+import atexit
 import ctypes
 import threading
+import weakref
 
 __all__ = ["RecModelType", "CooLongFloatMatrix", "RecModel", "LR", "DeepFM", "XDeepFM", "DCN", "PNN", "DNN",
            "Context", "DeviceArray", "EmbeddingTable", "ShardedTable", "ExchangeGroup", "comm_unique_id", "SampleParser", "RmxError", "IllegalArgumentError",
-           "ShapeError", "MatsError", "default_context", "set_device"]
+           "ShapeError", "MatsError", "default_context", "set_device", "shutdown"]
 
 MODEL_LR, MODEL_DEEPFM, MODEL_XDEEPFM, MODEL_DCN, MODEL_PNN, MODEL_DNN = range(6)
 
@@ -68,6 +70,46 @@ def get_tuning(key, default=0):
     return int(_lib.lib.rmx_get_tuning(key.encode(), int(default)))
 
 
+# ------------------------------------------------------------- teardown ----
+# Every handle-owning object registers here.  shutdown() (an atexit hook) destroys the live ones in
+# dependency order -- sharded / plain tables, models, device buffers, exchange groups, then contexts --
+# while the interpreter, librmx and the HIP runtime are all still up.  Left to __del__, they would be
+# freed during interpreter teardown, possibly after the HIP runtime's (or a profiler's) own exit
+# handlers (an exit-time SIGSEGV under rocprofv3).
+_LIVE_ORDER = ("shard", "table", "model", "array", "group", "ctx")
+_live = {k: weakref.WeakSet() for k in _LIVE_ORDER}
+_shut = False
+
+
+def _track(kind, obj):
+    _live[kind].add(obj)
+
+
+def shutdown():
+    """Synchronise every live Context, then destroy every live librmx object (idempotent; runs at
+    interpreter exit).  Objects destroyed here are closed: using them afterwards raises."""
+    global _shut, _default_ctx
+    if _shut:
+        return
+    _shut = True
+    for c in list(_live["ctx"]):
+        try:
+            if c.handle:
+                c.sync()
+        except Exception:
+            pass
+    for kind in _LIVE_ORDER:
+        for o in list(_live[kind]):
+            try:
+                o.close()
+            except Exception:
+                pass
+    _default_ctx = None
+
+
+atexit.register(shutdown)
+
+
 # ----------------------------------------------------------------- device ----
 class Context:
     """One GPU + one HIP stream (rmx_ctx)."""
@@ -77,6 +119,7 @@ class Context:
         check(_lib.lib.rmx_ctx_create(int(device), ctypes.byref(h)))
         self.handle = h
         self.device = int(device)
+        _track("ctx", self)
 
     @property
     def stream(self):
@@ -127,6 +170,7 @@ class DeviceArray:
         p = ctypes.c_void_p()
         check(_lib.lib.rmx_malloc(ctx.handle, self.nbytes, ctypes.byref(p)))
         self.ptr = p
+        _track("array", self)
 
     def view(self, offset, n):
         """Non-owning view of elements [offset, offset + n)."""
@@ -162,8 +206,11 @@ class DeviceArray:
             self.ptr = None
             return
         if self.ptr:
-            _lib.lib.rmx_free(self.ctx.handle, self.ptr)
+            if self.ctx.handle:  # (a context destroyed first has freed its buffers' stream already)
+                _lib.lib.rmx_free(self.ctx.handle, self.ptr)
             self.ptr = None
+
+    close = free
 
     def __del__(self):
         try:
@@ -188,6 +235,7 @@ class EmbeddingTable:
         self.rows = int(num_rows)
         self.k = int(embedding_dim)
         self.dtype = int(dtype)
+        _track("table", self)
 
     def upload(self, weights=None, embedding=None, layout=LAYOUT_ROW_MAJOR):
         """layout LAYOUT_K_MAJOR: embedding is the reference PS layout, k x V."""
@@ -240,6 +288,7 @@ class ExchangeGroup:
         check(_lib.lib.rmx_group_create(int(nranks), ctypes.byref(h)))
         self.handle = h
         self.nranks = int(nranks)
+        _track("group", self)
 
     def close(self):
         if self.handle:
@@ -282,6 +331,7 @@ class ShardedTable:
         self.k = int(embedding_dim)
         self.nranks = int(nranks)
         self.rank = int(rank)
+        _track("shard", self)
 
     def fill_synthetic(self, seed):
         check(_lib.lib.rmx_shard_fill_synthetic(self.handle, int(seed)))
@@ -308,6 +358,11 @@ class ShardedTable:
         else:
             raise ValueError('set_dedupe takes True, False or "auto", got %r' % (on,))
         check(_lib.lib.rmx_shard_set_dedupe(self.handle, mode))
+
+    def set_batch_hint(self, nnz):
+        """Seed the first exchange's bucket capacity from the ids per batch (every rank the same nnz, before
+        the first exchange; rmx_shard_set_batch_hint), so it does not take the counted overflow round."""
+        check(_lib.lib.rmx_shard_set_batch_hint(self.handle, int(nnz)))
 
     def last_sent(self):
         """Ids this rank sent to owners in its last exchange."""
@@ -398,6 +453,7 @@ class RecModel:
         self._ctx = ctx
         self._dev = None
         self._dev_mats_loaded = False
+        _track("model", self)
 
     def _create(self, ctx):
         inputDim, nFields, k, fc, cin, depth = self._args
@@ -409,6 +465,8 @@ class RecModel:
         return h
 
     def _device(self):
+        if self._meta is None:
+            raise RmxError(_lib.RMX_E_INVALID, "model is closed")
         if self._dev is None:
             if self._ctx is None:
                 self._ctx = default_context()
@@ -420,12 +478,18 @@ class RecModel:
         self._device()
         return self._ctx
 
+    def close(self):
+        """Destroy the device and metadata handles (rmx_model_destroy); the model is unusable after."""
+        d, self._dev = self._dev, None
+        m, self._meta = self._meta, None
+        if d:
+            _lib.lib.rmx_model_destroy(d)
+        if m:
+            _lib.lib.rmx_model_destroy(m)
+
     def __del__(self):
         try:
-            if self._dev:
-                _lib.lib.rmx_model_destroy(self._dev)
-            if self._meta:
-                _lib.lib.rmx_model_destroy(self._meta)
+            self.close()
         except Exception:
             pass
 

@@ -103,6 +103,8 @@ SIGNATURES = [
     ("rmx_shard_owner_of", c_i64, [c_vp, c_i64]),
     ("rmx_owner_hash", c_i64, [c_u64, c_i64, c_int, c_i64, c_vp]),
     ("rmx_shard_set_dedupe", c_int, [c_vp, c_int]),
+    ("rmx_shard_set_batch_hint", c_int, [c_vp, ctypes.c_int64]),
+    ("rmx_debug_wgrad_slices", c_int, [ctypes.c_int64, c_int, c_int, c_int]),
     ("rmx_shard_last_sent", c_i64, [c_vp]),
     ("rmx_shard_overflow_rounds", c_i64, [c_vp]),
     ("rmx_predict_ids", c_int, [c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp]),

@@ -119,3 +119,18 @@ def test_sample_parser_libsvm_libffm():
     assert coo.getValues().tolist() == [1.0, 0.5, 1.0]
     coo, fields, y = rmx.SampleParser.parse(["1 0:5:1 2:9:1"], rmx.RecModelType.BIAS_WEIGHT_EMBEDDING_MATS_FIELD)
     assert fields.tolist() == [0, 2] and coo.getColIndices().tolist() == [4, 8]
+
+
+def test_wgrad_slice_count_pinned_for_the_bench_shapes():
+    """the 208 x 208 dW's slice count S sets the fp32 summation order of the weight gradient.
+    It is a pure function of (rows, N, K, CU count) with constants fixed in the source, pinned here for
+    DeepFM training at B = 65,536 on the 256-CU MI355X (layer 1 624 x 400: S = 40; the
+    400 x 400 layers: S = 64); another CU count may pick another S (documented in include/rmx.h)."""
+    from rmx import _lib
+    S = _lib.lib.rmx_debug_wgrad_slices
+    assert S(65536, 400, 624, 256) == 40
+    assert S(65536, 624, 400, 256) == 40
+    assert S(65536, 400, 400, 256) == 64
+    assert S(32768, 400, 400, 256) == 64
+    assert S(65536, 400, 400, 304) % 8 == 0
+    assert S(0, 400, 400, 256) == _lib.RMX_E_INVALID

@@ -101,6 +101,23 @@ def test_job_status_companion_and_cpu_records():
     assert bench.job_status(None, None, {"parity_check": {"ok": True}}, {"value": 1.0}) == 0
 
 
+def test_record_status_error_is_not_a_parity_miss():
+    """an encoder / L-A sub-record that raised (e.g. out of memory at V = 100M) exits with its
+    own status and reason, not as a parity miss; a failed check is still a parity miss."""
+    import bench
+    enc_ok = {"note": "x", "V1M": {"parity_check": {"bitwise_equal": True}}}
+    la_ok = {"note": "x", "B100": {"parity_check": {"ok": True}}}
+    assert bench.record_status(enc_ok, la_ok) == 0
+    assert bench.record_status(None, None) == 0
+    assert bench.record_status({"V100M": {"error": "RmxError: out of device memory"}}, la_ok) == \
+        bench.STATUS_RECORD_ERROR
+    assert bench.record_status(enc_ok, {"B4096": {"error": "x"}}) == bench.STATUS_RECORD_ERROR
+    assert bench.record_status({"V1M": {"parity_check": {"bitwise_equal": False}}}, la_ok) == \
+        bench.STATUS_PARITY_MISS
+    assert bench.record_status(enc_ok, {"B100": {"parity_check": {"ok": False}}}) == bench.STATUS_PARITY_MISS
+    assert bench.STATUS_REASON[bench.STATUS_RECORD_ERROR] != bench.STATUS_REASON[bench.STATUS_PARITY_MISS]
+
+
 def test_bench_cli_launcher_exit_status(tmp_path):
     """The real entry point: `bench.py --gpus 2` with no WORLD_SIZE becomes the launcher; its ranks
     fail here (no GPU / librmx device), and the launcher exits non-zero instead of hanging."""

@@ -898,3 +898,96 @@ def test_out_of_range_ids_read_zero_rows(N, dedupe):
         p = oc.forward(om, n, np.repeat(np.arange(n, dtype=np.int64), F), np.array([0.01], np.float32), w, e,
                        oc.init_mats(om, SEED_MATS), 1)
         assert np.abs(got[0][bad_rows] - p).max() <= 1e-5, r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [2, 4])
+def test_group_batch_hint_first_exchange_needs_no_overflow_round(N):
+    """rmx_shard_set_batch_hint: with the same hint on every rank, the first fixed
+    exchange of uniform ids fits its buckets -- no overflow round -- and stays bitwise the replicated
+    forward; without it the first exchange takes the counted round."""
+    import rmx
+    V, B = 100_003, 1000
+    for hint in (True, False):
+        g = rmx.ExchangeGroup(N)
+
+        def rank(r):
+            ctx = rmx.Context(0)
+            sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+            sh.set_dedupe(False)
+            if hint:
+                sh.set_batch_hint(B * F)
+            sh.fill_synthetic(SEED_TAB)
+            ids = rmx.DeviceArray(ctx, B * F, np.int32)
+            rmx.gen_ids(ctx, SEED_IDS, 5 + r * B, B, F, V, ids)
+            m = _models_v(V)["deepfm"]()
+            m.setMats(m.initMats(SEED_MATS))
+            m.setBias(0.01)
+            got = rmx.DeviceArray(ctx, B, np.float32)
+            m.forward_ids_sharded(sh, B, ids, got, ctx.stream)
+            ctx.sync()
+            out = (got.numpy(), ids.numpy(), sh.overflow_rounds())
+            sh.close()
+            return out
+
+        outs = _run_ranks(N, rank)
+        ctx = rmx.default_context()
+        table = rmx.EmbeddingTable(ctx, V, K)
+        table.fill_synthetic(SEED_TAB)
+        m = _models_v(V)["deepfm"]()
+        m.setMats(m.initMats(SEED_MATS))
+        m.setBias(0.01)
+        for r, (got, h_ids, rounds) in enumerate(outs):
+            assert rounds == (0 if hint else 1), (hint, r, rounds)
+            ids = rmx.DeviceArray(ctx, B * F, np.int32)
+            ids.upload(h_ids)
+            ref = rmx.DeviceArray(ctx, B, np.float32)
+            m.forward_ids(table, B, ids, ref)
+            ctx.sync()
+            assert np.array_equal(got, ref.numpy()), (hint, r)
+        g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixed", [1, 0])
+def test_group_failed_exchange_fails_every_later_exchange(fixed):
+    """include/rmx.h: an exchange that fails on a rank at nranks > 1 fails every later exchange on the shard
+    at once, on the fixed path and on the counted one (the counted path did not mark the shard).
+    Rank 1's route fails by the test hook; rank 0 sees its peer post nothing."""
+    import rmx
+    N, V, B = 2, 50_021, 256
+    g = rmx.ExchangeGroup(N)
+    rmx.set_tuning("shard_fixed", fixed)
+    rmx.set_tuning("shard_debug_fail_rank", 2)  # rank 1
+
+    def rank(r):
+        ctx = rmx.Context(0)
+        sh = rmx.ShardedTable(ctx, V, K, N, r, group=g)
+        sh.set_dedupe(False)
+        sh.fill_synthetic(SEED_TAB)
+        ids = rmx.DeviceArray(ctx, B * F, np.int32)
+        rmx.gen_ids(ctx, SEED_IDS, r * B, B, F, V, ids)
+        w = rmx.DeviceArray(ctx, B * F, np.float32)
+        e = rmx.DeviceArray(ctx, B * F * K, np.float32)
+        errs = []
+        for _ in range(2):
+            try:
+                sh.gather(ids, B * F, w, e, ctx.stream)
+                ctx.sync()
+                errs.append(None)
+            except rmx.RmxError as ex:
+                errs.append(str(ex))
+        ctx.sync()
+        sh.close()
+        return errs
+
+    try:
+        res = _run_ranks(N, rank, timeout=200)
+    finally:
+        rmx.set_tuning("shard_debug_fail_rank", None)
+        rmx.set_tuning("shard_fixed", None)
+        g.close()
+    for r, errs in enumerate(res):
+        assert errs[0] is not None, (r, errs)
+        assert errs[1] is not None and "earlier exchange failed" in errs[1], (r, errs)
+    assert "injected" in res[1][0]

@@ -28,6 +28,8 @@ run() {  # run <name> <seconds> <cmd...>; stop on anything but success / plain t
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    t:*) files=${s#t:}; files=${files//,/ }   # t:tests/a.py,tests/b.py
+         run pytest_sel 900 python -u -m pytest $files -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py ;;
     benchd) run bench_driver 400 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
@@ -63,6 +65,40 @@ for s in $STEPS; do
     settle) for ms in 0 100 400 1000; do
               run settle_$ms 200 python bench.py --steps 20 --warmup 5 --no-companion --no-cpu-baseline --settle-ms $ms
             done ;;
+    pmcenc:*) spec=${s#pmcenc:}; V=${spec%%:*}; tab=${spec#*:}   # pmcenc:<vocab>:<row|line>
+         d="$OUT/pmc_enc_${V}_$tab"
+         for pass in fetch write tcc sq grbm; do
+           case $pass in
+             fetch) ctr="FETCH_SIZE" ;; write) ctr="WRITE_SIZE" ;; tcc) ctr="TCC_HIT_sum TCC_MISS_sum" ;;
+             sq) ctr="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM SQ_INSTS_SALU" ;;
+             grbm) ctr="GRBM_GUI_ACTIVE GRBM_COUNT" ;;
+           esac
+           run pmcenc_${V}_${tab}_$pass 300 rocprofv3 --pmc $ctr --output-format csv -d "$d/$pass" -o $pass -- \
+              python3 bench.py --workload encoder --vocab $V --enc-table $tab --steps 20 --warmup 3 || exit $?
+         done ;;
+    pmcwl:*) wl=${s#pmcwl:}   # fetch / write / sq / grbm passes of one bench workload's forward
+         d="$OUT/pmc_$wl"
+         for pass in fetch write tcc sq sq2 grbm; do
+           case $pass in
+             fetch) ctr="FETCH_SIZE" ;; write) ctr="WRITE_SIZE" ;; tcc) ctr="TCC_HIT_sum TCC_MISS_sum" ;;
+             sq) ctr="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU" ;;
+             sq2) ctr="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM" ;;
+             grbm) ctr="GRBM_GUI_ACTIVE GRBM_COUNT" ;;
+           esac
+           run pmcwl_${wl}_$pass 400 rocprofv3 --pmc $ctr --output-format csv -d "$d/$pass" -o $pass -- \
+              python3 bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline --no-companion --no-encoder-record --no-la-record --settle-ms 0 || exit $?
+         done ;;
+    profdrv) run profdrv 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profdrv" -o deepfm -- \
+            python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    abenc) for round in 1 2; do   # encoder line table: encoder_line8_kernel (1, 2) vs encoder_k16v2_kernel (0)
+             for V in 100000000 1000000; do
+               for l8 in 0 1 2; do
+                 run abenc_${V}_${l8}_$round 200 python bench.py --workload encoder --vocab $V --enc-table line --steps 100 --warmup 10 --set enc_line8=$l8 || exit $?
+                 python3 -c "import json,sys; d=json.loads([l for l in open('$OUT/abenc_${V}_${l8}_$round.log') if l.startswith('{')][-1]); e=d['encoder']['line_table']; print('V=$V enc_line8=$l8 round $round', e['avg_ms'], 'ms', e['line_frac'], d['encoder']['parity_check']['bitwise_equal'])" | tee -a $OUT/abenc.txt
+               done
+             done
+           done ;;
+    fdiag) run fdiag 300 env RMX_LIB=vbuild/fdiag/librmx.so python tools/diag_fused.py ;;
     list) run list 120 rocprofv3 -L ;;
     ablines) run ab_lines1 300 python bench.py --no-companion --no-cpu-baseline --steps 200 &&
          run ab_lines0 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 &&

@@ -42,8 +42,9 @@ def load(d):
         for r in csv.DictReader(open(f)):
             k = short(r["Kernel_Name"])
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            if r["Counter_Name"] in ("GRBM_GUI_ACTIVE",):
-                dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))  # (once per counter row)
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                dur[k + "#grbm"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     stats = {}
     for f in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -66,7 +67,7 @@ def stage_of(kernel, workload=""):
             return "tower_layer1"
         return "tower_layer3" if epi == 1 else "tower_layer2"
     kernel = re.sub(r"^\(anonymous namespace\)::", "", kernel)
-    for pat, st in (("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
+    for pat, st in (("encoder_k16v2_kernel", "encoder"), ("encoder_line8_kernel", "encoder"), ("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
                     ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
                     ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
                     ("owner_gather", "shard_exchange"), ("own_rows_kernel", "shard_exchange"),
@@ -85,6 +86,7 @@ def main():
     ap.add_argument("--stages", nargs=2, metavar=("TRAFFIC_JSON", "WORKLOAD"),
                     help="merge per-stage HBM bytes per launch into TRAFFIC_JSON under WORKLOAD")
     ap.add_argument("--batch", type=int, default=0, help="rows per launch of the profiled run")
+    ap.add_argument("--source", default="", help="the committed summary file these counters are in (profiles/...)")
     a = ap.parse_args()
     vals, dur, stats = load(a.dir)
     out = {}
@@ -97,8 +99,10 @@ def main():
             e["hbm_bytes"] = 2 * v["FETCH_SIZE"] * 1024 + v["WRITE_SIZE"] * 1024
             e["fetch_bytes_x2"] = 2 * v["FETCH_SIZE"] * 1024
             e["write_bytes"] = v["WRITE_SIZE"] * 1024
-        if "GRBM_GUI_ACTIVE" in v and dur.get(k):
-            t = sum(dur[k]) / len(dur[k])
+        if dur.get(k):  # dispatch durations under the PMC passes (profiled: clocks run lower than live)
+            e["pmc_avg_ns"] = sum(dur[k]) / len(dur[k])
+        if "GRBM_GUI_ACTIVE" in v and dur.get(k + "#grbm"):
+            t = sum(dur[k + "#grbm"]) / len(dur[k + "#grbm"])
             e["clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8 / t
         if "SQ_VALU_MFMA_BUSY_CYCLES" in v and "SQ_BUSY_CYCLES" in v and v["SQ_BUSY_CYCLES"] > 0:
             e["mfma_busy_per_sq_busy"] = v["SQ_VALU_MFMA_BUSY_CYCLES"] / v["SQ_BUSY_CYCLES"]
@@ -128,6 +132,12 @@ def main():
             parts.append("mfma_busy %.3g" % c["SQ_VALU_MFMA_BUSY_CYCLES"])
         if "mfma_util" in e:
             parts.append("MFMA util %.1f %%" % (100 * e["mfma_util"]))
+        if c.get("SQ_INSTS_MFMA"):
+            parts.append("valu/mfma %.2f" % (c.get("SQ_INSTS_VALU", 0) / c["SQ_INSTS_MFMA"]))
+        if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+            parts.append("L2 hit %.1f %%" % (100 * c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])))
+        if "pmc_avg_ns" in e:
+            parts.append("pmc avg %.1f us" % (e["pmc_avg_ns"] / 1e3))
         print(" | ".join(parts))
     if a.json:
         os.makedirs(os.path.dirname(a.json) or ".", exist_ok=True)
@@ -143,6 +153,13 @@ def main():
                             "write_bytes": round(e["write_bytes"]), "kernel": k, "batch": a.batch}
                 if "mfma_util" in e:
                     st[name]["mfma_util"] = round(e["mfma_util"], 4)
+                if "pmc_avg_ns" in e:
+                    st[name]["avg_ns"] = round(e["pmc_avg_ns"], 1)
+                if "clock_ghz" in e:
+                    st[name]["clock_ghz"] = round(e["clock_ghz"], 3)
+                st[name]["counters"] = {c: round(x, 1) for c, x in sorted(e["counters"].items())}
+                if a.source:
+                    st[name]["source"] = a.source
         db[wl] = st
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         json.dump(db, open(path, "w"), indent=1, sort_keys=True)
