@@ -482,8 +482,6 @@ def run_encoder(args, rmx, ctx, steps, warmup, Vw, B=65536):
     bpe = F * 4 + F * 4 + F * K * 4 + 4
     rec = {"kernel": ("encoder_k16v2_kernel (enc_u %d)" % rmx.get_tuning("enc_u", 20)) if rmx.get_tuning("enc_u", 20)
            else "encoder_k16_kernel<1, float>", "batch": B, "vocab": Vw,
-           **({"kernel_line_table": "encoder_line8_kernel (enc_line8 %d: one whole-line load per id)"
-               % rmx.get_tuning("enc_line8", 1)} if rmx.get_tuning("enc_line8", 1) else {}),
            "algorithmic_bytes_per_example": bpe, "peak_gbs": PEAK_HBM_GBS}
     saved = rmx.get_tuning("table_lines", 0)
     layouts = {"row": (0,), "line": (1,)}.get(getattr(args, "enc_table", "both"), (0, 1))
@@ -842,20 +840,18 @@ def run(args, workload, rmx, ctx, rank, world, dist, steps, warmup, B=0):
     # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
     # (FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_summary.py --stages); null when not profiled
     roof["traffic"] = None
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        ent = json.load(open(tpath)).get(workload, {}).get("cin_layer" if dom.startswith("cin_layer") else dom)
-        if ent and ent.get("batch") == B:
-            roof["traffic"] = ent["hbm_bytes"]
-            roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"
-            if "mfma_util" in ent:  # measured matrix-pipe occupancy of the same kernel (profiled run)
-                roof["mfma_util_pmc"] = ent["mfma_util"]
-                summ = next((q for q in ("profiles/r05/pmc_%s_summary.txt" % workload,
-                                         "profiles/r04/pmc_%s_summary.txt" % workload,
-                                         "profiles/r03/pmc_%s_summary.txt" % workload)
-                             if os.path.exists(os.path.join(ROOT, q))), None)
-                roof["mfma_util_source"] = ("rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), "
-                                            "%s" % summ)
+    ent = _traffic(workload, "cin_layer" if dom.startswith("cin_layer") else dom, B)
+    if ent:
+        roof["traffic"] = ent["hbm_bytes"]
+        roof["traffic_source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE), %s" % ent.get(
+            "source", "")
+        roof["traffic_kernel"] = ent.get("kernel")
+        if "mfma_util" in ent:  # measured matrix-pipe occupancy of the same kernel (profiled run)
+            roof["mfma_util_pmc"] = ent["mfma_util"]
+            roof["mfma_util_source"] = ("rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), "
+                                        "%s" % ent.get("source", ""))
+            if "clock_ghz" in ent:
+                roof["pmc_clock_ghz"] = ent["clock_ghz"]
     roof["kernel"] = dom
     roof["algorithmic_per_launch"] = work
 

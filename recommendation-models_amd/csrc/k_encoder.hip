@@ -11,8 +11,6 @@
 // oracle/rmx_oracle.c.
 #include "rmx_internal.hpp"
 
-#include <type_traits>
-
 namespace rmx {
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -258,100 +256,6 @@ __global__ __launch_bounds__(256) void encoder_generic_kernel(int M, const int32
   if (MODE == 3) y[b] = y[b] + y2;
 }
 
-// Round 6: line tables ([V][32] fp32 rows [emb 16 | w | pad], knob table_lines; the sharded partition's rows).
-// encoder_k16v2_kernel reads a line-table id with two instructions -- the 64-B row (4 lanes x 16 B) and the
-// 4-B weight (wtab = table + 16) -- i.e. two requests to the same 128-B line, and at V = 100M it reached only
-// 0.73 of the random-line rate the row table reaches with two lines per id.  Here 8 lanes
-// own a sample and one float4 load per lane fetches the WHOLE line (lanes 0-3 the embedding, lane 4 the weight
-// in .x, lanes 5-7 the padding): one request per id.  The ids of a 40-field chunk are loaded once (lane c:
-// fields 8 i + c, coalesced) and shared with a swizzle broadcast inside the 8-lane group.  Lanes 0-3 keep
-// encoder_k16v2_kernel's per-lane FM sums and lane 4 its first-order sum, field order, contraction off: y is
-// bit-identical (tests/test_encoder_v2.py).  Modes 0 and 1, fp32, no training outputs.
-template <int J>
-__device__ __forceinline__ int oct_bcast(int v) {  // every lane of an 8-lane group takes the group's lane J
-  return __builtin_amdgcn_ds_swizzle(v, 0x18 | (J << 5));  // bit mode: ((lane & 0x18) | J) within 32 lanes
-}
-__device__ __forceinline__ int oct_bcast(int v, int j) {  // (j is a constant after unrolling)
-  switch (j) {
-    case 0: return oct_bcast<0>(v);
-    case 1: return oct_bcast<1>(v);
-    case 2: return oct_bcast<2>(v);
-    case 3: return oct_bcast<3>(v);
-    case 4: return oct_bcast<4>(v);
-    case 5: return oct_bcast<5>(v);
-    case 6: return oct_bcast<6>(v);
-    default: return oct_bcast<7>(v);
-  }
-}
-
-template <int MODE, int U>
-__global__ __launch_bounds__(256) void encoder_line8_kernel(int M, const int32_t* __restrict__ ids,
-                                                            const float* __restrict__ lines, int F,
-                                                            float* __restrict__ y) {
-#pragma clang fp contract(off)
-  constexpr int NI = 5, CH = 8 * NI;  // ids per lane / fields per chunk
-  constexpr int NB = (CH + U - 1) / U;
-  constexpr bool FM = MODE == 1;
-  const int lane = threadIdx.x & 63;
-  const int s = lane >> 3, c = lane & 7;
-  const int b = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + s;
-  const bool valid = b < M;
-  const int32_t* irow = ids + (int64_t)(valid ? b : 0) * F;
-  float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), q4 = s4;
-  float y1 = 0.f;
-  const float* zero = g_enc_zero16 + 4 * (c & 3);  // a field past F reads zeros (x + 0 = x)
-  for (int f0 = 0; f0 < F; f0 += CH) {
-    int idv[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int f = f0 + 8 * i + c;
-      idv[i] = irow[f < F ? f : F - 1];
-    }
-#pragma unroll
-    for (int h = 0; h < NB; ++h) {
-      if (f0 + h * U >= F) break;  // (wave-uniform, per batch)
-      float4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int uu = h * U + u;
-        if (uu >= CH) break;  // (compile time)
-        const int id = oct_bcast(idv[uu >> 3], uu & 7);
-        const float* src = f0 + uu < F ? lines + ((int64_t)id << 5) + 4 * c : zero;
-        v[u] = *reinterpret_cast<const float4*>(src);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (h * U + u >= CH) break;
-        if (FM) {  // (meaningful on lanes 0-3: the embedding's float4s)
-          s4.x += v[u].x; s4.y += v[u].y; s4.z += v[u].z; s4.w += v[u].w;
-          q4.x += v[u].x * v[u].x; q4.y += v[u].y * v[u].y;
-          q4.z += v[u].z * v[u].z; q4.w += v[u].w * v[u].w;
-        }
-        y1 += v[u].x;  // (meaningful on lane 4: the weight)
-      }
-    }
-  }
-  float y2 = 0.f;
-  if (FM) {  // encoder_k16_kernel's reduction over lanes 0-3, the same order
-    float d0 = s4.x * s4.x - q4.x, d1 = s4.y * s4.y - q4.y;
-    float d2 = s4.z * s4.z - q4.z, d3 = s4.w * s4.w - q4.w;
-    float acc = 0.f;
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int src = (lane & ~7) | cc;
-      acc += __shfl(d0, src);
-      acc += __shfl(d1, src);
-      acc += __shfl(d2, src);
-      acc += __shfl(d3, src);
-    }
-    y2 = 0.5f * (acc / 16.0f);
-  }
-  const float w1 = __shfl(y1, (lane & ~7) | 4);
-  if (!valid || c != 0) return;
-  if (MODE == 0) y[b] = w1;
-  if (MODE == 1) y[b] = w1 + y2;
-}
-
 template <class T>
 static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids, const T* table, const T* wtab, int F,
                              int k, float* y, float bt, float* prob, int ld, int wld, float* xo, float* so) {
@@ -359,21 +263,6 @@ static void encoder_launch_t(hipStream_t s, int mode, int M, const int32_t* ids,
   const int eu = tuning_get("enc_u", 20);
   // (x / FM sums for the training forward: knob "enc_v2_x", default 1)
   const bool xs = xo || so;
-  // knob "enc_line8" (round 6, default 1): fp32 line tables on encoder_line8_kernel (one request per id)
-  if constexpr (std::is_same<T, float>::value) {
-    const int l8 = tuning_get("enc_line8", 1);
-    if (l8 != 0 && k == 16 && ids && !xs && (mode == 0 || mode == 1) && ld == 32 && wld == 32 && wtab == table + 16) {
-      dim3 grid((M + 31) / 32);
-      if (l8 == 2) {
-        if (mode == 0) hipLaunchKernelGGL((encoder_line8_kernel<0, 40>), grid, dim3(256), 0, s, M, ids, table, F, y);
-        else hipLaunchKernelGGL((encoder_line8_kernel<1, 40>), grid, dim3(256), 0, s, M, ids, table, F, y);
-      } else {
-        if (mode == 0) hipLaunchKernelGGL((encoder_line8_kernel<0, 20>), grid, dim3(256), 0, s, M, ids, table, F, y);
-        else hipLaunchKernelGGL((encoder_line8_kernel<1, 20>), grid, dim3(256), 0, s, M, ids, table, F, y);
-      }
-      return;
-    }
-  }
   if ((k == 16 || mode == 2) && ids && mode != 3 && (eu == 13 || eu == 20) &&
       (!xs || (mode != 2 && eu == 20 && tuning_get("enc_v2_x", 1) != 0))) {
     dim3 grid((M + 63) / 64);

@@ -28,8 +28,8 @@
 // Vector-memory instructions per unit: 9 in a layer-1 half-0 unit (1 id + 2 row + 1 weight DMA + 5 planes),
 // 5 in every other unit -- every wait is a compile-time vmcnt.
 //
-// LDS: the ring (3 x 39,936) + per wave [2 A slots | 4 id slots | 2 weight slots] (8 x 4,864) + b3 | wo
-// (3,328) = 162,048 B.  b1 and b2 are read once per row block with scalar loads (no LDS left for them).
+// LDS: the ring (3 x 39,936) + per wave [2 A slots | 4 id slots | 2 weight slots] (8 x 4,864) + b3 | wo | b1
+// (4,992) = 163,712 B.  b2 is DMA'd per row block into each wave's A slot that layer 1 no longer needs.
 //
 // Parity: each layer's products and K order are the head's / tail's, so h1, h2 and the logit's summands
 // are the same fp32 values; the FM + first order are encoder_k16_kernel<1>'s arithmetic (bit-identical y1 +
@@ -47,9 +47,10 @@ constexpr int kFId = 4 * 128;                    // per wave: 4 slots x [2 field
 constexpr int kFWr = 2 * 128;                    // per wave: 2 slots x [2 fields][16] first-order weights
 constexpr int kFWave = kFA + kFId + kFWr;
 constexpr int kFKS2 = 13;                        // K steps of layers 2 and 3 (Kpad 416)
-constexpr int kFPrm = 2 * kQN;                   // b3 | wo in LDS
+constexpr int kFPrm = 3 * kQN;                   // b3 | wo | b1 in LDS
 constexpr size_t kFLds = (size_t)kQSlots * kQUnit + (size_t)kQW * kFWave + sizeof(float) * kFPrm;
 static_assert(kFLds <= 160 * 1024, "LDS budget");
+static_assert(sizeof(float) * kQN <= 2048, "b2 fits a wave's free A slot (f_b2_dma)");
 
 // weight-fragment prefetch depth (column tiles) of the layer-2 units (2 measured the same, 0.3101-0.3102 vs
 // 0.3093-0.3101 ms) and the layer-3 units (2 spilled 7 registers)
@@ -60,12 +61,14 @@ static_assert(kFLds <= 160 * 1024, "LDS budget");
 #define RMX_FUSED_PF3 1
 #endif
 
-// Diagnostic builds only (tools/diag_fused.py; never set in librmx.so): s_memtime stamps of block 0's waves
-// at the layer boundaries of its first row blocks, s_memrealtime at the kernel's start and end (the clock)
+// Diagnostic builds only (tools/diag_fused.py; never set in librmx.so): bit 1 s_memtime stamps of block 0's
+// waves at the layer boundaries of its first row blocks, s_memrealtime at the kernel's start and end (the
+// clock); timing probes with wrong results: bit 2 layer 1's row gathers from a fixed (cached) address, bit 4
+// no row / weight gathers in layer 1 at all
 #ifndef RMX_FUSED_DIAG
 #define RMX_FUSED_DIAG 0
 #endif
-#if RMX_FUSED_DIAG
+#if RMX_FUSED_DIAG & 1
 constexpr int kFDiagIt = 4, kFDiagPh = 6;
 __device__ unsigned long long g_fused_t[kQW][kFDiagIt][kFDiagPh];  // [wave][row block][phase]
 __device__ unsigned long long g_fused_clk[kQW][4];                   // memtime / memrealtime at start, end
@@ -189,14 +192,52 @@ __device__ __forceinline__ void f_row_dma(const FusedS3Args& p, char* wl, int s,
   }
 }
 
-// b[16 t + 4 g .. + 3] through scalar loads (the address is wave-uniform; no LDS is left for b1 / b2):
-// one s_load of the tile's 16 values, each lane group takes its four
-// (b is made opaque per row block by the caller: hoisted out of the loop, the 25 x 16 values spilled)
-__device__ __forceinline__ f32x4 f_sbias(const float* b, int t, int g) {
-  typedef __attribute__((address_space(4))) const f32x4 cf32x4;
-  cf32x4* bt = reinterpret_cast<cf32x4*>(reinterpret_cast<uintptr_t>(b) + (uintptr_t)(64 * t));
-  const f32x4 v0 = bt[0], v1 = bt[1], v2 = bt[2], v3 = bt[3];
-  return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+// The same DMAs from ids already in registers (round 6): step s + 1's three ids (the rows of fields 2c, 2c + 1
+// and the weight) are read from their id slot at the start of step s's half-0 unit, beside prep's reads.
+// Read at the DMA (f_row_dma inside the MFMA stream), each id needed an s_waitcnt lgkmcnt(0) that also drained
+// the B fragments prefetched for the next tiles -- three times per half-0 unit.
+struct FRowIds {
+  int id0, id1, idw;
+};
+__device__ __forceinline__ FRowIds f_row_ids(char* wl, int s, int lane) {
+  const int* ids = reinterpret_cast<const int*>(wl + kFA + (s & 3) * 128);
+  int r = lane >> 2, lw = lane & 31;
+  asm volatile("" : "+v"(r), "+v"(lw));
+  return FRowIds{ids[r], ids[16 + r], ids[lw]};
+}
+__device__ __forceinline__ void f_row_dma_ids(const FusedS3Args& p, char* wl, int s, int lane, const FRowIds& q,
+                                              int part) {
+#if RMX_FUSED_DIAG & 4  // timing probe: no row / weight gathers in layer 1 (results wrong)
+  return;
+#endif
+  int g = swz_slot(lane >> 2, lane & 3);
+  asm volatile("" : "+v"(g));
+  const float* zero16 = g_rmx_zero16;
+  char* a = wl + (s & 1) * 2048;
+#if RMX_FUSED_DIAG & 2  // timing probe: every gather reads the lane's own row of the table's first 16 (cached)
+  if (part == 0) lds_dma<16>(p.table + ((int64_t)(lane >> 2) << p.gsh) + 4 * g, a);
+  if (part == 1) lds_dma<16>(p.table + ((int64_t)(lane >> 2) << p.gsh) + 4 * g, a + 1024);
+#else
+  if (part == 0) lds_dma<16>(q.id0 >= 0 ? p.table + ((int64_t)q.id0 << p.gsh) + 4 * g : zero16, a);
+  if (part == 1) lds_dma<16>(q.id1 >= 0 ? p.table + ((int64_t)q.id1 << p.gsh) + 4 * g : zero16, a + 1024);
+#endif
+  if (part == 2 && lane < 32)
+    lds_dma<4>(q.idw >= 0 ? p.wtab + ((int64_t)q.idw << p.wsh) : zero16, wl + kFA + kFId + (s & 1) * 128);
+}
+
+// The biases of layers 1 and 2 come from LDS (round 6).  Read with scalar loads (round 5), the compiler
+// reused one SGPR quad for all 25 tiles, so every s_load waited out its own round trip before the next:
+// s_memtime stamps (tools/diag_fused.py) put the layer-1 epilogue at 8-14 k cycles per row block and the
+// end of layer 2 likewise, ~6 % of the kernel.  b1 sits in the block's LDS beside b3 | wo (staged once per
+// launch); b2 has no room there, so each wave DMAs it into its own A slot that layer 1's last step freed
+// (slot (s - 1) & 1, untouched until the next row block's first rows land), during layer 2's first unit.
+__device__ __forceinline__ void f_b2_dma(const FusedS3Args& p, char* wl, int s, int lane) {
+  char* dst = wl + ((s - 1) & 1) * 2048;
+  const float* zero16 = g_rmx_zero16;
+  int l = lane;
+  asm volatile("" : "+v"(l));
+  lds_dma<16>(p.b2 + 4 * l, dst);                                  // bytes 0 .. 1023
+  lds_dma<16>(l < kQN / 4 - 64 ? p.b2 + 256 + 4 * l : zero16, dst + 1024);  // 1024 .. 1663, then zeros
 }
 
 // layer-3 half HF (column tiles 13 HF .. + 12; half 1 computes 12, tile 25 is padding): 13 units, one per
@@ -249,25 +290,27 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r16 = lane & 15;
   char* wl = fsmem + kQSlots * kQUnit + w * kFWave;  // this wave's rows / ids / weights
-  float* prm = reinterpret_cast<float*>(fsmem + kQSlots * kQUnit + kQW * kFWave);  // b3 | wo
+  float* prm = reinterpret_cast<float*>(fsmem + kQSlots * kQUnit + kQW * kFWave);  // b3 | wo | b1
   const int nit = p.rows.nit(blockIdx.x);
   const int KS = p.KS;
   const OutArgs& oa = p.oa;
   // knob "fused_prio" (timing A/B): the second-dispatched half of the waves at priority 1 (MI355X_MICROARCH.md,
   // two waves per SIMD item 4)
   if (p.prio && w >= kQW / 2) __builtin_amdgcn_s_setprio(1);
-#if RMX_FUSED_DIAG
+#if RMX_FUSED_DIAG & 1
   if (blockIdx.x == 0) {
     f_stamp(&g_fused_clk[w][0], lane, __builtin_amdgcn_s_memtime());
     f_stamp(&g_fused_clk[w][1], lane, __builtin_amdgcn_s_memrealtime());
   }
 #endif
 
-  for (int i = tid; i < kFPrm; i += kQThreads) {
+  for (int i = tid; i < 2 * kQN; i += kQThreads) {
     const int a = i / kQN, n = i - a * kQN;
     const float* src = a == 0 ? p.b3 : oa.wo;
     prm[i] = src ? src[n] : 0.f;
   }
+  // (a separate loop: a third source in the select above hit "illegal VGPR to SGPR copy" in the compiler)
+  for (int i = tid; i < kQN; i += kQThreads) prm[2 * kQN + i] = p.b1[i];
   int lo = (lane >> 2) * 32 + swz_slot(lane >> 2, lane & 3) * 8;
   asm volatile("" : "+v"(lo));
   const int fb = q_fbase(lane);
@@ -351,6 +394,8 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
 #pragma unroll 1
     for (int c = 0; c < KS; ++c, ++s) {
       q_enter<5>();  // previous unit: (c - 1, half 1) or the previous row block's last layer-3 unit, 5 DMAs
+      // step s + 1's ids landed two steps ago (its id DMA rode step s - 2; every q_enter since waited for it)
+      const FRowIds nid = f_row_ids(wl, s + 1, lane);
       prep(s);
       const int u = 2 * c;
       int dslot = slot == 0 ? 2 : slot - 1;
@@ -360,9 +405,9 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       const int sn = s;
       auto extra = [&](int t) {
         if (t == 6) id_dma(sn + 3);
-        if (t == 8) f_row_dma(p, wl, sn + 1, lane, 0);
-        if (t == 10) f_row_dma(p, wl, sn + 1, lane, 1);
-        if (t == 11) f_row_dma(p, wl, sn + 1, lane, 2);
+        if (t == 8) f_row_dma_ids(p, wl, sn + 1, lane, nid, 0);
+        if (t == 10) f_row_dma_ids(p, wl, sn + 1, lane, nid, 1);
+        if (t == 11) f_row_dma_ids(p, wl, sn + 1, lane, nid, 2);
       };
       q_unit<kQUT, 0, kQNT, 2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo, true,
                                    extra);
@@ -389,18 +434,19 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       pre = y1 + 0.5f * (a / 16.0f);
     }
     asm volatile("" : "+v"(pre));  // (formed here: sunk to the head, its 16 shuffled terms were spilled)
-    // h1 = ReLU(acc1 + b1), in place
+    // h1 = ReLU(acc1 + b1), in place (b1 from LDS)
     {
-      const float* b1 = p.b1;
-      asm volatile("" : "+s"(b1));
+      int o = 4 * g;
+      asm volatile("" : "+v"(o));
 #pragma unroll
-      for (int t = 0; t < kQNT; ++t) h1[t] = relu4(h1[t] + f_sbias(b1, t, g));
+      for (int t = 0; t < kQNT; ++t) h1[t] = relu4(h1[t] + *reinterpret_cast<const f32x4*>(prm + 2 * kQN + 16 * t + o));
     }
     // ---- layer 2: units (c, half 0), (c, half 1); h1 tiles 2c, 2c + 1 die after step c ----
     F_STAMP(it, 2);
     f32x4 h2[kQNT];
 #pragma unroll
     for (int t = 0; t < kQNT; ++t) h2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int sb2 = s;  // (b2 goes to A slot (sb2 - 1) & 1: f_b2_dma)
 #pragma unroll
     for (int c = 0; c < kFKS2; ++c) {
       q_enter<5>();
@@ -408,10 +454,17 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
       split3(h1[2 * c], 2 * c + 1 < kQNT ? h1[2 * c + 1] : z, ah, am, al);
       int dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQUT, 0, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
-                                           dslot, w, lo);
+      // unit (0, half 0) also DMAs b2 into this wave's free A slot, at its last tile (after the 5 plane DMAs)
+      auto b2x = [&](int t) {
+        if (c == 0 && t == kQUT - 1) f_b2_dma(p, wl, sb2, lane);
+      };
+      q_unit<kQUT, 0, kQNT, RMX_FUSED_PF2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
+                                                dslot, w, lo, true, b2x);
       slot = q_next(slot);
-      q_enter<5>();
+      if (c == 0)
+        q_enter<7>();  // 5 plane DMAs + the 2 of b2
+      else
+        q_enter<5>();
       dslot = slot == 0 ? 2 : slot - 1;
       q_unit<kQNT - kQUT, kQUT, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
                                                      lds, dslot, w, lo);
@@ -419,10 +472,13 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     }
     __builtin_amdgcn_sched_barrier(0);
     {
-      const float* b2 = p.b2;
-      asm volatile("" : "+s"(b2));
+      // b2 from this wave's A slot (its DMA landed units ago: every later q_enter waited for it)
+      // (the lane id made afresh by mbcnt: kept from the kernel's start, lane & 48 was spilled to scratch)
+      const int ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      int o = ((sb2 - 1) & 1) * 2048 + 16 * (ln >> 4);
+      asm volatile("" : "+v"(o));
 #pragma unroll
-      for (int t = 0; t < kQNT; ++t) h2[t] = relu4(h2[t] + f_sbias(b2, t, g));
+      for (int t = 0; t < kQNT; ++t) h2[t] = relu4(h2[t] + *reinterpret_cast<const f32x4*>(wl + o + 64 * t));
     }
     // ---- layer 3 + the output dot ----
     F_STAMP(it, 3);
@@ -434,8 +490,11 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     // ---- head: the four lane groups' columns, then bias, CAddTable, sigmoid (out_finish_kernel's order) ----
     part += __shfl_xor(part, 16);
     part += __shfl_xor(part, 32);
-    const int m = row0 + w * 16 + r16;
-    if (g == 0 && m < p.M) {
+    // (lane made afresh, as for b2: the kernel-start r16 was spilled here, and its reload waited vmcnt(0) --
+    // for every DMA in flight, the next row block's first units included)
+    const int ln = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int m = row0 + w * 16 + (ln & 15);
+    if (ln < 16 && m < p.M) {
       float y = part;
       if (oa.has_bo) y = y + oa.bo;
       float tt = pre + y;
@@ -446,7 +505,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   // the ring's trailing DMAs (units 0 / 1 of a row block that does not exist, the next block's ids / rows)
   // land before the block's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if RMX_FUSED_DIAG
+#if RMX_FUSED_DIAG & 1
   if (blockIdx.x == 0) {
     f_stamp(&g_fused_clk[w][2], lane, __builtin_amdgcn_s_memtime());
     f_stamp(&g_fused_clk[w][3], lane, __builtin_amdgcn_s_memrealtime());
@@ -456,7 +515,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
 
 }  // namespace
 
-#if RMX_FUSED_DIAG
+#if RMX_FUSED_DIAG & 1
 // out: [8 waves][4 row blocks][6 stamps] then [8 waves][4] (memtime, memrealtime at start and end)
 extern "C" int rmx_diag_fused(unsigned long long* out) {
   RMX_HIP(hipDeviceSynchronize());

@@ -95,33 +95,3 @@ def test_lr_forward_v2_bit_exact(ctx):
         res.append(out.numpy().copy())
     assert np.array_equal(res[0], res[1]) and np.array_equal(res[0], res[2])
 
-
-@pytest.mark.parametrize("F", [1, 7, 39, 40, 41, 83])
-@pytest.mark.parametrize("B", [1, 1000, 65537])
-def test_encoder_line8_bit_exact(ctx, F, B):
-    """Round 6: line tables on encoder_line8_kernel (8 lanes per sample, one whole-line load per id; knob
-    enc_line8 1 = 20 fields per batch, 2 = 40, 0 = encoder_k16v2_kernel): bitwise the row table's v2 result and
-    the oracle's first order + FM."""
-    V = 50000
-    ids = oc.gen_ids(SEED_IDS, 5, B, F, V)
-    wt, et = oc.gen_table(SEED_TAB, V, K)
-    ids_dev = rmx.DeviceArray.from_numpy(ctx, ids.astype(np.int32))
-    m = rmx.DeepFM(V, F, K, [32])
-    rows = rmx.EmbeddingTable(ctx, V, K)
-    rows.upload(wt, et)
-    ref_dev = _encode(ctx, m, rows, B, ids_dev, 20)
-    rmx.set_tuning("table_lines", 1)
-    lines = rmx.EmbeddingTable(ctx, V, K)
-    lines.upload(wt, et)
-    try:
-        for l8 in (0, 1, 2):
-            rmx.set_tuning("enc_line8", l8)
-            got = _encode(ctx, m, lines, B, ids_dev, 20)
-            assert np.array_equal(got, ref_dev), l8
-    finally:
-        rmx.set_tuning("enc_line8", None)
-    n = min(B, 4096)
-    w, e = oc.gather(wt, et, 1, ids[:n * F].astype(np.int64))
-    index = np.repeat(np.arange(n, dtype=np.int64), F)
-    ref = (oc.first_order(n, index, w) + oc.fm(n, F, K, e)).astype(np.float32)
-    assert np.array_equal(ref_dev[:n], ref)

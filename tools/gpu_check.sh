@@ -98,7 +98,16 @@ for s in $STEPS; do
                done
              done
            done ;;
+    ab:*) spec=${s#ab:}; wl=${spec%%:*}; libs=${spec#*:}; libs=${libs//,/ }   # ab:<workload>:tree,<vbuild name>,...
+         for round in 1 2 3; do
+           for L in $libs; do
+             if [ $L = tree ]; then LIB=recommendation-models_amd/csrc/librmx.so; else LIB=vbuild/$L/librmx.so; fi
+             run ab_${wl}_${L}_$round 200 env RMX_LIB=$LIB python bench.py --workload $wl --steps 200 --warmup 20 --no-companion --no-encoder-record --no-la-record --no-cpu-baseline || exit $?
+             python3 -c "import json; d=json.loads([l for l in open('$OUT/ab_${wl}_${L}_$round.log') if l.startswith('{')][-1]); print('$wl $L round $round', round(d['value']/1e6,2), 'M', d['ms_per_step'], {k: v['avg_ms'] for k, v in d['stages'].items()})" | tee -a $OUT/ab.txt
+           done
+         done ;;
     fdiag) run fdiag 300 env RMX_LIB=vbuild/fdiag/librmx.so python tools/diag_fused.py ;;
+    fdiag:*) v=${s#fdiag:}; run fdiag_$v 300 env RMX_LIB=vbuild/$v/librmx.so python tools/diag_fused.py ;;
     list) run list 120 rocprofv3 -L ;;
     ablines) run ab_lines1 300 python bench.py --no-companion --no-cpu-baseline --steps 200 &&
          run ab_lines0 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 &&

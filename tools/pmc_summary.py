@@ -67,7 +67,7 @@ def stage_of(kernel, workload=""):
             return "tower_layer1"
         return "tower_layer3" if epi == 1 else "tower_layer2"
     kernel = re.sub(r"^\(anonymous namespace\)::", "", kernel)
-    for pat, st in (("encoder_k16v2_kernel", "encoder"), ("encoder_line8_kernel", "encoder"), ("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
+    for pat, st in (("encoder_k16v2_kernel", "encoder"), ("encoder_k16_kernel<1", "encoder_fm"), ("encoder_k16_kernel<0", "first_order"),
                     ("encoder_k16_kernel<2", "first_order_sigmoid"), ("product16_kernel", "product"),
                     ("product_kernel", "product"), ("cross16_kernel", "cross"), ("cross_kernel", "cross"),
                     ("owner_gather", "shard_exchange"), ("own_rows_kernel", "shard_exchange"),
