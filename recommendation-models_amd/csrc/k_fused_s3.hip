@@ -62,9 +62,9 @@ static_assert(sizeof(float) * kQN <= 2048, "b2 fits a wave's free A slot (f_b2_d
 #endif
 
 // Diagnostic builds only (tools/diag_fused.py; never set in librmx.so): bit 1 s_memtime stamps of block 0's
-// waves at the layer boundaries of its first row blocks, s_memrealtime at the kernel's start and end (the
-// clock); timing probes with wrong results: bit 2 layer 1's row gathers from a fixed (cached) address, bit 4
-// no row / weight gathers in layer 1 at all
+// waves at the layer boundaries of its first row blocks and at every layer-1 unit of row block 1, s_memrealtime
+// at the kernel's start and end (the clock); timing probes with wrong results: bit 2 layer 1's row gathers
+// from a fixed (cached) address, bit 4 no row / weight gathers in layer 1 at all
 #ifndef RMX_FUSED_DIAG
 #define RMX_FUSED_DIAG 0
 #endif
@@ -72,18 +72,26 @@ static_assert(sizeof(float) * kQN <= 2048, "b2 fits a wave's free A slot (f_b2_d
 constexpr int kFDiagIt = 4, kFDiagPh = 6;
 __device__ unsigned long long g_fused_t[kQW][kFDiagIt][kFDiagPh];  // [wave][row block][phase]
 __device__ unsigned long long g_fused_clk[kQW][4];                   // memtime / memrealtime at start, end
+__device__ unsigned long long g_fused_u[kQW][2 * kFMaxF];            // row block 1's layer-1 units, at entry
 // one lane's vector store (the value and the address depend on the lane: never a scalar-cache store)
 __device__ __forceinline__ void f_stamp(unsigned long long* dst, int lane, unsigned long long v) {
   int l = lane;
   asm volatile("" : "+v"(l), "+v"(v));
   if (l == 0) dst[l] = v;
 }
+#define F_USTAMP(it, u)                                                                                  \
+  do {                                                                                                   \
+    if (blockIdx.x == 0 && (it) == 1) f_stamp(&g_fused_u[w][u], lane, __builtin_amdgcn_s_memtime());     \
+  } while (0)
 #define F_STAMP(it, ph)                                                                                  \
   do {                                                                                                   \
     if (blockIdx.x == 0 && (it) < kFDiagIt) f_stamp(&g_fused_t[w][it][ph], lane, __builtin_amdgcn_s_memtime()); \
   } while (0)
 #else
 #define F_STAMP(it, ph) \
+  do {                  \
+  } while (0)
+#define F_USTAMP(it, u) \
   do {                  \
   } while (0)
 #endif
@@ -394,6 +402,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
 #pragma unroll 1
     for (int c = 0; c < KS; ++c, ++s) {
       q_enter<5>();  // previous unit: (c - 1, half 1) or the previous row block's last layer-3 unit, 5 DMAs
+      F_USTAMP(it, 2 * c);
       // step s + 1's ids landed two steps ago (its id DMA rode step s - 2; every q_enter since waited for it)
       const FRowIds nid = f_row_ids(wl, s + 1, lane);
       prep(s);
@@ -413,6 +422,7 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
                                    extra);
       slot = q_next(slot);
       q_enter<9>();  // previous unit: 1 id + 2 row + 1 weight + 5 plane DMAs
+      F_USTAMP(it, 2 * c + 1);
       dslot = slot == 0 ? 2 : slot - 1;
       q_unit<kQNT - kQUT, kQUT>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u + 1, 2), lds, dslot, w, lo);
       slot = q_next(slot);
@@ -516,11 +526,14 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
 }  // namespace
 
 #if RMX_FUSED_DIAG & 1
-// out: [8 waves][4 row blocks][6 stamps] then [8 waves][4] (memtime, memrealtime at start and end)
+// out: [8 waves][4 row blocks][6 stamps], [8 waves][4] (memtime, memrealtime at start and end), then
+// [8 waves][80] row block 1's layer-1 unit entries
 extern "C" int rmx_diag_fused(unsigned long long* out) {
   RMX_HIP(hipDeviceSynchronize());
   RMX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(g_fused_t)));
   RMX_HIP(hipMemcpyFromSymbol(out + sizeof(g_fused_t) / 8, HIP_SYMBOL(g_fused_clk), sizeof(g_fused_clk)));
+  RMX_HIP(hipMemcpyFromSymbol(out + (sizeof(g_fused_t) + sizeof(g_fused_clk)) / 8, HIP_SYMBOL(g_fused_u),
+                              sizeof(g_fused_u)));
   return RMX_OK;
 }
 #endif

@@ -46,12 +46,13 @@ while time.time() < t_end:
 m.forward_ids(t, B, ids, out)
 ctx.sync()
 NW, NIT, NPH = 8, 4, 6
-buf = (ctypes.c_ulonglong * (NW * NIT * NPH + NW * 4))()
+NU1 = 80
+buf = (ctypes.c_ulonglong * (NW * NIT * NPH + NW * 4 + NW * NU1))()
 fn = rmx._lib.lib.rmx_diag_fused
 fn.argtypes = [ctypes.c_void_p]
 assert fn(buf) == 0
 st = np.array(buf[:NW * NIT * NPH], dtype=np.int64).reshape(NW, NIT, NPH)
-clk = np.array(buf[NW * NIT * NPH:], dtype=np.int64).reshape(NW, 4)
+clk = np.array(buf[NW * NIT * NPH:NW * NIT * NPH + NW * 4], dtype=np.int64).reshape(NW, 4)
 ghz = (clk[:, 2] - clk[:, 0]) / ((clk[:, 3] - clk[:, 1]) / 100e6) / 1e9
 span = clk[:, 2] - clk[:, 0]
 print("%d warm forwards; block 0: kernel span %.0f cycles (wave 0), clock %.3f GHz (waves %.3f-%.3f)"
@@ -82,3 +83,14 @@ tot = [st[w, 1, 0] - st[w, 0, 0] for w in range(NW) if st[w, 1, 0]]
 if tot:
     fl = sum(floor.values())
     print("row block 0 -> 1, whole: mean %.0f cycles, MFMA floor %d (eff %.3f)" % (np.mean(tot), fl, fl / np.mean(tot)))
+
+u = np.array(buf[NW * NIT * NPH + NW * 4:], dtype=np.int64).reshape(NW, NU1)
+nu = 2 * KS
+ends = np.concatenate([u[:, 1:nu], st[:, 1, 1:2]], axis=1)  # unit k ends at unit k + 1's entry (last: layer 1 end)
+d = ends - u[:, :nu]
+print("row block 1, layer-1 units (cycles, mean over waves; MFMA floor per unit %d / %d for half 0 / 1):"
+      % (13 * 6 * 2 * 16, 12 * 6 * 2 * 16))
+h0, h1 = d[:, 0::2].mean(axis=0), d[:, 1::2].mean(axis=0)
+print("  half 0: " + " ".join("%d" % x for x in h0))
+print("  half 1: " + " ".join("%d" % x for x in h1))
+print("  mean half 0 %.0f, half 1 %.0f" % (h0.mean(), h1.mean()))
