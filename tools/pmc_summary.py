@@ -35,12 +35,22 @@ def short(name):
     return name.replace("void ", "").replace("rmx::", "").replace("__bf16", "bf16")
 
 
-def load(d):
+def load(d, cin_layers=0):
+    """cin_layers L > 0: the CIN instantiation's dispatches are told apart by their order in each pass (one
+    forward runs L CIN layers back to back), so each CIN layer gets its own entry, '<kernel>#L<i>'."""
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        order = {}
+        if cin_layers:
+            cin = sorted({int(r["Dispatch_Id"]) for r in rows
+                          if re.search(r"gemm_kernel<Tile<[^>]*>, 3, ", short(r["Kernel_Name"]))})
+            order = {dsp: i % cin_layers for i, dsp in enumerate(cin)}
+        for r in rows:
             k = short(r["Kernel_Name"])
+            if int(r["Dispatch_Id"]) in order:
+                k = "%s#L%d" % (k, order[int(r["Dispatch_Id"])])
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))  # (once per counter row)
             if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
@@ -60,10 +70,14 @@ def stage_of(kernel, workload=""):
     if m:
         tile, amode, epi = m.group(1), int(m.group(2)), int(m.group(3))
         if amode == 3:
+            lm = re.search(r"#L(\d+)$", kernel)
+            if lm:
+                return ("cin_layer1", "cin_layer2", "cin_layer3+")[min(int(lm.group(1)), 2)]
             return "cin_layer"
         if amode in (1, 2):
             return "tower_layer1"
-        if workload.startswith("pnn") and epi == 0 and tile.startswith("1, 13, 8, 2"):
+        if workload.startswith("pnn") and epi == 0:
+            # (PNN's layers 2 and 3 run in the bf16 tail: its one stored dense-A GEMM is layer 1 over [x | ip])
             return "tower_layer1"
         return "tower_layer3" if epi == 1 else "tower_layer2"
     kernel = re.sub(r"^\(anonymous namespace\)::", "", kernel)
@@ -87,8 +101,9 @@ def main():
                     help="merge per-stage HBM bytes per launch into TRAFFIC_JSON under WORKLOAD")
     ap.add_argument("--batch", type=int, default=0, help="rows per launch of the profiled run")
     ap.add_argument("--source", default="", help="the committed summary file these counters are in (profiles/...)")
+    ap.add_argument("--cin-layers", type=int, default=0, help="CIN layers per forward (per-layer CIN entries)")
     a = ap.parse_args()
-    vals, dur, stats = load(a.dir)
+    vals, dur, stats = load(a.dir, a.cin_layers)
     out = {}
     for k in sorted(set(vals) | set(stats)):
         v = {c: sum(x) / len(x) for c, x in vals[k].items()}
