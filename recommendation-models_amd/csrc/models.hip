@@ -9,11 +9,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "rmx_models.hpp"
@@ -474,9 +472,6 @@ void model_release(rmx_model& m) {
   dev_free(m.la_w16);
   dev_free(m.la_rowptr);
   dev_free(m.la_out);
-  if (m.la_pin) (void)hipHostFree(m.la_pin);
-  m.la_pin = nullptr;
-  m.la_pin_cap = 0;
   for (auto& p : m.pending) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
@@ -896,72 +891,6 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
 // L-A: the reference's host-array contract.
 // Stages the L-A host arrays on the device (mats packed, E / w uploaded, irregular first order
 // precomputed) and describes them as one forward's inputs (implicit ids b*F + f).
-// L-A host arrays to HBM (round 6).  The caller's arrays are pageable (numpy; JNI GetPrimitiveArrayCritical on
-// the JVM heap), so hipMemcpyAsync copies them through the runtime's own staging on one host thread: at
-// B = 65,536 the gathered rows (174 MB) took 6.8 ms per call for 3.1 ms of DMA (bench.py models.deepfm_la).
-// Arrays of >= 4 MiB instead go through this model's pinned buffer: knob "la_pin_threads" host threads (default
-// 8; 0 = the runtime's path) copy 8-MiB chunks into it, and each chunk's DMA is queued as soon as its copy is
-// done, so the copies of chunk i + 1 run beside the DMA of chunk i.  The buffer is reused by the next call only
-// after this call's stream synchronisation (model_forward_host / rmx_backward end with one).  `off` places the
-// array in the buffer (several arrays per call).
-static int h2d_staged(rmx_model& m, void* dst, const void* src, size_t bytes, size_t off, size_t total,
-                      hipStream_t s) {
-  const int nthr = std::max(0, std::min(64, tuning_get("la_pin_threads", 8)));
-  if (bytes < ((size_t)4 << 20) || nthr == 0) {
-    RMX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
-    return RMX_OK;
-  }
-  if (total > m.la_pin_cap) {
-    RMX_HIP(hipStreamSynchronize(s));  // (a previous call's DMAs from the old buffer are long done; cheap)
-    if (m.la_pin) (void)hipHostFree(m.la_pin);
-    m.la_pin = nullptr;
-    m.la_pin_cap = 0;
-    // knob "la_pin_flags" (timing A/B): 0 hipHostMallocDefault, 1 non-coherent, 2 coherent
-    const int fl = tuning_get("la_pin_flags", 0);
-    const unsigned flags = fl == 1 ? hipHostMallocNonCoherent : (fl == 2 ? hipHostMallocCoherent : hipHostMallocDefault);
-    if (hipHostMalloc((void**)&m.la_pin, total, flags) != hipSuccess) {
-      m.la_pin = nullptr;
-      RMX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));  // (no pinned memory: the plain path)
-      return RMX_OK;
-    }
-    m.la_pin_cap = total;
-  }
-  constexpr size_t kChunk = (size_t)8 << 20;
-  const size_t nch = (bytes + kChunk - 1) / kChunk;
-  char* pin = m.la_pin + off;
-  std::vector<std::atomic<int>> done(nch);
-  for (auto& d : done) d.store(0);
-  auto work = [&](int t) {
-    for (size_t c = 0; c < nch; ++c) {
-      const size_t c0 = c * kChunk, cn = std::min(kChunk, bytes - c0);
-      const size_t per = (cn / nthr + 63) / 64 * 64;
-      const size_t a = std::min(cn, per * t), b = std::min(cn, per * (t + 1));
-      if (b > a) std::memcpy(pin + c0 + a, static_cast<const char*>(src) + c0 + a, b - a);
-      done[c].fetch_add(1, std::memory_order_release);
-    }
-  };
-  std::vector<std::thread> pool;
-  pool.reserve(nthr - 1);
-  for (int t = 1; t < nthr; ++t) pool.emplace_back(work, t);
-  // this thread copies slice 0 of each chunk, then queues the chunk's DMA once every slice is in
-  int st = RMX_OK;
-  for (size_t c = 0; c < nch; ++c) {
-    const size_t c0 = c * kChunk, cn = std::min(kChunk, bytes - c0);
-    const size_t per = (cn / nthr + 63) / 64 * 64;
-    const size_t b = std::min(cn, per);
-    if (b > 0) std::memcpy(pin + c0, static_cast<const char*>(src) + c0, b);
-    done[c].fetch_add(1, std::memory_order_release);
-    while (done[c].load(std::memory_order_acquire) < nthr) std::this_thread::yield();
-    if (st == RMX_OK && hipMemcpyAsync(static_cast<char*>(dst) + c0, pin + c0, cn, hipMemcpyHostToDevice, s) !=
-                            hipSuccess) {
-      set_error("L-A staging: hipMemcpyAsync from the pinned buffer failed");
-      st = RMX_E_HIP;
-    }
-  }
-  for (auto& th : pool) th.join();
-  return st;
-}
-
 int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, bool regular, bool sorted,
                      float bias, const float* weights, const float* embedding, const float* mats, FwdInputs* pin) {
   hipStream_t s = m.ctx->stream;
@@ -995,8 +924,10 @@ int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, boo
   // la_h2d: the gathered rows / weights (+ row pointers) to HBM; for bf16 models and irregular batches also
   // their rounding / the CSR first order that follows the copies
   StageTimer t_h2d(m, s, "la_h2d");
-  const size_t eb = m.type != RMX_MODEL_LR ? sizeof(float) * nnz * m.k : 0, wb = sizeof(float) * nnz;
-  if (eb > 0 && (st = h2d_staged(m, m.la_E, embedding, eb, 0, eb + wb, s))) return st;
+  // (the caller's pageable arrays go through the runtime's own staging copy: a pinned buffer filled by 1-16 host
+  // threads beside the chunks' DMAs measured slower at B = 4,096 and 65,536, profiles/r06/ab_la_staging.txt)
+  if (m.type != RMX_MODEL_LR && nnz > 0)
+    RMX_HIP(hipMemcpyAsync(m.la_E, embedding, sizeof(float) * nnz * m.k, hipMemcpyHostToDevice, s));
 
   const bool use_w = m.type != RMX_MODEL_DNN;
   const bool csr = use_w && (m.type == RMX_MODEL_LR || !regular);
@@ -1011,7 +942,7 @@ int model_stage_host(rmx_model& m, int B, int64_t nnz, const int64_t* index, boo
       for (int64_t n = 0; n < nnz; ++n) m.h_wperm[pos[(int32_t)index[n]]++] = weights[n];
       RMX_HIP(hipMemcpyAsync(m.la_w, m.h_wperm.data(), sizeof(float) * nnz, hipMemcpyHostToDevice, s));
     } else {
-      if ((st = h2d_staged(m, m.la_w, weights, wb, eb, eb + wb, s))) return st;
+      RMX_HIP(hipMemcpyAsync(m.la_w, weights, sizeof(float) * nnz, hipMemcpyHostToDevice, s));
     }
   }
   if (m.precision == kBF16 && nnz > 0) {

@@ -135,8 +135,6 @@ struct rmx_model {
   int64_t la16_cap = 0;
   std::vector<int64_t> h_rowptr;
   std::vector<float> h_wperm;
-  char* la_pin = nullptr;                        // pinned staging of large L-A host arrays (models.hip h2d_staged)
-  size_t la_pin_cap = 0;
 
   rmx::TrainState* train = nullptr;          // backward (train.hip), created on first use
   struct LaGrad {                            // L-A backward staging (rmx_backward), grown on demand

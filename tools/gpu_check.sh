@@ -108,7 +108,6 @@ for s in $STEPS; do
          done ;;
     fdiag) run fdiag 300 env RMX_LIB=vbuild/fdiag/librmx.so python tools/diag_fused.py ;;
     fdiag:*) v=${s#fdiag:}; run fdiag_$v 300 env RMX_LIB=vbuild/$v/librmx.so python tools/diag_fused.py ;;
-    laab) run laab 300 python tools/la_ab.py 0:0 8:0 8:1 16:1 4:1 ;;
     list) run list 120 rocprofv3 -L ;;
     ablines) run ab_lines1 300 python bench.py --no-companion --no-cpu-baseline --steps 200 &&
          run ab_lines0 300 python bench.py --no-companion --no-cpu-baseline --steps 200 --set table_lines=0 &&
