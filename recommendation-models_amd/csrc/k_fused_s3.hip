@@ -112,6 +112,7 @@ struct FusedS3Args {
   const float* b3;
   OutArgs oa;             // wo [416], bo, beta, out
   int prio;
+  int dma_split;          // the two wave halves issue their DMAs at different tiles (knob "fused_dma_split")
 };
 
 // unit u of a row block -> its weight planes (wave-uniform)
@@ -250,7 +251,7 @@ __device__ __forceinline__ void f_b2_dma(const FusedS3Args& p, char* wl, int s, 
 
 // layer-3 half HF (column tiles 13 HF .. + 12; half 1 computes 12, tile 25 is padding): 13 units, one per
 // K step, unrolled so that h2's tiles 2c, 2c + 1 are static registers (k_tail_s3.hip q_layer3)
-template <int HF>
+template <int HF, int DOFF>
 __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const float* prm, f32x4 (&h2)[kQNT],
                                          int& slot, int w, int lane, int lo, int fb, float& part) {
   const int g = lane >> 4;
@@ -267,9 +268,9 @@ __device__ __forceinline__ void f_layer3(const FusedS3Args& p, char* lds, const 
     const char* ub = lds + slot * kQUnit;
     const bf16_t* src = f_src23(p, 2 * kFKS2 + HF * kFKS2 + c + 2);
     if constexpr (HF == 0)
-      q_unit<kQUT, 0, kQUT, RMX_FUSED_PF3>(ub, fb, ah, am, al, acc, src, lds, dslot, w, lo);
+      q_unit<kQUT, 0, kQUT, RMX_FUSED_PF3, kQN, DOFF>(ub, fb, ah, am, al, acc, src, lds, dslot, w, lo);
     else
-      q_unit<kQUT - 1, 0, kQUT, RMX_FUSED_PF3>(ub, fb, ah, am, al, acc, src, lds, dslot, w, lo);
+      q_unit<kQUT - 1, 0, kQUT, RMX_FUSED_PF3, kQN, DOFF>(ub, fb, ah, am, al, acc, src, lds, dslot, w, lo);
     slot = q_next(slot);
   }
   // the output dot over this half's columns: ReLU(acc + b3)[n] * wo[n], n = 16 (13 HF + t) + 4 g + q
@@ -344,6 +345,16 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   __syncthreads();  // prm staged; this wave's units 0 and 1 landed (q_enter's barrier covers the rest)
 
   int slot = 0, s = 0;
+  // Round 6: the two waves of a SIMD (w and w + 4) issue their DMAs at different tiles of each unit -- the
+  // first half at tiles 0 .. 4 (and layer 1's gathers at 6 .. 11), the second half at tiles 6 .. 10 (gathers
+  // at 0 .. 3) -- so an LDS-DMA issue that holds one wave for ~100-200 cycles meets the partner's MFMAs
+  // instead of the partner's own DMA issue.  The vector-memory instructions per unit are the same, so every
+  // static vmcnt holds.  Each half runs its own copy of the loop (LATE is a compile-time flag; knob
+  // "fused_dma_split", default on; 0: both halves at tiles 0 .. 4).
+  const bool late = w >= kQW / 2 && p.dma_split;
+  auto body = [&](auto LATE) {
+  constexpr bool kLate = decltype(LATE)::value != 0;
+  constexpr int kDoff = kLate ? 6 : 0;
   for (int it = 0; it < nit; ++it) {
     int row0, nw;
     p.rows.desc(blockIdx.x, it, row0, nw);
@@ -413,18 +424,19 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       // ahead of the unit's first MFMA (k_head_s3.hip's order) cost 2 % (0.3142-0.3162 vs 0.3088-0.3111 ms)
       const int sn = s;
       auto extra = [&](int t) {
-        if (t == 6) id_dma(sn + 3);
-        if (t == 8) f_row_dma_ids(p, wl, sn + 1, lane, nid, 0);
-        if (t == 10) f_row_dma_ids(p, wl, sn + 1, lane, nid, 1);
-        if (t == 11) f_row_dma_ids(p, wl, sn + 1, lane, nid, 2);
+        if (t == (kLate ? 0 : 6)) id_dma(sn + 3);
+        if (t == (kLate ? 1 : 8)) f_row_dma_ids(p, wl, sn + 1, lane, nid, 0);
+        if (t == (kLate ? 2 : 10)) f_row_dma_ids(p, wl, sn + 1, lane, nid, 1);
+        if (t == (kLate ? 3 : 11)) f_row_dma_ids(p, wl, sn + 1, lane, nid, 2);
       };
-      q_unit<kQUT, 0, kQNT, 2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo, true,
-                                   extra);
+      q_unit<kQUT, 0, kQNT, 2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo,
+                                          true, extra);
       slot = q_next(slot);
       q_enter<9>();  // previous unit: 1 id + 2 row + 1 weight + 5 plane DMAs
       F_USTAMP(it, 2 * c + 1);
       dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQNT - kQUT, kQUT>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u + 1, 2), lds, dslot, w, lo);
+      q_unit<kQNT - kQUT, kQUT, kQNT, 2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u + 1, 2), lds,
+                                                    dslot, w, lo);
       slot = q_next(slot);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -468,15 +480,15 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       auto b2x = [&](int t) {
         if (c == 0 && t == kQUT - 1) f_b2_dma(p, wl, sb2, lane);
       };
-      q_unit<kQUT, 0, kQNT, RMX_FUSED_PF2, kQN>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2), lds,
-                                                dslot, w, lo, true, b2x);
+      q_unit<kQUT, 0, kQNT, RMX_FUSED_PF2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 2),
+                                                       lds, dslot, w, lo, true, b2x);
       slot = q_next(slot);
       if (c == 0)
         q_enter<7>();  // 5 plane DMAs + the 2 of b2
       else
         q_enter<5>();
       dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQNT - kQUT, kQUT, kQNT, RMX_FUSED_PF2>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
+      q_unit<kQNT - kQUT, kQUT, kQNT, RMX_FUSED_PF2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h2, f_src23(p, 2 * c + 3),
                                                      lds, dslot, w, lo);
       slot = q_next(slot);
     }
@@ -493,9 +505,9 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
     // ---- layer 3 + the output dot ----
     F_STAMP(it, 3);
     float part = 0.f;
-    f_layer3<0>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    f_layer3<0, kDoff>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
     F_STAMP(it, 4);
-    f_layer3<1>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
+    f_layer3<1, kDoff>(p, lds, prm, h2, slot, w, lane, lo, fb, part);
     F_STAMP(it, 5);
     // ---- head: the four lane groups' columns, then bias, CAddTable, sigmoid (out_finish_kernel's order) ----
     part += __shfl_xor(part, 16);
@@ -512,6 +524,11 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       oa.out[m] = 1.0f / (1.0f + expf(-tt));
     }
   }
+  };
+  if (late)
+    body(std::integral_constant<int, 1>{});
+  else
+    body(std::integral_constant<int, 0>{});
   // the ring's trailing DMAs (units 0 / 1 of a row block that does not exist, the next block's ids / rows)
   // land before the block's LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -604,6 +621,7 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   p.b3 = L3.b;
   p.oa = oa;
   p.prio = tuning_get("fused_prio", 0);
+  p.dma_split = tuning_get("fused_dma_split", 1);
   hipLaunchKernelGGL(tower_fused_s3_kernel, dim3(grid), dim3(kQThreads), kFLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;

@@ -77,7 +77,9 @@ struct QNoExtra {
 // unit U + 2, one per tile.  The fragments of tile t + 2 are read while tile t's MFMAs run.  extra(t) may
 // issue more vector-memory instructions at tile t (after that tile's plane DMA): a caller's own DMAs spread
 // over the MFMA stream instead of issued ahead of it.
-template <int NT, int T0, int NA, int PF = 2, int PS = kQN, class X = QNoExtra>
+// DOFF: the tile that carries the unit's first weight DMA (the rest follow one per tile); kernels whose two
+// waves per SIMD issue their DMAs at different tiles pass it per wave half (k_fused_s3.hip)
+template <int NT, int T0, int NA, int PF = 2, int PS = kQN, int DOFF = RMX_QTAIL_DOFF, class X = QNoExtra>
 __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah, const bf16x8& am, const bf16x8& al,
                                        f32x4 (&acc)[NA], const bf16_t* dsrc, char* lds, int dslot, int w, int lo,
                                        bool mm = true, const X& extra = X()) {
@@ -93,8 +95,8 @@ __device__ __forceinline__ void q_unit(const char* ub, int fb, const bf16x8& ah,
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (t + PF < NT) ldb(t + PF, bq[(t + PF) % (PF + 1)]);
-    // DMA q rides tile RMX_QTAIL_DOFF + q * RMX_QTAIL_DSTRIDE
-    constexpr int kD0 = RMX_QTAIL_DOFF, kDS = RMX_QTAIL_DSTRIDE;
+    // DMA q rides tile DOFF + q * RMX_QTAIL_DSTRIDE
+    constexpr int kD0 = DOFF, kDS = RMX_QTAIL_DSTRIDE;
     static_assert(kD0 + (kQQ - 1) * kDS < kQUT - 1, "every unit (12 or 13 tiles) carries all its DMAs");
     if (t >= kD0 && (t - kD0) % kDS == 0 && (t - kD0) / kDS < kQQ && !(RMX_QTAIL_DIAG & 1))
       q_dma<PS>(dsrc, lds, dslot, w, (t - kD0) / kDS, lo);

@@ -147,7 +147,8 @@ struct rmx_model {
   //      ordered on the device by an event (rmx::ModelUse) ----
   std::mutex mu;
   hipStream_t ws_stream = nullptr;  // stream of the last call that used the workspace
-  hipEvent_t ws_fence = nullptr;    // recorded on it at the end of that call
+  hipEvent_t ws_fence = nullptr;    // recorded on it at the end of that call (or, lazy, at the hand-over)
+  bool ws_fence_lazy = false;       // the fence is not recorded yet: record it on ws_stream at the hand-over
 
   // ---- stage timing ----
   bool timing = false;
@@ -208,17 +209,35 @@ struct StreamUse {
   hipStream_t s;
   std::unique_lock<std::mutex> lk;
   int st = RMX_OK;
-  StreamUse(T& oo, hipStream_t ss) : o(oo), s(ss), lk(oo.mu) {
+  // The fence is recorded lazily (round 6, knob "lazy_fence") for calls on the object's own context stream:
+  // only when a later call arrives on another stream, on that context stream, under the lock -- it then
+  // follows every operation the previous call enqueued there, which is all the hand-over needs.  Recorded
+  // after every call, the marker sits between each pair of back-to-back launches.  A caller's own stream
+  // keeps the eager record: it may be destroyed before the next call, the context's stream cannot be (the
+  // object holds its context).
+  bool lazy;
+  StreamUse(T& oo, hipStream_t ss)
+      : o(oo), s(ss), lk(oo.mu),
+        lazy(oo.ctx && ss == oo.ctx->stream && tuning_get("lazy_fence", 0) != 0) {
     if (!o.ws_fence && hipEventCreateWithFlags(&o.ws_fence, hipEventDisableTiming) != hipSuccess) {
       o.ws_fence = nullptr;
       st = RMX_E_HIP;
-    } else if (o.ws_stream && o.ws_stream != s && hipStreamWaitEvent(s, o.ws_fence, 0) != hipSuccess) {
-      st = RMX_E_HIP;
+    } else if (o.ws_stream && o.ws_stream != s) {
+      if ((o.ws_fence_lazy && hipEventRecord(o.ws_fence, o.ws_stream) != hipSuccess) ||
+          hipStreamWaitEvent(s, o.ws_fence, 0) != hipSuccess)
+        st = RMX_E_HIP;
     }
     if (st) set_error("stream hand-over: HIP event create / wait failed");
   }
   ~StreamUse() {
-    if (o.ws_fence && hipEventRecord(o.ws_fence, s) == hipSuccess) o.ws_stream = s;
+    if (!o.ws_fence) return;
+    if (lazy) {
+      o.ws_stream = s;
+      o.ws_fence_lazy = true;
+    } else if (hipEventRecord(o.ws_fence, s) == hipSuccess) {
+      o.ws_stream = s;
+      o.ws_fence_lazy = false;
+    }
   }
 };
 typedef StreamUse<rmx_model> ModelUse;

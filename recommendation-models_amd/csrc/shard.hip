@@ -189,6 +189,7 @@ struct rmx_shard {
   std::mutex mu;
   hipStream_t ws_stream = nullptr;
   hipEvent_t ws_fence = nullptr;
+  bool ws_fence_lazy = false;  // (rmx::StreamUse)
 };
 
 namespace rmx {
