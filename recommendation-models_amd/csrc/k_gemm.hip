@@ -198,7 +198,7 @@ bool tower_fm_fusable(const DenseLayer& L, int M, const AGatherArgs* ga, bool su
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* ga, float* C, int ldc, Epi epi, const OutArgs* oa, const XColArgs* xc,
-                       const FmArgs* fm) {
+                       const FmArgs* fm, bool cols32) {
   if (M <= 0) return RMX_OK;
   if (fm && (epi != Epi::kReluStore || !tower_fm_fusable(L, M, ga, fm->sums != 0))) {
     set_error("gemm: the fused first order + FM needs a gathered split-GEMM layer 1");
@@ -275,8 +275,12 @@ int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A
     // fp32 layer on the bf16 matrix cores through the exact 3-way split (k_gemm_s3.hip)
     p.Wp = reinterpret_cast<const float*>(L.W3);
     p.Kpad = (L.Kpad / 16 + 1) / 2 * 32;
+    // cols32: DeepFM's column-split small-batch path (models.hip, knob "s3_cols") runs its dense-A layers on
+    // 32-column blocks
+    p.cols32 = cols32 && amode == kDenseA && L.Npad % 32 == 0 ? 1 : 0;
+    const int bn = p.cols32 ? 32 : kS3BN;
     int st = launch_tower_s3(s, p, amode, epi);
-    if (st == RMX_OK && epi == Epi::kOutput && L.Npad > kS3BN) st = launch_out_finish(s, M, L.Npad / kS3BN, *oa);
+    if (st == RMX_OK && epi == Epi::kOutput && L.Npad > bn) st = launch_out_finish(s, M, L.Npad / bn, *oa);
     return st;
   }
   switch (nt) {

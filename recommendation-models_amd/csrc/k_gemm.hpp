@@ -125,6 +125,7 @@ struct GemmArgs {
   float* xcol;         // kEpiRelu: raw extra columns n >= xn_main -> xcol[m * xld + n - xn_main] (DCN cross)
   int xn_main, xld;
   int prio;            // 1: the first half of the block's waves issue at raised priority (s_setprio)
+  int cols32;          // kPrecS3 dense A: 32-column blocks (small launch batches, k_gemm_s3.hip s3_cols)
   int nt_store;        // 1: stored activations use non-temporal stores (knob "gemm_nt_store")
   // DeepFM first order + FM fused into tower layer 1 (kGatherK16 + kPrecS3, column slice 0): the A
   // tiles that stream through LDS are the gathered field rows, so the FM sums ride along and

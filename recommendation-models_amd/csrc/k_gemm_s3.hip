@@ -203,6 +203,20 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   const int var = tuning_get("s3_tower", 1);
   p.prio = tuning_get("gemm_prio", 0);
   p.nt_store = tuning_get("gemm_nt_store", 0);
+  // p.cols32 (knob "s3_cols", round 6): 128-row x 32-column blocks for small launch batches.  The whole-tower
+  // kernel (k_small_s3.hip) streams every layer's split planes through EVERY block (3.67 MB per 16 samples);
+  // here each block streams 1/13 of a layer's planes and its 128 A rows come from the materialised x / h in
+  // L2 (the 13 column blocks of a row block run on one XCD: blockIdx.x = row block, and the grid's row-block
+  // count is a multiple of 8 at the batches that take it).  Same products in the same K order per output.
+  if (p.cols32 && amode == kDenseA) {
+    // knob "s3_cols_ring": LDS-DMA ring depth (2, 3 (default) or 4 stages of 22 KiB).  At B = 1,024 the
+    // layers took 0.0206 / 0.0153 / 0.0193 ms on 2 stages, 0.0168 / 0.0130 / 0.0172 on 3, 0.0166 / 0.0128 /
+    // 0.0169 on 4; 4 lost at B >= 4,096 (profiles/r06/ab_cols32.txt)
+    const int rg = tuning_get("s3_cols_ring", 3);
+    if (rg == 2) return launch_epi<Tile<1, 2, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
+    if (rg == 3) return launch_epi<Tile<1, 2, 8, 1, 1, 2, 3>, kPrecS3>(s, p, amode, epi);
+    return launch_epi<Tile<1, 2, 8, 1, 1, 2, 4>, kPrecS3>(s, p, amode, epi);
+  }
   if (var == 2) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 2, 0>, kPrecS3>(s, p, amode, epi);
   // 3: 16-row waves, a single-buffered 57 KiB stage, two blocks per CU (4 waves / SIMD)
   if (var == 3) return launch_epi<Tile<1, kS3NT, 8, 1, 1, 4, 1>, kPrecS3>(s, p, amode, epi);

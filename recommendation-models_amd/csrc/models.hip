@@ -601,12 +601,14 @@ int ensure_ws(rmx_model& m, int B) {
     if ((st = dev_alloc(&m.h[0], (size_t)B * maxN))) return st;
     if ((st = dev_alloc(&m.h[1], (size_t)B * maxN))) return st;
     // partial logits of an output layer run in column slices (k_gemm_s3.hip)
-    if ((st = dev_alloc(&m.opart, (size_t)B * (m.layers.back().Npad / 208 + 1)))) return st;
+    // (up to Npad / 16 slices: 208-column slices, or the 32-column blocks of small batches, s3_cols)
+    if ((st = dev_alloc(&m.opart, (size_t)B * (m.layers.back().Npad / 16 + 1)))) return st;
   }
   if ((st = dev_alloc(&m.y12, B))) return st;
   if ((st = dev_alloc(&m.pre2, B))) return st;
   if (m.dcn_fused && (st = dev_alloc(&m.xcol, (size_t)B * (m.cross_depth + 1)))) return st;
-  if (m.type == RMX_MODEL_PNN || (m.type != RMX_MODEL_LR && needs_gather_x(m))) {
+  if (m.type == RMX_MODEL_PNN || (m.type != RMX_MODEL_LR && needs_gather_x(m)) ||
+      (m.type == RMX_MODEL_DEEPFM && B <= tuning_get("s3_cols", kS3ColsMaxB))) {
     if ((st = dev_alloc(&m.xbuf, (size_t)B * xbuf_ld_max(m)))) return st;
   }
   if (!m.cin_layers.empty()) {
@@ -713,6 +715,44 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
     StageTimer t(m, s, "first_order_sigmoid");
     if (in.y1) return launch_sigmoid_out(s, B, in.y1, in.beta, in.out);
     return launch_encoder(s, 2, B, in.ids, nullptr, in.wtab, in.dtype, F, 0, nullptr, &in.beta, in.out, in.ld, in.wld);
+  }
+
+  // DeepFM fp32 at a small launch batch, column-split (round 6, knob "s3_cols" = the largest B that takes it):
+  // the encoder writes the gathered rows x (and y1 + y2), then each layer runs on 128-row x 32-column blocks
+  // that stream 1/13 of its split planes (k_gemm_s3.hip p.cols32), the output layer writing 13 partial logits
+  // that out_finish_kernel sums in order with the head
+  if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) && k == 16 &&
+      B <= tuning_get("s3_cols", kS3ColsMaxB) && m.xbuf && m.layers.size() >= 2 && m.layers[0].W3 && f32_split_enabled() &&
+      m.layers[0].Kpad == F * k) {
+    {
+      StageTimer t(m, s, "encoder_fm_x");
+      if ((st = launch_encoder(s, 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr, in.ld,
+                               in.wld, m.xbuf)))
+        return st;
+    }
+    OutArgs oa{};
+    oa.wo = m.wo;
+    oa.bo = m.bo;
+    oa.has_bo = m.has_bo ? 1 : 0;
+    oa.pre = m.y12;
+    oa.beta = in.beta;
+    oa.out = in.out;
+    oa.part = m.opart;
+    const float* A = m.xbuf;
+    int lda = F * k;
+    static const char* lnames[] = {"tower_layer1", "tower_layer2", "tower_layer3", "tower_layer4+"};
+    for (size_t i = 0; i < m.layers.size(); ++i) {
+      const bool last = i + 1 == m.layers.size();
+      const DenseLayer& L = m.layers[i];
+      float* C = m.h[i & 1];
+      StageTimer t(m, s, lnames[std::min<size_t>(i, 3)]);
+      if ((st = launch_tower_layer(s, L, B, A, lda, nullptr, C, L.Npad, last ? Epi::kOutput : Epi::kReluStore,
+                                   last ? &oa : nullptr, nullptr, nullptr, true)))
+        return st;
+      A = C;
+      lda = L.Npad;
+    }
+    return RMX_OK;
   }
 
   // DeepFM fp32 at a small launch batch: the whole tower + first order + FM + head in one launch, one block

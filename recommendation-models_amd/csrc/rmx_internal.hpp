@@ -118,7 +118,7 @@ struct FmArgs {
 
 int launch_tower_layer(hipStream_t s, const DenseLayer& L, int M, const float* A, int lda,
                        const AGatherArgs* gather, float* C, int ldc, Epi epi, const OutArgs* oa,
-                       const XColArgs* xc = nullptr, const FmArgs* fm = nullptr);
+                       const XColArgs* xc = nullptr, const FmArgs* fm = nullptr, bool cols32 = false);
 // true when launch_tower_layer(L, M, gather, kReluStore) computes the FmArgs outputs (sums: + FM)
 bool tower_fm_fusable(const DenseLayer& L, int M, const AGatherArgs* gather, bool sums);
 // true when gathered layer 1 runs a 2-deep ring tile whose DMAs also carry the first-order weights
@@ -197,6 +197,10 @@ bool dx_s3_usable(const DenseLayer& L, int ldx);
 // fp32 packed [n16][Npad][16] -> the three bf16 planes of the split GEMM (k_gemm_s3.hip)
 int launch_pack_split3(hipStream_t s, const float* Wp, int n16, int Npad, bf16_t* W3);
 int64_t split3_elems(int n16, int Npad);  // bf16 elements of W3
+// DeepFM's column-split small-batch path (models.hip, k_gemm_s3.hip p.cols32) up to this batch (knob "s3_cols"):
+// B = 1,024 17.8 -> 19.2 M examples/s, but slower than the whole-tower kernel from B = 4,096 on
+// (profiles/r06/ab_cols32.txt)
+constexpr int kS3ColsMaxB = 2048;
 bool f32_split_enabled();                 // rmx_set_tuning("f32_split") (default on)
 // partial logits [ny][M] -> head combination + sigmoid
 int launch_out_finish(hipStream_t s, int M, int ny, const OutArgs& oa);

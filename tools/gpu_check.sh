@@ -106,11 +106,18 @@ for s in $STEPS; do
              python3 -c "import json; d=json.loads([l for l in open('$OUT/ab_${wl}_${L}_$round.log') if l.startswith('{')][-1]); print('$wl $L round $round', round(d['value']/1e6,2), 'M', d['ms_per_step'], {k: v['avg_ms'] for k, v in d['stages'].items()})" | tee -a $OUT/ab.txt
            done
          done ;;
-    abset:*) spec=${s#abset:}; wl=${spec%%:*}; sets=${spec#*:}; sets=${sets//;/ }   # abset:<workload>:k=v;k=v,k2=v2;...
+    abset:*) spec=${s#abset:}; wl=${spec%%:*}; sets=${spec#*:}; sets=${sets//\// }   # abset:<workload>:k=v/k=v,k2=v2/...
          for round in 1 2 3; do
            for S in $sets; do
              run abset_${wl}_${S//[=,]/_}_$round 200 python bench.py --workload $wl --steps 200 --warmup 20 --no-companion --no-encoder-record --no-la-record --no-cpu-baseline --set "$S" || exit $?
              python3 -c "import json; d=json.loads([l for l in open('$OUT/abset_${wl}_${S//[=,]/_}_$round.log') if l.startswith('{')][-1]); print('$wl $S round $round', round(d['value']/1e6,2), 'M', d['ms_per_step'], {k: v['avg_ms'] for k, v in d['stages'].items()})" | tee -a $OUT/abset.txt
+           done
+         done ;;
+    bsweep:*) sets=${s#bsweep:}; sets=${sets//\// }   # bsweep:k=v/k2=v2 ... : small batches, each knob set
+         for B in 1024 4096 8192 16384; do
+           for S in $sets; do
+             run bsweep_${B}_${S//[=,]/_} 200 python bench.py --batch $B --no-companion --no-encoder-record --no-la-record --parity-only --steps 200 --warmup 10 --set "$S" || exit $?
+             python3 -c "import json; d=json.loads([l for l in open('$OUT/bsweep_${B}_${S//[=,]/_}.log') if l.startswith('{')][-1]); print('B $B $S', round(d['value']/1e6,2), 'M', d['ms_per_step'], {k: v['avg_ms'] for k, v in d['stages'].items()}, d['cpu_baseline']['parity_check']['max_abs_diff'])" | tee -a $OUT/bsweep.txt
            done
          done ;;
     fdiag) run fdiag 300 env RMX_LIB=vbuild/fdiag/librmx.so python tools/diag_fused.py ;;
