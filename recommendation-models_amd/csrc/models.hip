@@ -720,10 +720,12 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
   // DeepFM fp32 at a small launch batch, column-split (round 6, knob "s3_cols" = the largest B that takes it):
   // the encoder writes the gathered rows x (and y1 + y2), then each layer runs on 128-row x 32-column blocks
   // that stream 1/13 of its split planes (k_gemm_s3.hip p.cols32), the output layer writing 13 partial logits
-  // that out_finish_kernel sums in order with the head
+  // that out_finish_kernel sums in order with the head (layer 1 gathering its rows from the table instead of
+  // the encoder's x measured slower: 0.031 vs 0.013 + 0.017 ms at B = 1,024, profiles/r06/ab_cols32_gather.txt).
+  // Auto choice only: s3_small 0 (the per-layer paths) and 2 (the whole-tower kernel, below) both bypass it
   if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) && k == 16 &&
-      B <= tuning_get("s3_cols", kS3ColsMaxB) && m.xbuf && m.layers.size() >= 2 && m.layers[0].W3 && f32_split_enabled() &&
-      m.layers[0].Kpad == F * k) {
+      B <= tuning_get("s3_cols", kS3ColsMaxB) && tuning_get("s3_small", 1) == 1 && m.xbuf && m.layers.size() >= 2 &&
+      m.layers[0].W3 && f32_split_enabled() && m.layers[0].Kpad == F * k) {
     {
       StageTimer t(m, s, "encoder_fm_x");
       if ((st = launch_encoder(s, 1, B, in.ids, in.table, in.wtab, in.dtype, F, k, m.y12, nullptr, nullptr, in.ld,

@@ -175,6 +175,9 @@ for s in $STEPS; do
          run pmc_b${B}_grbm 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcb_$B/grbm" -o grbm -- $A &&
          run pmc_b${B}_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb_$B/fetch" -o fetch -- $A &&
          run pmc_b${B}_tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmcb_$B/tcc" -o tcc -- $A ;;
+    trb:*) B=${s#trb:}   # DeepFM at launch batch B: kernel trace only (per-kernel durations and gaps)
+         run trace_b$B 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trb_$B" -o k -- \
+            python3 bench.py --batch $B --steps 50 --warmup 5 --no-cpu-baseline --no-companion --no-encoder-record --no-la-record --settle-ms 0 ;;
     wgprobe) for dg in 0 1 2 4 6 0; do   # dW timing probes (wgrad_sq_kernel DG; results wrong by construction)
                run wgprobe_$dg 300 python bench.py --workload deepfm_train --steps 20 --warmup 5 --no-companion --set wgrad_diag=$dg || exit $?
              done ;;
