@@ -213,6 +213,12 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
     // layers took 0.0206 / 0.0153 / 0.0193 ms on 2 stages, 0.0168 / 0.0130 / 0.0172 on 3, 0.0166 / 0.0128 /
     // 0.0169 on 4; 4 lost at B >= 4,096 (profiles/r06/ab_cols32.txt)
     const int rg = tuning_get("s3_cols_ring", 3);
+    // knob "s3_cols_wm": waves (16 rows each) per block, 4 (default), 8 or 2.  At B = 1,024: 19.2 M examples/s
+    // on 8 (104 blocks), 22.9 M on 4 (208 blocks), 20.5 M on 2; at 2,048: 37.7 / 39.2 / 39.0 M
+    // (profiles/r06/ab_cols32_wm.txt)
+    const int wm = tuning_get("s3_cols_wm", 4);
+    if (wm == 4) return launch_epi<Tile<1, 2, 4, 1, 1, 2, 3>, kPrecS3>(s, p, amode, epi);
+    if (wm == 2) return launch_epi<Tile<1, 2, 2, 1, 1, 2, 3>, kPrecS3>(s, p, amode, epi);
     if (rg == 2) return launch_epi<Tile<1, 2, 8, 1, 1, 2, 2>, kPrecS3>(s, p, amode, epi);
     if (rg == 3) return launch_epi<Tile<1, 2, 8, 1, 1, 2, 3>, kPrecS3>(s, p, amode, epi);
     return launch_epi<Tile<1, 2, 8, 1, 1, 2, 4>, kPrecS3>(s, p, amode, epi);

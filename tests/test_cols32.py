@@ -31,9 +31,11 @@ def ctx():
 def _restore_knobs():
     yield
     rmx.set_tuning("s3_cols", None)
+    rmx.set_tuning("s3_cols_wm", None)
 
 
-def _forward(ctx, B, V, knob, poison=False):
+def _forward(ctx, B, V, knob, poison=False, wm=4):
+    rmx.set_tuning("s3_cols_wm", wm)
     rmx.set_tuning("s3_cols", knob)  # (before the model's workspace exists: it sizes x for the path)
     m = rmx.DeepFM(V, F, K, list(FC))
     m.setMats(m.initMats(SEED_MATS))
@@ -62,6 +64,9 @@ def test_cols32_matches_small_kernel_and_oracle(ctx, B):
     (a, a2), st, h_ids = _forward(ctx, B, V, 1 << 20, poison=True)
     assert "encoder_fm_x" in st and "tower_small" not in st, st
     assert np.array_equal(a, a2)
+    for wm in (8, 2):  # the other block heights: the same products in the same order per output
+        (w, _), _, _ = _forward(ctx, B, V, 1 << 20, wm=wm)
+        assert np.array_equal(a, w), wm
     (b, _), st0, _ = _forward(ctx, B, V, 0)
     assert "encoder_fm_x" not in st0
     assert float(np.abs(a - b).max()) <= 5e-6
