@@ -178,6 +178,7 @@ for s in $STEPS; do
     trb:*) B=${s#trb:}   # DeepFM at launch batch B: kernel trace only (per-kernel durations and gaps)
          run trace_b$B 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trb_$B" -o k -- \
             python3 bench.py --batch $B --steps 50 --warmup 5 --no-cpu-baseline --no-companion --no-encoder-record --no-la-record --settle-ms 0 ;;
+    graph) run probe_graph 300 python tools/probe_graph.py ;;
     wgprobe) for dg in 0 1 2 4 6 0; do   # dW timing probes (wgrad_sq_kernel DG; results wrong by construction)
                run wgprobe_$dg 300 python bench.py --workload deepfm_train --steps 20 --warmup 5 --no-companion --set wgrad_diag=$dg || exit $?
              done ;;
