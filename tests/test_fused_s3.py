@@ -161,10 +161,10 @@ def test_fused_tower_default_batch_rule(ctx, B, want):
 
 
 @pytest.mark.parametrize("B", [40000, 65536])
-@pytest.mark.parametrize("knob", ["fused_prio"])
+@pytest.mark.parametrize("knob", ["fused_prio", "fused_dma_split"])
 def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
-    """The schedule knobs move work, not arithmetic -- fused_prio (the second half of the waves at priority 1):
-    the same bits either way."""
+    """The schedule knobs move work, not arithmetic -- fused_prio (the second half of the waves at priority 1),
+    fused_dma_split (the halves' DMAs at different tiles): the same bits either way."""
     V = 50000
     m, mats, table, ids, out = _setup(ctx, B, V)
     vals = (0, 1)
