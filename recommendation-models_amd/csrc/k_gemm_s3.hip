@@ -209,7 +209,7 @@ int launch_tower_s3(hipStream_t s, GemmArgs& p, int amode, Epi epi) {
   // L2 (the 13 column blocks of a row block run on one XCD: blockIdx.x = row block, and the grid's row-block
   // count is a multiple of 8 at the batches that take it).  Same products in the same K order per output.
   if (p.cols32 && amode == kDenseA) {
-    // knob "s3_cols_ring": LDS-DMA ring depth (2, 3 (default) or 4 stages of 22 KiB).  At B = 1,024 the
+    // knob "s3_cols_ring" (the 8-wave blocks): LDS-DMA ring depth (2, 3 (default) or 4 stages of 22 KiB).  At B = 1,024 the
     // layers took 0.0206 / 0.0153 / 0.0193 ms on 2 stages, 0.0168 / 0.0130 / 0.0172 on 3, 0.0166 / 0.0128 /
     // 0.0169 on 4; 4 lost at B >= 4,096 (profiles/r06/ab_cols32.txt)
     const int rg = tuning_get("s3_cols_ring", 3);
