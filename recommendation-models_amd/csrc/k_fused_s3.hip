@@ -144,6 +144,16 @@ __device__ __forceinline__ const bf16_t* f_ahead(const FusedS3Args& p, int u, in
   return f_unit_src(p, v < p.NU ? v : v - p.NU);
 }
 
+// layer 1's unit (c, half) + 2 = (c + 1, half) of W1, or -- at the last K step -- layer 2's (0, half): W1 / W2
+// are held in SGPRs across the loop and selected (f_ahead indexed the kernel arguments by a run-time unit, a
+// scalar load whose lgkmcnt(0) wait also drained the unit's first LDS reads)
+__device__ __forceinline__ const bf16_t* f_ahead1(const bf16_t* W1, const bf16_t* W2, int c, int KS, int half) {
+  const bool l1 = c + 1 < KS;
+  const bf16_t* W = l1 ? W1 : W2;
+  const int cc = l1 ? c + 1 : 0;
+  return W + (int64_t)(cc * 3 * kQN + half * kQUT * 16) * 32;
+}
+
 // unit V (a compile-time constant after unrolling) of layers 2 + 3 (V < 52), or V - 52 of the next row block's
 // layer 1: a kernel-argument pointer made opaque at its use plus a constant offset -- formed from the
 // runtime KS, or hoisted out of the row-block loop, the 52 unit sources spilled (SGPRs into VGPR lanes)
@@ -408,6 +418,9 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       }
       split3(a0, a1, ah, am, al);
     };
+    const bf16_t* W1 = p.W1;
+    const bf16_t* W2 = p.W2;
+    asm volatile("" : "+s"(W1), "+s"(W2));  // (loaded once per row block, selected per unit)
     // (forming step s + 1's A at the end of step s's half-1 unit, before the barrier, measured the same:
     // 0.3086-0.3097 vs 0.3094-0.3098 ms, profiles/r05/ab_fused.txt -- not kept)
 #pragma unroll 1
@@ -417,7 +430,6 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
       // step s + 1's ids landed two steps ago (its id DMA rode step s - 2; every q_enter since waited for it)
       const FRowIds nid = f_row_ids(wl, s + 1, lane);
       prep(s);
-      const int u = 2 * c;
       int dslot = slot == 0 ? 2 : slot - 1;
       // the ids (3 steps ahead), rows and weights (1 step ahead) ride tiles 6, 8, 10, 11 of the unit's MFMA
       // stream, after its 5 plane DMAs: an LDS-DMA issue can hold its wave ~100-200 cycles, and four of them
@@ -429,13 +441,13 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
         if (t == (kLate ? 2 : 10)) f_row_dma_ids(p, wl, sn + 1, lane, nid, 1);
         if (t == (kLate ? 3 : 11)) f_row_dma_ids(p, wl, sn + 1, lane, nid, 2);
       };
-      q_unit<kQUT, 0, kQNT, 2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u, 2), lds, dslot, w, lo,
+      q_unit<kQUT, 0, kQNT, 2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead1(W1, W2, c, KS, 0), lds, dslot, w, lo,
                                           true, extra);
       slot = q_next(slot);
       q_enter<9>();  // previous unit: 1 id + 2 row + 1 weight + 5 plane DMAs
       F_USTAMP(it, 2 * c + 1);
       dslot = slot == 0 ? 2 : slot - 1;
-      q_unit<kQNT - kQUT, kQUT, kQNT, 2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead(p, u + 1, 2), lds,
+      q_unit<kQNT - kQUT, kQUT, kQNT, 2, kQN, kDoff>(lds + slot * kQUnit, fb, ah, am, al, h1, f_ahead1(W1, W2, c, KS, 1), lds,
                                                     dslot, w, lo);
       slot = q_next(slot);
     }
