@@ -360,8 +360,10 @@ __global__ __launch_bounds__(kQThreads, 1) void tower_fused_s3_kernel(FusedS3Arg
   // at 0 .. 3) -- so an LDS-DMA issue that holds one wave for ~100-200 cycles meets the partner's MFMAs
   // instead of the partner's own DMA issue.  The vector-memory instructions per unit are the same, so every
   // static vmcnt holds.  Each half runs its own copy of the loop (LATE is a compile-time flag; knob
-  // "fused_dma_split", default on; 0: both halves at tiles 0 .. 4).
-  const bool late = w >= kQW / 2 && p.dma_split;
+  // "fused_dma_split": 1 the second half late; 2 (default since late round 6) every wave late, i.e. layer 1's
+  // gathers at the head of each half-0 unit -- half a unit more lead on the row lines: configs[3]'s V = 100M
+  // partition +1.3 / +1.9 % on two boxes, V = 1M neutral, profiles/r06/ab_fused_dma2.txt; 0: every wave early).
+  const bool late = (w >= kQW / 2 && p.dma_split) || p.dma_split == 2;  // (2: every wave on the late tiles)
   auto body = [&](auto LATE) {
   constexpr bool kLate = decltype(LATE)::value != 0;
   constexpr int kDoff = kLate ? 6 : 0;
@@ -633,7 +635,7 @@ int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer&
   p.b3 = L3.b;
   p.oa = oa;
   p.prio = tuning_get("fused_prio", 0);
-  p.dma_split = tuning_get("fused_dma_split", 1);
+  p.dma_split = tuning_get("fused_dma_split", 2);
   hipLaunchKernelGGL(tower_fused_s3_kernel, dim3(grid), dim3(kQThreads), kFLds, s, p);
   RMX_HIP(hipGetLastError());
   return RMX_OK;

@@ -164,10 +164,11 @@ def test_fused_tower_default_batch_rule(ctx, B, want):
 @pytest.mark.parametrize("knob", ["fused_prio", "fused_dma_split"])
 def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
     """The schedule knobs move work, not arithmetic -- fused_prio (the second half of the waves at priority 1),
-    fused_dma_split (the halves' DMAs at different tiles): the same bits either way."""
+    fused_dma_split (0: every wave's DMAs at the early tiles, 1: the second half's late, 2: every wave's late):
+    the same bits either way."""
     V = 50000
     m, mats, table, ids, out = _setup(ctx, B, V)
-    vals = (0, 1)
+    vals = (0, 1, 2) if knob == "fused_dma_split" else (0, 1)
     res = {}
     try:
         for v in vals:
@@ -175,7 +176,8 @@ def test_fused_tower_schedule_knobs_bitwise(ctx, B, knob):
             res[v] = _fwd(ctx, m, table, B, ids, out, True)
     finally:
         rmx.set_tuning(knob, None)
-    assert np.array_equal(res[vals[0]], res[vals[1]])
+    for v in vals[1:]:
+        assert np.array_equal(res[vals[0]], res[v]), v
 
 
 @pytest.mark.parametrize("Fn", [1, 2, 7, 40])
