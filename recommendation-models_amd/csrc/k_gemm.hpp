@@ -557,20 +557,21 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       key = hc * 2 + pr;
     }
   };
-  auto cin_x0 = [&](int c16, float* xv) {  // the x0 scalars of chunk c16 (LDS)
-    int f, key;
+  // the x0 scalars of chunk c16 (LDS) and its u-slice key, decoded once: the step that uses them reads the
+  // key from here instead of decoding the chunk again at its head (a chunk-map LDS read, or div_f, ahead of
+  // the A generation)
+  auto cin_x0 = [&](int c16, float* xv, int& key) {
+    int f;
     cin_chunk(c16, f, key);
 #pragma unroll
     for (int i = 0; i < MT; ++i) xv[i] = c16 * 16 < p.K ? extra[arow[i] * p.XS + f] : 0.f;
   };
-  auto cin_a_x = [&](int h, int c16, const float* xv, f32x4* a) {
+  auto cin_a_x = [&](int h, int c16, const float* xv, int key, f32x4* a) {
     if (c16 * 16 >= p.K) {
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       return;
     }
-    int f, key;
-    cin_chunk(c16, f, key);
     if (key != cur_hc[h]) load_u(h, key);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -578,11 +579,14 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
   };
   auto cin_a = [&](int h, int c16, f32x4* a) {
     float xv[MT];
-    cin_x0(c16, xv);
-    cin_a_x(h, c16, xv, a);
+    int key;
+    cin_x0(c16, xv, key);
+    cin_a_x(h, c16, xv, key, a);
   };
-  // kPrecS3: the x0 scalars of the next K step, read during this step's MFMAs (x0 is static in LDS)
+  // kPrecS3: the x0 scalars (and u-slice keys) of the next K step, read during this step's MFMAs (x0 is
+  // static in LDS)
   float x0q[2][MT];
+  int kq[2] = {0, 0};
 
   // kPrecS3: one 32-wide K step c.  Lane group g holds, at bf16 position 4h + q of its fragment,
   // K index 16h + 4g + q of the step (fp32 chunk 2c + h, slot g) -- the order W3 is packed in.
@@ -606,11 +610,11 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       if constexpr (WRING) wsum(c);
     } else {
       if (c == 0) {
-        cin_x0(0, x0q[0]);
-        cin_x0(1, x0q[1]);
+        cin_x0(0, x0q[0], kq[0]);
+        cin_x0(1, x0q[1], kq[1]);
       }
-      cin_a_x(0, 2 * c, x0q[0], a0);
-      cin_a_x(1, 2 * c + 1, x0q[1], a1);
+      cin_a_x(0, 2 * c, x0q[0], kq[0], a0);
+      cin_a_x(1, 2 * c + 1, x0q[1], kq[1], a1);
     }
     RMX_TMARK(3);  // 3: A fragments (LDS reads / CIN generation)
     bf16x8 ah[MT], am[MT], al[MT];
@@ -652,8 +656,8 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
       if (t + 1 < kIPW) dpre(t + 1);
       if constexpr (!A_LDS)
         if (t == 0) {
-          cin_x0(2 * c + 2, x0q[0]);
-          cin_x0(2 * c + 3, x0q[1]);
+          cin_x0(2 * c + 2, x0q[0], kq[0]);
+          cin_x0(2 * c + 3, x0q[1], kq[1]);
         }
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this tile's MFMAs
       const f32x4* b = bq[t % (PF + 1)];
@@ -1027,13 +1031,13 @@ __global__ __launch_bounds__(T::NTHR, T::OCC) void gemm_kernel(GemmArgs p) {
           if constexpr (WRING) wsum(c);
         } else {
           if (c == 0) {
-            cin_x0(0, x0q[0]);
-            cin_x0(1, x0q[1]);
+            cin_x0(0, x0q[0], kq[0]);
+            cin_x0(1, x0q[1], kq[1]);
           }
-          cin_a_x(0, 2 * c, x0q[0], a0);
-          cin_a_x(1, 2 * c + 1, x0q[1], a1);
-          cin_x0(2 * c + 2, x0q[0]);
-          cin_x0(2 * c + 3, x0q[1]);
+          cin_a_x(0, 2 * c, x0q[0], kq[0], a0);
+          cin_a_x(1, 2 * c + 1, x0q[1], kq[1], a1);
+          cin_x0(2 * c + 2, x0q[0], kq[0]);
+          cin_x0(2 * c + 3, x0q[1], kq[1]);
         }
 #pragma unroll
         for (int i = 0; i < MT; ++i) split3(a0[i], a1[i], ah[i], am[i], al[i]);
