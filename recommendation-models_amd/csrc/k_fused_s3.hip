@@ -579,20 +579,12 @@ bool tower_fused_s3_usable(const DenseLayer& L1, const DenseLayer& L2, const Den
         L3.bias_mode == 1))
     return false;
   if (!L1.b || !L2.b) return false;
-  // knob "s3_fused": 0 off (head + tail), 2 always, 1 (default) when at least one round of full 128-row blocks
-  // fills every CU (B >= 32,768 on 256 CUs): at B = 16,384 (one round of 64-row half blocks) head + tail ran
-  // 154.4 M against the fused tower's 147.7 M; at 32,768 / 49,152 the fused tower wins, 201.1 / 189.0 M against
-  // 190.3 / 184.0 M (profiles/r05/ab_fused_batch.txt)
-  const int knob = tuning_get("s3_fused", 1);
-  if (knob == 0) return false;
-  if (knob == 2) return true;
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    ncu = 256;
-  int grid = 0;
-  const QRows r = q_rows(M, ncu, grid);
-  return grid >= ncu && r.nfull >= ncu;
+  // knob "s3_fused": 0 off (head + tail), 1 (default) / 2 on.  Round 5 kept it to batches whose full 128-row
+  // blocks fill every CU (B = 16,384: head + tail 154.4 M against the fused tower's 147.7 M then,
+  // profiles/r05/ab_fused_batch.txt); after round 6's fused-tower work it wins at every batch the small-batch
+  // kernels leave to it (they take B <= 8,192 first): B = 9,216 / 12,288 / 16,384 / 24,576 107 / 142 / 173 / 180 M
+  // against head + tail's 90 / 119 / 152 / 157 M (profiles/r06/ab_fused_mid_batches.txt)
+  return tuning_get("s3_fused", 1) != 0;
 }
 
 int launch_tower_fused_s3(hipStream_t s, const DenseLayer& L1, const DenseLayer& L2, const DenseLayer& L3, int M, int F,

@@ -144,11 +144,11 @@ def test_fused_tower_is_the_default_at_the_bench_batch(ctx):
     assert list(stages) == ["tower_fused"], stages
 
 
-@pytest.mark.parametrize("B,want", [(16384, ["tower_layer1", "tower_tail"]), (32768, ["tower_fused"]),
-                                    (49152, ["tower_fused"])])
+@pytest.mark.parametrize("B,want", [(8192, ["tower_small"]), (9216, ["tower_fused"]), (16384, ["tower_fused"]),
+                                    (32768, ["tower_fused"]), (49152, ["tower_fused"])])
 def test_fused_tower_default_batch_rule(ctx, B, want):
-    """knob s3_fused 1 (default) takes the fused tower once a round of full 128-row blocks fills the CUs
-    (B >= 32,768 on 256 CUs); below, head + tail with their half blocks (measured faster at B = 16,384)."""
+    """knob s3_fused 1 (default) takes the fused tower at every batch the small-batch kernels leave to it (they
+    take B <= 8,192 on 256 CUs): since round 6 it beats head + tail from B = 9,216 up (107 vs 90 M there)."""
     V = 50000
     m, mats, table, ids, out = _setup(ctx, B, V)
     for k in ("s3_fused", "s3_head", "s3_tail", "s3_small"):
