@@ -216,7 +216,9 @@ __device__ void s_wave(const SmallArgs& p, float* ssmem, int tid, int w, int lan
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
       const int i = tid + u * kSThreads, r = i / F, m = m0 + r;
-      iv[u] = *((i < kSR * F && m < p.M) ? p.ids + (int64_t)m * F + (i - r * F) : neg1);
+      const bool ok = i < kSR * F && m < p.M;
+      // (ids == nullptr: the L-A path's staged rows, id = m F + f)
+      iv[u] = p.ids ? *(ok ? p.ids + (int64_t)m * F + (i - r * F) : neg1) : (ok ? m * F + (i - r * F) : -1);
     }
 #pragma unroll
     for (int u = 0; u < NP; ++u)

@@ -759,7 +759,8 @@ int model_forward(rmx_model& m, hipStream_t s, const FwdInputs& in) {
 
   // DeepFM fp32 at a small launch batch: the whole tower + first order + FM + head in one launch, one block
   // per 16 samples (k_small_s3.hip; knob "s3_small")
-  if (m.type == RMX_MODEL_DEEPFM && in.ids && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) &&
+  // (also the L-A path's staged rows, in.ids == nullptr: the kernel forms id = b F + f)
+  if (m.type == RMX_MODEL_DEEPFM && !in.y1 && in.dtype == kF32 && !needs_gather_x(m) &&
       tower_small_s3_usable(m, B, F, k, true)) {
     StageTimer t(m, s, "tower_small");
     OutArgs oa{};
